@@ -1,0 +1,24 @@
+# Builds libdmip.so (gfx950) in-tree. Used by __graft_entry__.build(); `make -j2` by hand.
+PKG := diffusion-modelling-for-inverse-problems_amd
+CSRC := $(PKG)/csrc
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-parameter
+OBJS := $(CSRC)/dmip_kernels.o $(CSRC)/dmip_capi.o
+HDRS := $(CSRC)/dmip_device.h $(CSRC)/dmip_internal.h include/dmip.h
+
+all: $(PKG)/libdmip.so
+
+$(CSRC)/dmip_kernels.o: $(CSRC)/dmip_kernels.hip $(HDRS)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(CSRC)/dmip_capi.o: $(CSRC)/dmip_capi.cpp $(HDRS)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(PKG)/libdmip.so: $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(OBJS) -o $@
+
+clean:
+	rm -f $(OBJS) $(PKG)/libdmip.so
+
+.PHONY: all clean

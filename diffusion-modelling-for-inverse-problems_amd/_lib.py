@@ -1,0 +1,154 @@
+"""ctypes binding of libdmip.so (include/dmip.h).
+
+The library is built in-tree (Makefile / __graft_entry__.build()) next to this file. It must be
+loaded AFTER `import torch` so that it binds to the HIP runtime torch already loaded (both carry
+SONAME libamdhip64.so.7; the dynamic loader then reuses torch's copy and device pointers and
+streams are shared). There is no fallback: if the library is missing, every device entry point
+raises.
+"""
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("DMIP_LIB", os.path.join(_HERE, "libdmip.so"))
+
+DMIP_OK, DMIP_ERR_INVALID, DMIP_ERR_UNSUPPORTED, DMIP_ERR_HIP, DMIP_ERR_ALLOC = range(5)
+DMIP_INPUT_X_Y_T, DMIP_INPUT_X_T = 0, 1
+DMIP_ACT_TANH_TWICE_FIRST, DMIP_ACT_TANH = 0, 1
+DMIP_PREC_BF16 = 0
+
+# every symbol include/dmip.h declares (checked by tests/test_capi.py)
+EXPORTED = (
+    "dmip_mlp_create", "dmip_mlp_destroy", "dmip_mlp_forward", "dmip_em_sample", "dmip_rng_words",
+    "dmip_rng_normals", "dmip_schedule", "dmip_last_error", "dmip_abi_version", "dmip_sampler_supported",
+)
+
+
+class DmipVpsde(ctypes.Structure):
+    _fields_ = [("beta_min", ctypes.c_double), ("beta_max", ctypes.c_double), ("T", ctypes.c_double)]
+
+
+_c_void_p = ctypes.c_void_p
+_i32, _i64, _u64 = ctypes.c_int, ctypes.c_int64, ctypes.c_uint64
+_f32 = ctypes.c_float
+
+_lib = None
+_lock = threading.Lock()
+calls = {"em_sample": 0, "mlp_forward": 0}  # instrumentation: proves the HIP path ran
+
+
+def _declare(lib):
+    lib.dmip_last_error.restype = ctypes.c_char_p
+    lib.dmip_abi_version.restype = _i32
+    lib.dmip_sampler_supported.argtypes = [_i32, _i32, _i32]
+    lib.dmip_mlp_create.argtypes = [_i32, _i32, _i32, ctypes.POINTER(_i32), _i32, _i32, _i32,
+                                    ctypes.POINTER(_c_void_p), ctypes.POINTER(_c_void_p),
+                                    ctypes.POINTER(_c_void_p)]
+    lib.dmip_mlp_destroy.argtypes = [_c_void_p]
+    lib.dmip_mlp_forward.argtypes = [_c_void_p, _c_void_p, _c_void_p, _i64, _c_void_p, _i32, _i64,
+                                     _c_void_p, _i32, _c_void_p]
+    lib.dmip_em_sample.argtypes = [_c_void_p, ctypes.POINTER(DmipVpsde), _c_void_p, _i32, _i32, _i32,
+                                   _i64, _i64, _i32, _f32, _f32, _u64, _i32, _c_void_p, _c_void_p,
+                                   _c_void_p]
+    lib.dmip_rng_words.argtypes = [_u64, _i64, _u64, _i64, _i32, _c_void_p, _c_void_p]
+    lib.dmip_rng_normals.argtypes = [_u64, _i64, _u64, _i64, _i32, _c_void_p, _c_void_p]
+    lib.dmip_schedule.argtypes = [_i32, ctypes.POINTER(DmipVpsde), _c_void_p, _c_void_p]
+    for name in ("dmip_mlp_create", "dmip_mlp_destroy", "dmip_mlp_forward", "dmip_em_sample",
+                 "dmip_rng_words", "dmip_rng_normals", "dmip_schedule", "dmip_sampler_supported"):
+        getattr(lib, name).restype = _i32
+
+
+def lib():
+    """The loaded library; raises RuntimeError if it has not been built."""
+    global _lib
+    if _lib is None:
+        with _lock:
+            if _lib is None:
+                if not os.path.exists(LIB_PATH):
+                    raise RuntimeError(
+                        f"dmip: HIP library not found at {LIB_PATH}; build it with "
+                        "`python -c 'import __graft_entry__ as g; g.build()'` or `make` at the repo root")
+                handle = ctypes.CDLL(LIB_PATH)
+                _declare(handle)
+                _lib = handle
+    return _lib
+
+
+def check(rc):
+    if rc == DMIP_OK:
+        return
+    msg = lib().dmip_last_error().decode(errors="replace")
+    if rc in (DMIP_ERR_INVALID, DMIP_ERR_UNSUPPORTED):
+        raise ValueError(f"dmip: {msg}")
+    raise RuntimeError(f"dmip: {msg} (status {rc})")
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def stream_of(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def require_device(t, what="tensor"):
+    if not (isinstance(t, torch.Tensor) and t.is_cuda):
+        raise RuntimeError(f"dmip: {what} must be on a HIP device (got {getattr(t, 'device', type(t))});"
+                           " the dmip kernels have no CPU path")
+
+
+def vpsde(beta_min, beta_max, T):
+    return DmipVpsde(float(beta_min), float(beta_max), float(T))
+
+
+class MlpHandle:
+    """Owns a dmip_mlp* (packed device weights) for one snapshot of a network's parameters."""
+
+    def __init__(self, layers, in_dim, out_dim, xdim, input_layout, device):
+        L = len(layers) - 1
+        widths = (_i32 * L)(*[int(layers[i][0].shape[0]) for i in range(L)])
+        with torch.cuda.device(device):
+            ws = [w.detach().float().contiguous().cpu() for w, _ in layers]
+            bs = [b.detach().float().contiguous().cpu() for _, b in layers]
+            wp = (_c_void_p * (L + 1))(*[w.data_ptr() for w in ws])
+            bp = (_c_void_p * (L + 1))(*[b.data_ptr() for b in bs])
+            out = _c_void_p()
+            check(lib().dmip_mlp_create(in_dim, out_dim, L, widths, DMIP_ACT_TANH_TWICE_FIRST,
+                                        input_layout, xdim, wp, bp, ctypes.byref(out)))
+        self.h = out
+        self.device = device
+        self.width = int(layers[0][0].shape[0])
+        self.n_hidden = L
+        self.in_dim, self.out_dim, self.xdim = in_dim, out_dim, xdim
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h and _lib is not None:
+            try:
+                torch.cuda.synchronize(self.device)
+            except Exception:
+                pass
+            _lib.dmip_mlp_destroy(h)
+            self.h = None
+
+
+def mlp_forward(handle, x, y, t, out, y_stride, t_stride):
+    calls["mlp_forward"] += 1
+    check(lib().dmip_mlp_forward(handle.h, ptr(x), ptr(y), y_stride, ptr(t), t_stride, x.shape[0],
+                                 ptr(out), DMIP_PREC_BF16, stream_of(x.device)))
+
+
+def em_sample(handle, sde, y, n_chains, chain_offset, num_steps, mean, std, seed, out, noise=None):
+    calls["em_sample"] += 1
+    n_y, ydim = y.shape
+    check(lib().dmip_em_sample(handle.h, ctypes.byref(sde), ptr(y), n_y, ydim, handle.xdim,
+                               int(n_chains), int(chain_offset), int(num_steps), float(mean),
+                               float(std), ctypes.c_uint64(int(seed) & 0xFFFFFFFFFFFFFFFF),
+                               DMIP_PREC_BF16, ptr(noise), ptr(out), stream_of(y.device)))
+
+
+def sampler_supported(width, n_hidden, xdim):
+    return bool(lib().dmip_sampler_supported(width, n_hidden, xdim))

@@ -1,0 +1,367 @@
+// libdmip.so C-ABI (include/dmip.h): handle management, host-side weight packing into the
+// kernels' MFMA fragment layouts, argument validation, stream-ordered launches.
+//
+// Packing conventions (shared with dmip_kernels.hip):
+//   * One 1 KiB fragment block = 64 lanes x 8 bf16, the A operand of one
+//     v_mfma_f32_32x32x16_bf16: lane l = i + 32h holds A[row i][k = 8h + j], j = 0..7.
+//   * Hidden layer k-order: the B operand is the previous layer's accumulator registers, so
+//     element j of lane half h in k-step s is hidden unit kperm(s, h, j) (see below).
+//   * r-form activations: kernels carry r = 1/(1+exp(2z)) = (1 - tanh z)/2, so the next layer
+//     uses weights -2W and bias b + sum_k W; pre-activations of tanh layers are scaled by
+//     c = 2 log2(e) (exp2 instead of exp).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/dmip.h"
+#include "dmip_internal.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+  return fail(DMIP_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+constexpr double kC = 2.8853900817779268;  // 2 log2(e)
+
+uint16_t f2bf(float f) {  // round to nearest even (inputs are finite)
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+float bf2f(uint16_t b) {
+  uint32_t u = (uint32_t)b << 16;
+  float f;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
+
+inline int kperm(int s, int h, int j) { return 32 * (s >> 1) + 16 * (s & 1) + 8 * (j >> 2) + 4 * h + (j & 3); }
+inline int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+inline int k1s_for(int n_slots) { return (n_slots + 15) / 16; }
+
+template <typename T>
+int upload(T** dst, const std::vector<T>& src) {
+  *dst = nullptr;
+  if (src.empty()) return DMIP_OK;
+  hipError_t e = hipMalloc((void**)dst, src.size() * sizeof(T));
+  if (e != hipSuccess) return fail(DMIP_ERR_ALLOC, std::string("hipMalloc: ") + hipGetErrorString(e));
+  e = hipMemcpy(*dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice);
+  if (e != hipSuccess) return hip_fail(e, "hipMemcpy");
+  return DMIP_OK;
+}
+
+}  // namespace
+
+struct dmip_mlp {
+  int in_dim = 0, out_dim = 0, n_hidden = 0, width = 0, act_mode = 0, layout = 0, xdim = 0;
+  int k1s_full = 0;
+  char* hidden = nullptr;         // [(L-1)][W/32][W/16] KiB
+  char* ao_samp = nullptr;        // [W/16] KiB, output rows duplicated into lanes 32-63
+  char* ao_full = nullptr;        // [W/16] KiB, natural output rows
+  float* bias_hidden = nullptr;   // [(L-1)][W/32][2][16]
+  float* bias_out_samp = nullptr; // [2][16]
+  float* bias_out_full = nullptr; // [2][16]
+  char* a1_full = nullptr;        // [W/32][k1s_full] KiB (every input column varying)
+  float* w1 = nullptr;            // layer-1 fp32 [W][in_dim] (per-y prep of the sampler's A1)
+  float* b1 = nullptr;
+  ~dmip_mlp() {
+    for (void* p : {(void*)hidden, (void*)ao_samp, (void*)ao_full, (void*)bias_hidden, (void*)bias_out_samp,
+                    (void*)bias_out_full, (void*)a1_full, (void*)w1, (void*)b1})
+      if (p) (void)hipFree(p);
+  }
+};
+
+extern "C" {
+
+const char* dmip_last_error(void) { return g_err.c_str(); }
+
+int dmip_abi_version(void) { return DMIP_ABI_VERSION; }
+
+int dmip_sampler_supported(int width, int n_hidden, int xdim) {
+  return dmip::sampler_shape_supported(width, n_hidden, xdim) ? 1 : 0;
+}
+
+int dmip_mlp_create(int in_dim, int out_dim, int n_hidden, const int* widths, int act_mode, int input_layout,
+                    int xdim, const float* const* weights, const float* const* biases, dmip_mlp** out) {
+  if (!out || !widths || !weights || !biases) return fail(DMIP_ERR_INVALID, "null argument");
+  *out = nullptr;
+  if (n_hidden < 1) return fail(DMIP_ERR_INVALID, "n_hidden must be >= 1");
+  const int W = widths[0];
+  for (int i = 1; i < n_hidden; ++i)
+    if (widths[i] != W) return fail(DMIP_ERR_UNSUPPORTED, "hidden widths must all be equal");
+  if (W % 32 != 0 || W < 32) return fail(DMIP_ERR_UNSUPPORTED, "hidden width must be a multiple of 32");
+  if (out_dim < 1 || out_dim > 32) return fail(DMIP_ERR_UNSUPPORTED, "out_dim must be in [1, 32]");
+  if (act_mode != DMIP_ACT_TANH_TWICE_FIRST)
+    return fail(DMIP_ERR_UNSUPPORTED, "only the reference activation chain (tanh twice on layer 1) is compiled");
+  if (input_layout != DMIP_INPUT_X_Y_T && input_layout != DMIP_INPUT_X_T)
+    return fail(DMIP_ERR_INVALID, "unknown input layout");
+  if (xdim < 1 || xdim + 1 > in_dim) return fail(DMIP_ERR_INVALID, "xdim inconsistent with in_dim");
+  if (input_layout == DMIP_INPUT_X_T && in_dim != xdim + 1)
+    return fail(DMIP_ERR_INVALID, "X_T layout needs in_dim == xdim + 1");
+  for (int i = 0; i <= n_hidden; ++i)
+    if (!weights[i] || !biases[i]) return fail(DMIP_ERR_INVALID, "null layer pointer");
+
+  dmip_mlp* net = new (std::nothrow) dmip_mlp;
+  if (!net) return fail(DMIP_ERR_ALLOC, "host allocation");
+  net->in_dim = in_dim;
+  net->out_dim = out_dim;
+  net->n_hidden = n_hidden;
+  net->width = W;
+  net->act_mode = act_mode;
+  net->layout = input_layout;
+  net->xdim = xdim;
+  const int T = W / 32, KS = W / 16, L = n_hidden;
+
+  // ---- hidden W x W layers: A = bf16(-2c W), init = c b - 0.5 sum_k A
+  std::vector<uint16_t> hid((size_t)(L - 1) * T * KS * 512);
+  std::vector<float> bh((size_t)(L - 1) * T * 32);
+  for (int li = 0; li < L - 1; ++li) {
+    const float* Wl = weights[li + 1];
+    const float* bl = biases[li + 1];
+    std::vector<uint16_t> A((size_t)W * W);
+    std::vector<float> init(W);
+    for (int r = 0; r < W; ++r) {
+      double acc = 0.0;
+      for (int k = 0; k < W; ++k) {
+        const uint16_t a = f2bf((float)(-2.0 * kC * (double)Wl[(size_t)r * W + k]));
+        A[(size_t)r * W + k] = a;
+        acc += (double)bf2f(a);
+      }
+      init[r] = (float)(kC * (double)bl[r] - 0.5 * acc);
+    }
+    for (int rt = 0; rt < T; ++rt)
+      for (int s = 0; s < KS; ++s)
+        for (int l = 0; l < 64; ++l)
+          for (int j = 0; j < 8; ++j) {
+            const int i = l & 31, h = l >> 5;
+            hid[(((size_t)(li * T + rt) * KS + s) * 64 + l) * 8 + j] = A[(size_t)(rt * 32 + i) * W + kperm(s, h, j)];
+          }
+    for (int rt = 0; rt < T; ++rt)
+      for (int h = 0; h < 2; ++h)
+        for (int r = 0; r < 16; ++r) bh[((size_t)(li * T + rt) * 2 + h) * 16 + r] = init[rt * 32 + acc_row(r, h)];
+  }
+
+  // ---- output layer: A = bf16(-2 W), init = b - 0.5 sum_k A (no tanh scale: raw drift a)
+  const float* Wo = weights[L];
+  const float* bo = biases[L];
+  std::vector<uint16_t> Ao((size_t)out_dim * W);
+  std::vector<float> init_o(out_dim);
+  for (int d = 0; d < out_dim; ++d) {
+    double acc = 0.0;
+    for (int k = 0; k < W; ++k) {
+      const uint16_t a = f2bf((float)(-2.0 * (double)Wo[(size_t)d * W + k]));
+      Ao[(size_t)d * W + k] = a;
+      acc += (double)bf2f(a);
+    }
+    init_o[d] = (float)((double)bo[d] - 0.5 * acc);
+  }
+  std::vector<uint16_t> ao_s((size_t)KS * 512, 0), ao_f((size_t)KS * 512, 0);
+  std::vector<float> bo_s(32, 0.0f), bo_f(32, 0.0f);
+  for (int s = 0; s < KS; ++s)
+    for (int l = 0; l < 64; ++l)
+      for (int j = 0; j < 8; ++j) {
+        const int i = l & 31, h = l >> 5;
+        const int ds = i < 4 ? i : (i < 8 ? i - 4 : -1);  // sampler: rows 0-3 duplicated at 4-7
+        if (ds >= 0 && ds < out_dim) ao_s[((size_t)s * 64 + l) * 8 + j] = Ao[(size_t)ds * W + kperm(s, h, j)];
+        if (i < out_dim) ao_f[((size_t)s * 64 + l) * 8 + j] = Ao[(size_t)i * W + kperm(s, h, j)];
+      }
+  for (int h = 0; h < 2; ++h)
+    for (int r = 0; r < 16; ++r) {
+      const int row = acc_row(r, h);
+      const int ds = row < 4 ? row : (row < 8 ? row - 4 : -1);
+      if (ds >= 0 && ds < out_dim) bo_s[h * 16 + r] = init_o[ds];
+      if (row < out_dim) bo_f[h * 16 + r] = init_o[row];
+    }
+
+  // ---- layer 1, forward variant: every column varying, split bf16 [hi | hi | lo | b_hi | b_lo]
+  const float* W1 = weights[0];
+  const float* b1 = biases[0];
+  const int IN = in_dim;
+  net->k1s_full = k1s_for(3 * IN + 2);
+  const int K1S = net->k1s_full;
+  std::vector<uint16_t> a1f((size_t)T * K1S * 512, 0);
+  for (int jr = 0; jr < W; ++jr) {
+    const int rt = jr / 32, i = jr % 32;
+    for (int k = 0; k < K1S * 16; ++k) {
+      float val = 0.0f;
+      auto split = [&](double v, bool lo) {
+        const float f = (float)v;
+        const uint16_t hi = f2bf(f);
+        return lo ? bf2f(f2bf(f - bf2f(hi))) : bf2f(hi);
+      };
+      if (k < IN) val = split(kC * W1[(size_t)jr * IN + k], false);
+      else if (k < 2 * IN) val = split(kC * W1[(size_t)jr * IN + k - IN], false);
+      else if (k < 3 * IN) val = split(kC * W1[(size_t)jr * IN + k - 2 * IN], true);
+      else if (k == 3 * IN) val = split(kC * b1[jr], false);
+      else if (k == 3 * IN + 1) val = split(kC * b1[jr], true);
+      const int s = k / 16, hh = (k % 16) / 8, jj = k % 8;
+      a1f[(((size_t)(rt * K1S + s)) * 64 + i + 32 * hh) * 8 + jj] = f2bf(val);
+    }
+  }
+
+  int rc = DMIP_OK;
+  std::vector<char> hid_b(hid.size() * 2), ao_sb(ao_s.size() * 2), ao_fb(ao_f.size() * 2), a1f_b(a1f.size() * 2);
+  std::memcpy(hid_b.data(), hid.data(), hid_b.size());
+  std::memcpy(ao_sb.data(), ao_s.data(), ao_sb.size());
+  std::memcpy(ao_fb.data(), ao_f.data(), ao_fb.size());
+  std::memcpy(a1f_b.data(), a1f.data(), a1f_b.size());
+  std::vector<float> w1v(W1, W1 + (size_t)W * IN), b1v(b1, b1 + W);
+  if ((rc = upload(&net->hidden, hid_b)) || (rc = upload(&net->ao_samp, ao_sb)) || (rc = upload(&net->ao_full, ao_fb)) ||
+      (rc = upload(&net->bias_hidden, bh)) || (rc = upload(&net->bias_out_samp, bo_s)) ||
+      (rc = upload(&net->bias_out_full, bo_f)) || (rc = upload(&net->a1_full, a1f_b)) ||
+      (rc = upload(&net->w1, w1v)) || (rc = upload(&net->b1, b1v))) {
+    delete net;
+    return rc;
+  }
+  *out = net;
+  return DMIP_OK;
+}
+
+int dmip_mlp_destroy(dmip_mlp* net) {
+  delete net;
+  return DMIP_OK;
+}
+
+int dmip_mlp_forward(const dmip_mlp* net, const float* x_dev, const float* y_dev, int64_t y_stride,
+                     const float* t_dev, int t_stride, int64_t n, float* out_dev, int precision, void* stream) {
+  if (!net || !x_dev || !t_dev || !out_dev) return fail(DMIP_ERR_INVALID, "null argument");
+  if (precision != DMIP_PREC_BF16) return fail(DMIP_ERR_UNSUPPORTED, "unknown precision");
+  if (n < 0) return fail(DMIP_ERR_INVALID, "n < 0");
+  if (n == 0) return DMIP_OK;
+  const int ydim = net->layout == DMIP_INPUT_X_Y_T ? net->in_dim - net->xdim - 1 : 0;
+  if (ydim > 0 && !y_dev) return fail(DMIP_ERR_INVALID, "y required for an X_Y_T network");
+  if (ydim > 0 && y_stride != 0 && y_stride != ydim) return fail(DMIP_ERR_INVALID, "y_stride must be 0 or ydim");
+  if (t_stride != 0 && t_stride != 1) return fail(DMIP_ERR_INVALID, "t_stride must be 0 or 1");
+  dmip::ForwardParams p{};
+  p.hidden = net->hidden;
+  p.a1 = net->a1_full;
+  p.ao = net->ao_full;
+  p.bias_hidden = net->bias_hidden;
+  p.bias_out = net->bias_out_full;
+  p.x = x_dev;
+  p.y = y_dev;
+  p.t = t_dev;
+  p.out = out_dev;
+  p.n = n;
+  p.y_stride = y_stride;
+  p.t_stride = t_stride;
+  p.xdim = net->xdim;
+  p.ydim = ydim;
+  p.out_dim = net->out_dim;
+  bool ok = false;
+  hipError_t e = dmip::launch_forward(p, net->width, net->n_hidden, net->in_dim, (hipStream_t)stream, &ok);
+  if (!ok) return fail(DMIP_ERR_UNSUPPORTED, "no compiled forward kernel for width " + std::to_string(net->width) +
+                                                 ", layers " + std::to_string(net->n_hidden) + ", in_dim " +
+                                                 std::to_string(net->in_dim));
+  if (e != hipSuccess) return hip_fail(e, "mlp_forward launch");
+  return DMIP_OK;
+}
+
+int dmip_em_sample(const dmip_mlp* net, const dmip_vpsde* sde, const float* y_dev, int n_y, int ydim, int xdim,
+                   int64_t n_chains, int64_t chain_offset, int num_steps, float mean, float stdv, uint64_t seed,
+                   int precision, const float* noise_dev, float* x_out_dev, void* stream) {
+  if (!net || !sde || !y_dev || !x_out_dev) return fail(DMIP_ERR_INVALID, "null argument");
+  if (precision != DMIP_PREC_BF16) return fail(DMIP_ERR_UNSUPPORTED, "unknown precision");
+  if (net->layout != DMIP_INPUT_X_Y_T) return fail(DMIP_ERR_INVALID, "sampler needs an x,y,t network (CDE)");
+  if (xdim != net->xdim || net->out_dim != xdim) return fail(DMIP_ERR_INVALID, "xdim does not match the network");
+  if (ydim != net->in_dim - xdim - 1) return fail(DMIP_ERR_INVALID, "ydim does not match the network");
+  if (n_y < 1 || n_y > 65535) return fail(DMIP_ERR_INVALID, "n_y must be in [1, 65535]");
+  if (n_chains < 0 || chain_offset < 0) return fail(DMIP_ERR_INVALID, "negative chain count/offset");
+  if (num_steps < 1) return fail(DMIP_ERR_INVALID, "num_steps must be >= 1");
+  if (!(sde->T > 0.0)) return fail(DMIP_ERR_INVALID, "T must be > 0");
+  if (n_chains == 0) return DMIP_OK;
+  if (!dmip::sampler_shape_supported(net->width, net->n_hidden, xdim))
+    return fail(DMIP_ERR_UNSUPPORTED, "no compiled sampler for width " + std::to_string(net->width) + ", layers " +
+                                          std::to_string(net->n_hidden) + ", xdim " + std::to_string(xdim));
+  hipStream_t st = (hipStream_t)stream;
+  const int T = net->width / 32;
+  const int k1s = k1s_for(3 * (xdim + 1) + 2);
+  const size_t a1_bytes = (size_t)n_y * T * k1s * 1024;
+  char* a1 = nullptr;
+  hipError_t e = hipMallocAsync((void**)&a1, a1_bytes, st);
+  if (e != hipSuccess) return fail(DMIP_ERR_ALLOC, std::string("hipMallocAsync: ") + hipGetErrorString(e));
+
+  dmip::A1PrepParams ap{};
+  ap.w1 = net->w1;
+  ap.b1 = net->b1;
+  ap.y = y_dev;
+  ap.a1 = a1;
+  ap.width = net->width;
+  ap.in_dim = net->in_dim;
+  ap.xdim = xdim;
+  ap.ydim = ydim;
+  ap.y_col0 = xdim;
+  ap.t_col = net->in_dim - 1;
+  ap.k1s = k1s;
+  e = dmip::launch_a1_prep(ap, n_y, st);
+  if (e != hipSuccess) {
+    (void)hipFreeAsync(a1, st);
+    return hip_fail(e, "a1_prep launch");
+  }
+
+  dmip::SamplerParams p{};
+  p.hidden = net->hidden;
+  p.a1 = a1;
+  p.ao = net->ao_samp;
+  p.bias_hidden = net->bias_hidden;
+  p.bias_out = net->bias_out_samp;
+  p.noise = noise_dev;
+  p.x_out = x_out_dev;
+  p.n_chains = n_chains;
+  p.chain_offset = chain_offset;
+  p.num_steps = num_steps;
+  p.T = (float)sde->T;
+  p.bmin = (float)sde->beta_min;
+  p.bdiff = (float)(sde->beta_max - sde->beta_min);
+  p.delta = (float)(sde->T / (double)num_steps);
+  p.sqrt_delta = (float)std::sqrt(sde->T / (double)num_steps);
+  p.mean = mean;
+  p.stdv = stdv;
+  p.seed = seed;
+  bool ok = false;
+  e = dmip::launch_sampler(p, net->width, net->n_hidden, xdim, n_y, st, &ok);
+  (void)hipFreeAsync(a1, st);
+  if (!ok) return fail(DMIP_ERR_UNSUPPORTED, "no compiled sampler");
+  if (e != hipSuccess) return hip_fail(e, "em_sampler launch");
+  return DMIP_OK;
+}
+
+int dmip_rng_words(uint64_t seed, int64_t chain_offset, uint64_t stream_id, int64_t n_chains, int n_words,
+                   uint32_t* out_dev, void* stream) {
+  if (!out_dev || n_chains < 0 || n_words < 0) return fail(DMIP_ERR_INVALID, "bad argument");
+  if (n_chains == 0 || n_words == 0) return DMIP_OK;
+  hipError_t e = dmip::launch_rng_words(seed, chain_offset, stream_id, n_chains, n_words, out_dev, (hipStream_t)stream);
+  return e == hipSuccess ? DMIP_OK : hip_fail(e, "rng_words launch");
+}
+
+int dmip_rng_normals(uint64_t seed, int64_t chain_offset, uint64_t stream_id, int64_t n_chains, int n_pairs,
+                     float* out_dev, void* stream) {
+  if (!out_dev || n_chains < 0 || n_pairs < 0) return fail(DMIP_ERR_INVALID, "bad argument");
+  if (n_chains == 0 || n_pairs == 0) return DMIP_OK;
+  hipError_t e = dmip::launch_rng_normals(seed, chain_offset, stream_id, n_chains, n_pairs, out_dev, (hipStream_t)stream);
+  return e == hipSuccess ? DMIP_OK : hip_fail(e, "rng_normals launch");
+}
+
+int dmip_schedule(int num_steps, const dmip_vpsde* sde, float* out_dev, void* stream) {
+  if (!out_dev || !sde || num_steps < 1) return fail(DMIP_ERR_INVALID, "bad argument");
+  hipError_t e = dmip::launch_schedule(num_steps, (float)sde->T, (float)sde->beta_min,
+                                       (float)(sde->beta_max - sde->beta_min), out_dev, (hipStream_t)stream);
+  return e == hipSuccess ? DMIP_OK : hip_fail(e, "schedule launch");
+}
+
+}  // extern "C"

@@ -1,0 +1,173 @@
+// Device-side building blocks shared by the dmip kernels (gfx950 / CDNA4 only).
+//
+//  * MFMA fragment types for v_mfma_f32_32x32x16_bf16 (wave64, 32x32 f32 accumulator tile).
+//  * The per-chain counter-keyed RNG (splitmix64-seeded xoshiro128** + Box-Muller), restated
+//    bit-for-bit on the integer side by oracle/dmip_oracle.py (rng_init/rng_next/rng_normals).
+//  * The reverse-time schedule and VP-SDE coefficients with the reference's fp32 rounding
+//    (models/diffusion.py:31-42, sdes.py:21-35,77-87): every multiply/add is an explicit
+//    round-to-nearest intrinsic so the compiler cannot contract them into FMAs.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dmip {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// 2*log2(e): pre-activations are produced pre-scaled by this so tanh needs no extra multiply.
+constexpr float kTanhScale = 2.8853900817779268f;
+
+__device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// ------------------------------------------------------------------------------------ RNG
+struct Rng {
+  uint32_t s0, s1, s2, s3;
+};
+
+__device__ __forceinline__ uint64_t splitmix_next(uint64_t& st) {
+  st += 0x9E3779B97F4A7C15ull;
+  uint64_t z = st;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// Keyed by the GLOBAL chain index: identical draws however chains are split over
+// workgroups / GPUs.
+__device__ __forceinline__ Rng rng_init(uint64_t seed, uint64_t chain, uint64_t stream) {
+  uint64_t sm = seed + chain * 0xD1B54A32D192ED03ull + stream * 0x8CB92BA72F3D8DD7ull;
+  uint64_t z0 = splitmix_next(sm);
+  uint64_t z1 = splitmix_next(sm);
+  Rng r;
+  r.s0 = (uint32_t)z0;
+  r.s1 = (uint32_t)(z0 >> 32);
+  r.s2 = (uint32_t)z1;
+  r.s3 = (uint32_t)(z1 >> 32);
+  if ((r.s0 | r.s1 | r.s2 | r.s3) == 0u) r.s0 = 1u;
+  return r;
+}
+
+__device__ __forceinline__ uint32_t rotl32(uint32_t x, int k) { return (x << k) | (x >> (32 - k)); }
+
+__device__ __forceinline__ uint32_t rng_next(Rng& r) {
+  const uint32_t result = rotl32(r.s1 * 5u, 7) * 9u;
+  const uint32_t t = r.s1 << 9;
+  r.s2 ^= r.s0;
+  r.s3 ^= r.s1;
+  r.s1 ^= r.s2;
+  r.s0 ^= r.s3;
+  r.s2 ^= t;
+  r.s3 = rotl32(r.s3, 11);
+  return result;
+}
+
+// Box-Muller on 24-bit uniforms: u1 in (0,1] for the log, u2 in [0,1) in revolutions
+// (v_sin_f32 / v_cos_f32 take their argument in units of 2*pi).
+__device__ __forceinline__ void rng_normal_pair(Rng& r, float& n0, float& n1) {
+  const uint32_t a = rng_next(r);
+  const uint32_t b = rng_next(r);
+  const float u1 = 1.0f - (float)(a >> 8) * 0x1p-24f;
+  const float u2 = (float)(b >> 8) * 0x1p-24f;
+  const float rad = __fsqrt_rn(-1.3862943611198906f * __log2f(u1));  // sqrt(-2 ln u1)
+  n0 = rad * __builtin_amdgcn_cosf(u2);
+  n1 = rad * __builtin_amdgcn_sinf(u2);
+}
+
+template <int D>
+__device__ __forceinline__ void rng_normals(Rng& r, float (&n)[D]) {
+#pragma unroll
+  for (int p = 0; p < (D + 1) / 2; ++p) {
+    float a, b;
+    rng_normal_pair(r, a, b);
+    n[2 * p] = a;
+    if (2 * p + 1 < D) n[2 * p + 1] = b;
+  }
+}
+
+// ------------------------------------------------------------------------------ schedule
+// torch.linspace(0,1,S+1)[i] in fp32 (ATen CPU kernel: first half i*step, second half
+// 1-(S-i)*step with a single rounding) -- models/diffusion.py:34.
+__device__ __forceinline__ float linspace_at(int i, int S) {
+  const float step = __fdiv_rn(1.0f, (float)S);
+  if (i < (S + 1) / 2) return __fmul_rn((float)i, step);
+  return __fmaf_rn(-(float)(S - i), step, 1.0f);
+}
+
+struct StepCoef {
+  float tau;   // T - t_i, the time the net and coefficients see (sdes.py:78)
+  float beta;  // beta(T - t_i)                                    (sdes.py:21-22)
+  float g;     // sqrt(beta) (pow 0.5)                             (sdes.py:33-35)
+};
+
+__device__ __forceinline__ StepCoef step_coef(int i, int S, float T, float bmin, float bdiff) {
+  StepCoef c;
+  const float ts = __fmul_rn(linspace_at(i, S), T);
+  c.tau = __fsub_rn(T, ts);
+  c.beta = __fadd_rn(bmin, __fmul_rn(bdiff, c.tau));
+  c.g = __fsqrt_rn(c.beta);
+  return c;
+}
+
+// x <- fl(x + fl(delta*mu)) + fl(fl(sqrt(delta)*g)*xi),  mu = fl(g*a) - fl(fl(-0.5*beta)*x)
+// (models/diffusion.py:40-42 with sdes.py:77-79,86-87 at lambda = 0).
+__device__ __forceinline__ float em_update(float x, float a, float xi, const StepCoef& c,
+                                           float delta, float sqrt_delta) {
+  const float mu = __fsub_rn(__fmul_rn(c.g, a), __fmul_rn(__fmul_rn(-0.5f, c.beta), x));
+  const float drift = __fadd_rn(x, __fmul_rn(delta, mu));
+  return __fadd_rn(drift, __fmul_rn(__fmul_rn(sqrt_delta, c.g), xi));
+}
+
+// ---------------------------------------------------------------------------- activation
+// The kernels propagate r = 1/(1+exp(2z)) instead of tanh(z) = 1 - 2r; the "1 - 2r" is folded
+// into the next layer on the host (weights -2W, bias b + sum_k W). The pre-activation arrives
+// already multiplied by 2*log2(e), so one layer's activation is exp2 + add + rcp.
+__device__ __forceinline__ float act_r(float zs) {
+  return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(zs));
+}
+// tanh(tanh(z)) of the reference's first layer (nets.py:21-26 double Tanh) in r-form:
+// q = r(z); tanh(z) = 1 - 2q; r1 = r(2 log2e * (1 - 2q)).
+__device__ __forceinline__ float act_r_twice(float zs) {
+  const float q = act_r(zs);
+  return act_r(__builtin_fmaf(-2.0f * kTanhScale, q, kTanhScale));
+}
+
+template <bool TWICE>
+__device__ __forceinline__ void act_pack(const f32x16& acc, bf16x8& lo, bf16x8& hi) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float a = TWICE ? act_r_twice(acc[j]) : act_r(acc[j]);
+    const float b = TWICE ? act_r_twice(acc[8 + j]) : act_r(acc[8 + j]);
+    lo[j] = (__bf16)a;
+    hi[j] = (__bf16)b;
+  }
+}
+
+// ------------------------------------------------------------------------ sync primitives
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  // vmcnt = N (bits 3:0 and 15:14), expcnt = 7 and lgkmcnt = 15 (no wait on those)
+  __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+}
+
+__device__ __forceinline__ void lds_barrier() {
+  // all of this wave's LDS reads have returned, then a raw workgroup barrier. The asm memory
+  // clobbers keep the compiler from moving LDS accesses across it; no vmcnt(0) is implied, so
+  // LDS-DMA weight prefetches stay in flight across the barrier.
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+// one 1 KiB wave-instruction of LDS-DMA: lane l copies 16 B from g + 16 l to lds + 16 l.
+__device__ __forceinline__ void glds16(const char* g_wave_base, char* lds_wave_base, int lane) {
+  __builtin_amdgcn_global_load_lds((const void*)(g_wave_base + lane * 16),
+                                   (lds_void*)lds_wave_base, 16, 0, 0);
+}
+
+}  // namespace dmip

@@ -1,0 +1,59 @@
+// Internal (non-exported) launch interface between the C-ABI layer (dmip_capi.cpp) and the
+// kernels (dmip_kernels.hip). Plain structs of device pointers; no torch types anywhere.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace dmip {
+
+struct SamplerParams {
+  const char* hidden;         // (NL-1)*(W/32) row-tile chunks of (W/16) KiB bf16 fragments
+  const char* a1;             // per-y layer-1 blocks [n_y][W/32][K1S] KiB (a1_prep_kernel)
+  const char* ao;             // output layer blocks [W/16] KiB (rows duplicated into both lane halves)
+  const float* bias_hidden;   // [NL-1][W/32][2][16] accumulator init per lane half
+  const float* bias_out;      // [2][16]
+  const float* noise;         // injected normals [S+1][n_y][n_chains][D] (slot 0 -> x0) or null
+  float* x_out;               // [n_y][n_chains][D]
+  long long n_chains;         // chains per y
+  long long chain_offset;     // global index of chain 0 (keys the RNG)
+  int num_steps;
+  float T, bmin, bdiff, delta, sqrt_delta, mean, stdv;
+  unsigned long long seed;
+};
+
+struct ForwardParams {
+  const char* hidden;
+  const char* a1;             // [W/32][K1S] KiB, all inputs varying
+  const char* ao;             // [W/16] KiB, natural output rows
+  const float* bias_hidden;
+  const float* bias_out;
+  const float* x;             // [n][xdim]
+  const float* y;             // [n][ydim] (y_stride = ydim) or one row (y_stride = 0)
+  const float* t;             // [n] (t_stride = 1) or one value (t_stride = 0)
+  float* out;                 // [n][out_dim]
+  long long n;
+  long long y_stride;
+  int t_stride;
+  int xdim, ydim, out_dim;
+};
+
+struct A1PrepParams {
+  const float* w1;   // [width][in_dim] fp32 (nn.Linear layout)
+  const float* b1;   // [width]
+  const float* y;    // [n_y][ydim]
+  char* a1;          // out: [n_y][width/32][k1s] KiB
+  int width, in_dim, xdim, ydim, y_col0, t_col, k1s;
+};
+
+hipError_t launch_sampler(const SamplerParams& p, int width, int n_hidden, int xdim, int n_y, hipStream_t st,
+                          bool* supported);
+bool sampler_shape_supported(int width, int n_hidden, int xdim);
+hipError_t launch_forward(const ForwardParams& p, int width, int n_hidden, int in_dim, hipStream_t st,
+                          bool* supported);
+hipError_t launch_a1_prep(const A1PrepParams& p, int n_y, hipStream_t st);
+hipError_t launch_rng_words(unsigned long long seed, long long off, unsigned long long stream, long long n,
+                            int n_words, unsigned int* out, hipStream_t st);
+hipError_t launch_rng_normals(unsigned long long seed, long long off, unsigned long long stream, long long n,
+                              int n_pairs, float* out, hipStream_t st);
+hipError_t launch_schedule(int S, float T, float bmin, float bdiff, float* out, hipStream_t st);
+
+}  // namespace dmip

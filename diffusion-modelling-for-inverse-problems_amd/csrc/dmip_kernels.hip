@@ -1,0 +1,513 @@
+// dmip kernels for gfx950 (MI355X, CDNA4): the fused persistent reverse-SDE sampler, the score
+// MLP forward, and the small prep/debug kernels behind the C-ABI in include/dmip.h.
+//
+// Data flow of the sampler (one wave = 32 posterior chains, 8 waves = one workgroup):
+//   * The chain state (x, RNG) lives in VGPRs for all num_steps; HBM is written once at the end.
+//   * Hidden activations never leave the registers: a layer's 32x32 f32 accumulator tile (column =
+//     chain on the lane, rows = hidden units in the 16 registers) is activated, packed to bf16 and
+//     used directly as the B operand of the next layer's v_mfma_f32_32x32x16_bf16. The weight
+//     (A) fragments are pre-permuted on the host to the matching k order.
+//   * Weights: layer 1 (with the y-conditioning folded in), the output layer and the biases are
+//     LDS-resident; the W x W hidden layers are LDS-resident when they fit and otherwise streamed
+//     from L2 through an R-slot LDS ring by LDS-DMA (global_load_lds_dwordx4), one row tile
+//     (32 rows x W) per slot, with counted vmcnt waits and raw s_barriers.
+//   * Layer 1 runs on MFMA with split-bf16 operands (x, tau and the weights as hi+lo pairs), so
+//     the chain state enters the net at ~fp32 accuracy.
+// Reference: models/diffusion.py:27-46 (loop), sdes.py:77-87 (drift/diffusion), nets.py:17-35 (MLP).
+#include "dmip_device.h"
+#include "dmip_internal.h"
+
+namespace dmip {
+
+template <int W, int NL, int K1S, int R, bool RES>
+struct Lay {
+  static constexpr int T = W / 32;            // 32-row tiles per layer
+  static constexpr int KS = W / 16;           // 16-deep k-steps over a hidden layer
+  static constexpr int CHUNK = KS * 1024;     // one row tile of a W x W layer, bf16 fragments
+  static constexpr int NC = (NL - 1) * T;     // hidden chunks per network evaluation
+  static constexpr int A1_OFF = 0;
+  static constexpr int A1_BYTES = T * K1S * 1024;
+  static constexpr int AO_OFF = A1_OFF + A1_BYTES;
+  static constexpr int AO_BYTES = KS * 1024;
+  static constexpr int BH_OFF = AO_OFF + AO_BYTES;
+  static constexpr int BH_BYTES = (NL - 1) * T * 2 * 16 * 4;
+  static constexpr int BO_OFF = BH_OFF + BH_BYTES;
+  static constexpr int BO_BYTES = 2 * 16 * 4;
+  static constexpr int W_OFF = BO_OFF + BO_BYTES;
+  static constexpr int SLOTS = RES ? NC : R;
+  static constexpr int TOTAL = W_OFF + SLOTS * CHUNK;
+};
+
+// ---------------------------------------------------------------------- shared LDS staging
+template <int NW>
+__device__ __forceinline__ void stage_blocks(char* lds, const char* g, int n_blocks, int w, int lane) {
+  for (int p = w; p < n_blocks; p += NW) glds16(g + p * 1024, lds + p * 1024, lane);
+}
+
+__device__ __forceinline__ void stage_floats(float* lds, const float* g, int n, int tid, int nthreads) {
+  for (int i = tid; i < n; i += nthreads) lds[i] = g[i];
+}
+
+template <int NW, int PPW, int CHUNK, int NC, int R>
+__device__ __forceinline__ void ring_issue(char* ring, const char* hidden, long long gc, int w, int lane) {
+  const int chunk = (int)(gc % NC);
+  const int slot = (int)(gc % R);
+#pragma unroll
+  for (int q = 0; q < PPW; ++q) {
+    const int p = w * PPW + q;
+    glds16(hidden + (size_t)chunk * CHUNK + p * 1024, ring + slot * CHUNK + p * 1024, lane);
+  }
+}
+
+// ------------------------------------------------------------------- one network evaluation
+// Hidden W x W layers + output layer, given layer-1 activations in H0. Returns the output
+// accumulator tile (rows = output dims, see the host packers for the row maps).
+template <int W, int NL, int K1S, int NW, int R, bool RES, bool CONSERVATIVE>
+struct Net {
+  using L = Lay<W, NL, K1S, R, RES>;
+  static constexpr int T = L::T;
+  static constexpr int KS = L::KS;
+  static constexpr int PPW = RES ? 1 : KS / NW;
+
+  char* lds;
+  const char* hidden;
+  long long gc;  // global chunk counter (ring mode)
+  int w, lane;
+
+  __device__ __forceinline__ const char* chunk_sync() {
+    if constexpr (RES) {
+      return nullptr;
+    } else {
+      if constexpr (CONSERVATIVE) wait_vmcnt<0>();
+      else wait_vmcnt<(R - 2) * PPW>();
+      lds_barrier();
+      ring_issue<NW, PPW, L::CHUNK, L::NC, R>(lds + L::W_OFF, hidden, gc + R - 1, w, lane);
+      const char* slot = lds + L::W_OFF + (int)(gc % R) * L::CHUNK;
+      ++gc;
+      return slot;
+    }
+  }
+
+  __device__ __forceinline__ f32x16 bias_tile(int off) const {
+    const float* b = (const float*)(lds + off) + (lane >> 5) * 16;
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = b[r];
+    return acc;
+  }
+
+  template <int LI>
+  __device__ __forceinline__ void hidden_layer(const bf16x8 (&Hin)[KS], bf16x8 (&Hout)[KS]) {
+    f32x16 pend;
+#pragma unroll
+    for (int rt = 0; rt < T; ++rt) {
+      const char* wb;
+      if constexpr (RES) {
+        // keep the resident weights in LDS: without this the compiler hoists every fragment
+        // read out of the step loop into (spilled) registers
+        asm volatile("" ::: "memory");
+        wb = lds + L::W_OFF + (LI * T + rt) * L::CHUNK;
+      } else {
+        wb = chunk_sync();
+      }
+      f32x16 acc = bias_tile(L::BH_OFF + ((LI * T + rt) * 2) * 64);
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const bf16x8 a = *(const bf16x8*)(wb + s * 1024 + lane * 16);
+        acc = mfma32(a, Hin[s], acc);
+      }
+      // activation of the previous tile overlaps this tile's MFMAs
+      if (rt > 0) act_pack<false>(pend, Hout[2 * (rt - 1)], Hout[2 * (rt - 1) + 1]);
+      pend = acc;
+    }
+    act_pack<false>(pend, Hout[2 * (T - 1)], Hout[2 * (T - 1) + 1]);
+  }
+
+  template <int LI>
+  __device__ __forceinline__ void hidden_chain(bf16x8 (&Ha)[KS], bf16x8 (&Hb)[KS], f32x16& out) {
+    if constexpr (LI == NL - 1) {  // all W x W layers done: output layer
+      asm volatile("" ::: "memory");
+      out = bias_tile(L::BO_OFF);
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const bf16x8 a = *(const bf16x8*)(lds + L::AO_OFF + s * 1024 + lane * 16);
+        out = mfma32(a, Ha[s], out);
+      }
+    } else {
+      hidden_layer<LI>(Ha, Hb);
+      hidden_chain<LI + 1>(Hb, Ha, out);
+    }
+  }
+
+  // layer 1 from the B1 operand (split-bf16 inputs), double tanh (nets.py:21-26)
+  __device__ __forceinline__ void layer1(const bf16x8 (&B1)[K1S], bf16x8 (&H)[KS]) {
+    f32x16 pend;
+#pragma unroll
+    for (int rt = 0; rt < T; ++rt) {
+      asm volatile("" ::: "memory");
+      f32x16 acc = {};
+#pragma unroll
+      for (int s = 0; s < K1S; ++s) {
+        const bf16x8 a = *(const bf16x8*)(lds + L::A1_OFF + (rt * K1S + s) * 1024 + lane * 16);
+        acc = mfma32(a, B1[s], acc);
+      }
+      if (rt > 0) act_pack<true>(pend, H[2 * (rt - 1)], H[2 * (rt - 1) + 1]);
+      pend = acc;
+    }
+    act_pack<true>(pend, H[2 * (T - 1)], H[2 * (T - 1) + 1]);
+  }
+
+  __device__ __forceinline__ f32x16 eval(const bf16x8 (&B1)[K1S]) {
+    bf16x8 Ha[KS], Hb[KS];
+    layer1(B1, Ha);
+    f32x16 out;
+    hidden_chain<0>(Ha, Hb, out);
+    return out;
+  }
+
+  // load the resident parts (and the whole hidden stack in resident mode); then start the ring
+  __device__ __forceinline__ void prologue(const char* a1, const char* ao, const float* bias_hidden,
+                                           const float* bias_out) {
+    const int tid = threadIdx.x;
+    stage_blocks<NW>(lds + L::A1_OFF, a1, T * K1S, w, lane);
+    stage_blocks<NW>(lds + L::AO_OFF, ao, KS, w, lane);
+    if constexpr (RES) stage_blocks<NW>(lds + L::W_OFF, hidden, L::NC * KS, w, lane);
+    stage_floats((float*)(lds + L::BH_OFF), bias_hidden, L::BH_BYTES / 4, tid, NW * 64);
+    stage_floats((float*)(lds + L::BO_OFF), bias_out, L::BO_BYTES / 4, tid, NW * 64);
+    wait_vmcnt<0>();
+    __syncthreads();
+    if constexpr (!RES) {
+      for (int q = 0; q < R - 1; ++q)
+        ring_issue<NW, PPW, L::CHUNK, L::NC, R>(lds + L::W_OFF, hidden, (long long)q, w, lane);
+    }
+  }
+
+  __device__ __forceinline__ void epilogue() {
+    wait_vmcnt<0>();  // no LDS-DMA may still be landing when the workgroup retires
+  }
+};
+
+// B1 operand of layer 1 for the sampler: u = [hi(v) | lo(v) | hi(v) | 1 | 1 | 0...],
+// v = (x_0..x_{D-1}, tau); lane half h supplies u[16 s + 8 h + j].
+template <int D, int K1S>
+__device__ __forceinline__ void build_b1(const float (&x)[D], float tau, int h, bf16x8 (&B1)[K1S]) {
+  constexpr int NV = D + 1;
+  float v[NV];
+#pragma unroll
+  for (int k = 0; k < D; ++k) v[k] = x[k];
+  v[D] = tau;
+  __bf16 vh[NV], vl[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    vh[k] = (__bf16)v[k];
+    vl[k] = (__bf16)(v[k] - (float)vh[k]);
+  }
+#pragma unroll
+  for (int s = 0; s < K1S; ++s) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      // both candidate slot values (h = 0 and h = 1) are compile-time; select by lane half
+      const int k0 = 16 * s + j, k1 = 16 * s + 8 + j;
+      auto slot = [&](int k) -> __bf16 {
+        if (k < NV) return vh[k];
+        if (k < 2 * NV) return vl[k - NV];
+        if (k < 3 * NV) return vh[k - 2 * NV];
+        if (k < 3 * NV + 2) return (__bf16)1.0f;
+        return (__bf16)0.0f;
+      };
+      B1[s][j] = h ? slot(k1) : slot(k0);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------- sampler kernel
+template <int W, int NL, int D, int NW, int R, bool RES, bool NOISE>
+__global__ void __launch_bounds__(NW * 64, (NW * 64 + 255) / 256)
+em_sampler_kernel(SamplerParams p) {
+  constexpr int K1S = (3 * (D + 1) + 2 + 15) / 16;
+  using L = Lay<W, NL, K1S, R, RES>;
+  static_assert(L::TOTAL <= 160 * 1024, "LDS budget");
+  static_assert(RES || (L::KS % NW == 0), "ring pieces per wave");
+  static_assert(D <= 4, "sampler output rows are duplicated into both lane halves (D <= 4)");
+  __shared__ __attribute__((aligned(16))) char lds[L::TOTAL];
+
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int h = lane >> 5;
+  const int yi = blockIdx.y;
+  const long long c_local = (long long)blockIdx.x * (NW * 32) + w * 32 + (lane & 31);
+  const bool valid = c_local < p.n_chains;
+
+  Net<W, NL, K1S, NW, R, RES, NOISE> net{lds, p.hidden, 0, w, lane};
+  net.prologue(p.a1 + (size_t)yi * L::T * K1S * 1024, p.ao, p.bias_hidden, p.bias_out);
+
+  float x[D];
+  Rng rng = rng_init(p.seed, (uint64_t)(p.chain_offset + c_local), (uint64_t)yi);
+  {
+    float n[D];
+    if constexpr (NOISE) {
+      const float* src = p.noise + (((size_t)yi * p.n_chains + (valid ? c_local : 0)) * D);
+#pragma unroll
+      for (int k = 0; k < D; ++k) n[k] = src[k];
+    } else {
+      rng_normals<D>(rng, n);
+    }
+#pragma unroll
+    for (int k = 0; k < D; ++k) x[k] = __fadd_rn(__fmul_rn(n[k], p.stdv), p.mean);
+  }
+  const size_t noise_step = (size_t)gridDim.y * p.n_chains * D;
+
+  for (int i = 0; i < p.num_steps; ++i) {
+    const StepCoef cf = step_coef(i, p.num_steps, p.T, p.bmin, p.bdiff);
+    bf16x8 B1[K1S];
+    build_b1<D, K1S>(x, cf.tau, h, B1);
+    const f32x16 out = net.eval(B1);
+    float xi[D];
+    if constexpr (NOISE) {
+      const float* src = p.noise + noise_step * (i + 1) + (((size_t)yi * p.n_chains + (valid ? c_local : 0)) * D);
+#pragma unroll
+      for (int k = 0; k < D; ++k) xi[k] = src[k];
+    } else {
+      rng_normals<D>(rng, xi);
+    }
+#pragma unroll
+    for (int k = 0; k < D; ++k) x[k] = em_update(x[k], out[k], xi[k], cf, p.delta, p.sqrt_delta);
+  }
+  net.epilogue();
+  if (valid && h == 0) {
+    float* dst = p.x_out + ((size_t)yi * p.n_chains + c_local) * D;
+#pragma unroll
+    for (int k = 0; k < D; ++k) dst[k] = x[k];
+  }
+}
+
+// ---------------------------------------------------------------------- MLP forward kernel
+// out[n] = MLP(cat[x, y, t]) for arbitrary rows (model.sde.a(x, y, t), nets.py:32-35); every
+// input column varies per row, so layer 1 takes the whole row as split-bf16 slots.
+template <int W, int NL, int IN, int NW, int R, bool RES>
+__global__ void __launch_bounds__(NW * 64, (NW * 64 + 255) / 256)
+mlp_forward_kernel(ForwardParams p) {
+  constexpr int K1S = (3 * IN + 2 + 15) / 16;
+  using L = Lay<W, NL, K1S, R, RES>;
+  static_assert(L::TOTAL <= 160 * 1024, "LDS budget");
+  __shared__ __attribute__((aligned(16))) char lds[L::TOTAL];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int h = lane >> 5;
+  Net<W, NL, K1S, NW, R, RES, true> net{lds, p.hidden, 0, w, lane};
+  net.prologue(p.a1, p.ao, p.bias_hidden, p.bias_out);
+
+  const long long n_tiles = (p.n + 31) / 32;
+  const long long rounds = (n_tiles + (long long)gridDim.x * NW - 1) / ((long long)gridDim.x * NW);
+  for (long long rd = 0; rd < rounds; ++rd) {
+    const long long tile = (rd * gridDim.x + blockIdx.x) * NW + w;
+    const long long row = tile * 32 + (lane & 31);
+    const bool valid = row < p.n;
+    float v[IN];
+    const long long rr = valid ? row : 0;
+#pragma unroll
+    for (int k = 0; k < IN; ++k) {
+      float val;
+      if (k < p.xdim) val = p.x[rr * p.xdim + k];
+      else if (k < p.xdim + p.ydim) val = p.y[(p.y_stride ? rr * p.y_stride : 0) + (k - p.xdim)];
+      else val = p.t[p.t_stride ? rr : 0];
+      v[k] = val;
+    }
+    __bf16 vh[IN], vl[IN];
+#pragma unroll
+    for (int k = 0; k < IN; ++k) {
+      vh[k] = (__bf16)v[k];
+      vl[k] = (__bf16)(v[k] - (float)vh[k]);
+    }
+    bf16x8 B1[K1S];
+#pragma unroll
+    for (int s = 0; s < K1S; ++s) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        auto slot = [&](int k) -> __bf16 {
+          if (k < IN) return vh[k];
+          if (k < 2 * IN) return vl[k - IN];
+          if (k < 3 * IN) return vh[k - 2 * IN];
+          if (k < 3 * IN + 2) return (__bf16)1.0f;
+          return (__bf16)0.0f;
+        };
+        B1[s][j] = h ? slot(16 * s + 8 + j) : slot(16 * s + j);
+      }
+    }
+    const f32x16 out = net.eval(B1);
+    if (valid) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int orow = (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (orow < p.out_dim) p.out[row * p.out_dim + orow] = out[r];
+      }
+    }
+  }
+  net.epilogue();
+}
+
+// ------------------------------------------------------------------ per-y layer-1 prep kernel
+// A1 fragment blocks for the sampler: row j of the augmented layer-1 matrix is
+//   [hi(cW_v) | hi(cW_v) | lo(cW_v) | hi(c_j) | lo(c_j) | 0...]   (v = x columns, then t)
+// with c = 2 log2(e) and c_j = c (b1_j + W1_{j,y} . y) -- the y-conditioning is hoisted out of
+// the step loop into this per-y bias.
+__global__ void a1_prep_kernel(A1PrepParams p) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  const int yi = blockIdx.y;
+  if (j >= p.width) return;
+  const float* wrow = p.w1 + (size_t)j * p.in_dim;
+  double cj = p.b1[j];
+  for (int m = 0; m < p.ydim; ++m) cj += (double)wrow[p.y_col0 + m] * (double)p.y[(size_t)yi * p.ydim + m];
+  cj *= (double)kTanhScale;
+  const int nv = p.xdim + 1;
+  const int kpad = p.k1s * 16;
+  __bf16* blk = (__bf16*)(p.a1 + (size_t)yi * (p.width / 32) * p.k1s * 1024);
+  const int rt = j / 32, i = j % 32;
+  for (int k = 0; k < kpad; ++k) {
+    float val = 0.0f;
+    int vk = -1, part = 0;
+    if (k < nv) { vk = k; part = 0; }
+    else if (k < 2 * nv) { vk = k - nv; part = 0; }
+    else if (k < 3 * nv) { vk = k - 2 * nv; part = 1; }
+    if (vk >= 0) {
+      const int col = vk < p.xdim ? vk : p.t_col;
+      const float cw = (float)((double)kTanhScale * (double)wrow[col]);
+      const __bf16 hi = (__bf16)cw;
+      val = part == 0 ? (float)hi : (float)(__bf16)(cw - (float)hi);
+    } else if (k == 3 * nv) {
+      val = (float)(__bf16)(float)cj;
+    } else if (k == 3 * nv + 1) {
+      const float cf = (float)cj;
+      val = (float)(__bf16)(cf - (float)(__bf16)cf);
+    }
+    const int s = k / 16, hh = (k % 16) / 8, jj = k % 8;
+    const int ln = i + 32 * hh;
+    blk[((size_t)(rt * p.k1s + s) * 64 + ln) * 8 + jj] = (__bf16)val;
+  }
+}
+
+// --------------------------------------------------------------------------- debug kernels
+__global__ void rng_words_kernel(unsigned long long seed, long long chain_offset, unsigned long long stream,
+                                 long long n, int n_words, unsigned int* out) {
+  const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n) return;
+  Rng r = rng_init(seed, (uint64_t)(chain_offset + c), stream);
+  for (int k = 0; k < n_words; ++k) out[c * n_words + k] = rng_next(r);
+}
+
+__global__ void rng_normals_kernel(unsigned long long seed, long long chain_offset, unsigned long long stream,
+                                   long long n, int n_pairs, float* out) {
+  const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n) return;
+  Rng r = rng_init(seed, (uint64_t)(chain_offset + c), stream);
+  for (int k = 0; k < n_pairs; ++k) {
+    float a, b;
+    rng_normal_pair(r, a, b);
+    out[(c * n_pairs + k) * 2] = a;
+    out[(c * n_pairs + k) * 2 + 1] = b;
+  }
+}
+
+__global__ void schedule_kernel(int S, float T, float bmin, float bdiff, float* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > S) return;
+  const float ts = __fmul_rn(linspace_at(i, S), T);
+  const StepCoef c = step_coef(i, S, T, bmin, bdiff);
+  out[i * 4 + 0] = ts;
+  out[i * 4 + 1] = c.tau;
+  out[i * 4 + 2] = c.beta;
+  out[i * 4 + 3] = c.g;
+}
+
+// ------------------------------------------------------------------------------ dispatch
+template <int W, int NL, int D, int NW, int R, bool RES>
+static hipError_t launch_sampler_t(const SamplerParams& p, int n_y, hipStream_t st) {
+  const long long per_wg = NW * 32;
+  dim3 grid((unsigned)((p.n_chains + per_wg - 1) / per_wg), (unsigned)n_y);
+  if (p.noise) hipLaunchKernelGGL((em_sampler_kernel<W, NL, D, NW, R, RES, true>), grid, dim3(NW * 64), 0, st, p);
+  else hipLaunchKernelGGL((em_sampler_kernel<W, NL, D, NW, R, RES, false>), grid, dim3(NW * 64), 0, st, p);
+  return hipGetLastError();
+}
+
+template <int W, int NL, int IN, int NW, int R, bool RES>
+static hipError_t launch_forward_t(const ForwardParams& p, hipStream_t st) {
+  const long long tiles = (p.n + 31) / 32;
+  long long wgs = (tiles + NW - 1) / NW;
+  if (wgs > 2048) wgs = 2048;
+  if (wgs < 1) wgs = 1;
+  hipLaunchKernelGGL((mlp_forward_kernel<W, NL, IN, NW, R, RES>), dim3((unsigned)wgs), dim3(NW * 64), 0, st, p);
+  return hipGetLastError();
+}
+
+// Supported shapes: the BASELINE widths (64 linear, 256 scatterometry) plus 128; three hidden
+// layers (config_*.yml use [W]*3). Width 512 is not instantiated yet.
+#define DMIP_W_CASES(X, NL, D) \
+  X(64, NL, D, 8, 0, true)     \
+  X(128, NL, D, 8, 0, true)    \
+  X(256, NL, D, 8, 4, false)
+
+hipError_t launch_sampler(const SamplerParams& p, int width, int n_hidden, int xdim, int n_y, hipStream_t st,
+                          bool* supported) {
+  *supported = true;
+#define X(Wv, NLv, Dv, NWv, Rv, RESv) \
+  if (width == Wv && n_hidden == NLv && xdim == Dv) return launch_sampler_t<Wv, NLv, Dv, NWv, Rv, RESv>(p, n_y, st);
+  DMIP_W_CASES(X, 3, 2)
+  DMIP_W_CASES(X, 3, 3)
+  DMIP_W_CASES(X, 2, 2)
+  DMIP_W_CASES(X, 2, 3)
+#undef X
+  *supported = false;
+  return hipSuccess;
+}
+
+bool sampler_shape_supported(int width, int n_hidden, int xdim) {
+#define X(Wv, NLv, Dv, NWv, Rv, RESv) \
+  if (width == Wv && n_hidden == NLv && xdim == Dv) return true;
+  DMIP_W_CASES(X, 3, 2)
+  DMIP_W_CASES(X, 3, 3)
+  DMIP_W_CASES(X, 2, 2)
+  DMIP_W_CASES(X, 2, 3)
+#undef X
+  return false;
+}
+
+hipError_t launch_forward(const ForwardParams& p, int width, int n_hidden, int in_dim, hipStream_t st,
+                          bool* supported) {
+  *supported = true;
+#define X(Wv, NLv, INv, NWv, Rv, RESv) \
+  if (width == Wv && n_hidden == NLv && in_dim == INv) return launch_forward_t<Wv, NLv, INv, NWv, Rv, RESv>(p, st);
+  DMIP_W_CASES(X, 3, 5)   // linear CDE: x(2) y(2) t
+  DMIP_W_CASES(X, 3, 27)  // scatterometry CDE: x(3) y(23) t
+  DMIP_W_CASES(X, 3, 3)   // linear prior MLP2: x(2) t
+  DMIP_W_CASES(X, 3, 4)   // scatterometry prior MLP2: x(3) t
+#undef X
+  *supported = false;
+  return hipSuccess;
+}
+
+hipError_t launch_a1_prep(const A1PrepParams& p, int n_y, hipStream_t st) {
+  dim3 grid((unsigned)((p.width + 127) / 128), (unsigned)n_y);
+  hipLaunchKernelGGL(a1_prep_kernel, grid, dim3(128), 0, st, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_rng_words(unsigned long long seed, long long off, unsigned long long stream, long long n,
+                            int n_words, unsigned int* out, hipStream_t st) {
+  hipLaunchKernelGGL(rng_words_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, seed, off, stream, n,
+                     n_words, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_rng_normals(unsigned long long seed, long long off, unsigned long long stream, long long n,
+                              int n_pairs, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(rng_normals_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, seed, off, stream, n,
+                     n_pairs, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_schedule(int S, float T, float bmin, float bdiff, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(schedule_kernel, dim3((unsigned)((S + 256) / 256)), dim3(256), 0, st, S, T, bmin, bdiff, out);
+  return hipGetLastError();
+}
+
+}  // namespace dmip

@@ -1,0 +1,258 @@
+"""CDE / CDiffE / PosteriorDiffusionEstimator with the reference's construct-and-sample API
+(models/diffusion.py:14-229).
+
+Sampling is the hot path and runs on the HIP device only:
+  * CDE: one launch of the fused persistent reverse-SDE kernel for all num_steps
+    (libdmip dmip_em_sample). The chain state never leaves the registers.
+  * PosteriorDiffusionEstimator and the (repaired) CDiffE sampler: per-step launches of the fused
+    MFMA network kernel (dmip_mlp_forward) with the SDE update as device tensor ops; a fused
+    two-network / CDiffE kernel is the next step.
+There is no CPU sampling path: without a HIP device the samplers raise.
+
+RNG: the reference draws x0 and the per-step noise from torch's global generator. Here every chain
+has its own counter-keyed stream (seed, global chain index, y index); the seed itself is drawn from
+torch's global generator, so torch.manual_seed(s) still makes a sampling call reproducible, and the
+samples of a chain do not depend on how chains are split over workgroups or GPUs.
+"""
+import numpy as np
+import torch
+from torch import nn
+
+from . import _lib
+from . import sdes
+from .losses import PosteriorLoss
+from .nets import MLP, MLP2, PosteriorScore
+
+device = 'cuda' if torch.cuda.is_available() else 'cpu'
+
+
+def _draw_seed():
+    return int(torch.randint(0, 2 ** 62, (1,)).item())
+
+
+class BaseClassDiffusionModel:
+    """models/diffusion.py:14-58."""
+
+    def __init__(self, xdim, ydim):
+        self.xdim = xdim
+        self.ydim = ydim
+        self.sde = None
+
+    def __call__(self, *args, **kwargs):
+        return self.forward(*args, **kwargs)
+
+    # ----------------------------------------------------------------- sampling API
+    def forward(self, y, num_samples=2000, num_steps=200, mean=0, std=1):
+        """Posterior samples for one observation y (ydim,): np.ndarray (num_samples, xdim) float32
+        (models/diffusion.py:27-46). Under torch.distributed with world_size > 1 the chains are
+        sharded over the ranks and every rank returns all num_samples (parallel.sample_sharded)."""
+        from . import parallel
+        x = parallel.sample_sharded(self, y, num_samples, num_steps, mean, std)
+        return x.cpu().numpy()
+
+    def _exec_device(self, y):
+        if isinstance(y, torch.Tensor) and y.is_cuda:
+            return y.device
+        p = next(self.sde.a.parameters())
+        if p.is_cuda:
+            return p.device
+        if torch.cuda.is_available():
+            return torch.device('cuda', torch.cuda.current_device())
+        raise RuntimeError("dmip: sampling needs a HIP device (the reverse-SDE sampler is a HIP kernel; "
+                           "there is no CPU sampling path)")
+
+    def _ys(self, y, dev):
+        ys = torch.as_tensor(y).to(device=dev, dtype=torch.float32)
+        return ys.reshape(-1, self.ydim).contiguous()
+
+    def sample_device(self, y, num_samples, num_steps=200, mean=0, std=1, seed=None, chain_offset=0,
+                      noise=None):
+        """Device-resident samples (n_y, num_samples, xdim) for ys (n_y, ydim) -- no host copy.
+        `chain_offset` selects a shard of a larger run; `noise` injects standard normals
+        (num_steps + 1, n_y, num_samples, xdim) (slot 0 -> x0) in place of the internal RNG."""
+        raise NotImplementedError
+
+    def sample_t(self, x, eps=1e-4):
+        """Training times (models/diffusion.py:48-58)."""
+        if self.sde.debias:
+            t_ = self.sde.base_sde.sample_debiasing_t([x.size(0), ] + [1 for _ in range(x.ndim - 1)]) + eps
+            t_ = t_.to(x)
+            t_[torch.where(t_ > self.sde.T)] -= eps
+            t_.requires_grad = True
+        else:
+            t_ = eps + torch.rand([x.size(0), ] + [1 for _ in range(x.ndim - 1)], requires_grad=True).to(x) * self.sde.T
+            t_[torch.where(t_ > self.sde.T)] = self.sde.T - eps
+        return t_
+
+    # ----------------------------------------------------------------- training API
+    @staticmethod
+    def _accumulate(logger_info, k, loss):
+        if isinstance(loss, tuple):
+            loss, info = loss
+            for key, value in info.items():
+                prev = logger_info.get(key, 0.0)
+                logger_info[key] = prev * k / (k + 1) + value.item() / (k + 1)
+        return loss
+
+    def _train_loop(self, optimizer, epoch_data_loader, batch_loss):
+        mean_loss = 0
+        logger_info = {}
+        for k, (x, y) in enumerate(epoch_data_loader()):
+            loss = self._accumulate(logger_info, k, batch_loss(x, y))
+            optimizer.zero_grad()
+            loss.backward()
+            optimizer.step()
+            mean_loss = mean_loss * k / (k + 1) + loss / (k + 1)
+        return mean_loss, logger_info
+
+
+class CDE(BaseClassDiffusionModel):
+    """Conditional diffusion estimator: score net a(x_t, y, t) (models/diffusion.py:60-105)."""
+
+    def __init__(self, xdim, ydim, hidden_layers):
+        super().__init__(xdim, ydim)
+        score_net = MLP(xdim + ydim + 1, xdim, hidden_layers, nn.Tanh()).to(device)
+        self.sde = sdes.PluginReverseSDE(sdes.VariancePreservingSDE(), score_net, T=1, debias=True)
+
+    def sample_device(self, y, num_samples, num_steps=200, mean=0, std=1, seed=None, chain_offset=0,
+                      noise=None):
+        dev = self._exec_device(y)
+        ys = self._ys(y, dev)
+        net = self.sde.a
+        if next(net.parameters()).device != dev:
+            raise RuntimeError(f"dmip: score network is on {next(net.parameters()).device}, y on {dev}")
+        handle = net.dmip_handle(dev, self.xdim)
+        base = self.sde.base_sde
+        if float(base.T) != float(self.sde.T):
+            raise ValueError("PluginReverseSDE.T must equal the base SDE's T")
+        seed = _draw_seed() if seed is None else seed
+        out = torch.empty(ys.shape[0], int(num_samples), self.xdim, device=dev, dtype=torch.float32)
+        if noise is not None:
+            noise = noise.to(device=dev, dtype=torch.float32).contiguous()
+            if tuple(noise.shape) != (int(num_steps) + 1, ys.shape[0], int(num_samples), self.xdim):
+                raise ValueError("noise must have shape (num_steps+1, n_y, num_samples, xdim)")
+        _lib.em_sample(handle, _lib.vpsde(base.beta_min, base.beta_max, self.sde.T), ys, num_samples,
+                       chain_offset, num_steps, mean, std, seed, out, noise)
+        return out
+
+    def train_epoch(self, optimizer, loss_fn, epoch_data_loader):
+        def batch_loss(x, y):
+            t = self.sample_t(x)
+            x_t, target, std, g = self.sde.base_sde.sample(t, x, return_noise=True)
+            if loss_fn.name == 'DSMLoss':
+                return loss_fn(self.sde.a(x_t, y, t) / g, std, target).mean()
+            return loss_fn(self.sde, x, y, x_t, t, target, std, g)
+        return self._train_loop(optimizer, epoch_data_loader, batch_loss)
+
+
+def _em_device_loop(model, ys, num_samples, num_steps, mean, std, seed, chain_offset, drift, zdim,
+                    keep, y_resample=None):
+    """Reverse-SDE EM loop on device tensors for the estimators without a fused kernel yet: the
+    network evaluations are dmip_mlp_forward launches, the update follows
+    models/diffusion.py:40-42 (same rounding order as the fused kernel)."""
+    dev = ys.device
+    base = model.sde.base_sde
+    T = float(model.sde.T)
+    n_y = ys.shape[0]
+    gen = torch.Generator(device=dev)
+    gen.manual_seed((seed + 7919 * int(chain_offset)) & 0x7FFFFFFFFFFFFFFF)
+    outs = []
+    ts = torch.linspace(0, 1, num_steps + 1) * T
+    delta = T / num_steps
+    with torch.no_grad():
+        for k in range(n_y):
+            y = ys[k]
+            x = torch.randn(num_samples, zdim, device=dev, generator=gen) * std + mean
+            for i in range(num_steps):
+                tau = (T - ts[i]).item()
+                tvec = torch.full((num_samples, 1), tau, device=dev)
+                z_in = x if y_resample is None else y_resample(x, y, tau, gen)
+                mu = drift(z_in, y, tvec)
+                sigma = base.g(tvec, z_in)
+                xi = torch.randn(z_in.shape, device=dev, generator=gen)
+                z = z_in + delta * mu + delta ** 0.5 * sigma * xi
+                x = z[:, :keep] if keep < z.shape[1] else z
+            outs.append(x[:, :keep])
+    return torch.stack(outs)
+
+
+class CDiffE(BaseClassDiffusionModel):
+    """Conditional diffusion over the joint z = (x, y) (models/diffusion.py:109-180).
+
+    The reference sampler (models/diffusion.py:158-180) raises TypeError (`sde.mu` without `cond`).
+    Repaired semantics, consistent with its training (models/diffusion.py:129-137): each step
+    re-diffuses the observation, y_t ~ q(y_t | y) at forward time T - t_i, evaluates the joint score
+    net a(x_t, y_t, T - t_i) (output xdim + ydim), takes the EM step on z_t = [x_t, y_t] and keeps x.
+    """
+
+    def __init__(self, xdim, ydim, hidden_layers):
+        super().__init__(xdim, ydim)
+        score_net = MLP(xdim + ydim + 1, xdim + ydim, hidden_layers, nn.Tanh()).to(device)
+        self.sde = sdes.PluginReverseSDE(sdes.VariancePreservingSDE(), score_net, T=1, debias=True)
+
+    def sample_device(self, y, num_samples, num_steps=200, mean=0, std=1, seed=None, chain_offset=0,
+                      noise=None):
+        if noise is not None:
+            raise ValueError("noise injection is only implemented for the fused CDE sampler")
+        dev = self._exec_device(y)
+        ys = self._ys(y, dev)
+        seed = _draw_seed() if seed is None else seed
+        base = self.sde.base_sde
+        xd = self.xdim
+
+        def y_resample(x, y, tau, gen):
+            tt = torch.full((x.shape[0], 1), tau, device=x.device)
+            eps = torch.randn(x.shape[0], self.ydim, device=x.device, generator=gen)
+            y_t = base.mean_weight(tt) * y + base.var(tt) ** 0.5 * eps
+            return torch.cat([x[:, :xd], y_t], dim=1)
+
+        def drift(z, y, tvec):
+            a = self.sde.a(z[:, :xd].contiguous(), z[:, xd:].contiguous(), tvec)
+            return base.g(tvec, z) * a - base.f(tvec, z)
+
+        return _em_device_loop(self, ys, int(num_samples), int(num_steps), mean, std, seed, chain_offset,
+                               drift, xd, xd, y_resample)
+
+    def train_epoch(self, optimizer, loss_fn, epoch_data_loader):
+        def batch_loss(x, y):
+            z = torch.concat([x, y], dim=1)
+            t = self.sample_t(z)
+            diffused, target, std, g = self.sde.base_sde.sample(t, z, return_noise=True)
+            x_t, y_t = diffused[:, :self.xdim], diffused[:, self.xdim:]
+            if loss_fn.name == 'DSMLoss':
+                return loss_fn(self.sde.a(x_t, y_t, t) / g, std, target).mean()
+            return loss_fn(self.sde, x, y, diffused, t, target, std, g)
+        return self._train_loop(optimizer, epoch_data_loader, batch_loss)
+
+
+class PosteriorDiffusionEstimator(BaseClassDiffusionModel):
+    """Prior score + likelihood score, score = g (prior(x,t) + lik(x,y,t)) (models/diffusion.py:182-229)."""
+
+    def __init__(self, xdim, ydim, hidden_layers):
+        super().__init__(xdim, ydim)
+        forward_process = sdes.VariancePreservingSDE()
+        prior_net = MLP2(xdim + 1, xdim, hidden_layers, nn.Tanh()).to(device)
+        likelihood_net = MLP(xdim + ydim + 1, xdim, hidden_layers, nn.Tanh()).to(device)
+        score_net = PosteriorScore(prior_net, likelihood_net, forward_process)
+        self.sde = sdes.PluginReverseSDE(forward_process, score_net, T=1, debias=True)
+        self.loss_fn = PosteriorLoss
+
+    def sample_device(self, y, num_samples, num_steps=200, mean=0, std=1, seed=None, chain_offset=0,
+                      noise=None):
+        if noise is not None:
+            raise ValueError("noise injection is only implemented for the fused CDE sampler")
+        dev = self._exec_device(y)
+        ys = self._ys(y, dev)
+        seed = _draw_seed() if seed is None else seed
+        base = self.sde.base_sde
+
+        def drift(x, y, tvec):
+            return base.g(tvec, x) * self.sde.a(x, y, tvec) - base.f(tvec, x)
+
+        return _em_device_loop(self, ys, int(num_samples), int(num_steps), mean, std, seed, chain_offset,
+                               drift, self.xdim, self.xdim)
+
+    def train_epoch(self, optimizer, loss_fn, epoch_data_loader):
+        def batch_loss(x, y):
+            return loss_fn(self.sde, x, y, self.sample_t(x))
+        return self._train_loop(optimizer, epoch_data_loader, batch_loss)

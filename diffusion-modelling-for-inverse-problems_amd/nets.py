@@ -1,0 +1,112 @@
+"""Score networks with the reference's module layout (nets.py:17-57, 143-157).
+
+`MLP` / `MLP2` keep the exact parameter naming of the reference (`0.*, 3.*, 5.*, 7.*` for three
+hidden layers) so reference checkpoints load unchanged, including the quirk that makes the first
+hidden layer apply tanh twice: the reference stores its activation module a second time as
+`self.act` on the nn.Sequential (nets.py:26), which registers it as an extra child between layer 0
+and the next Linear and shifts the numbering.
+
+Evaluation on a HIP device with autograd off goes to the fused MFMA kernel
+(libdmip dmip_mlp_forward); the weights are packed once per parameter snapshot. Autograd (the
+training losses) uses the eager module chain.
+"""
+import collections
+
+import torch
+from torch import nn
+
+from . import _lib
+
+
+class _TanhChainMLP(nn.Sequential):
+    input_layout = _lib.DMIP_INPUT_X_Y_T
+
+    def __init__(self, input_dim, output_dim, hidden_layers, activation):
+        self.input_dim = input_dim
+        self.output_dim = output_dim
+        self.hidden_layers = list(hidden_layers)
+        w = [input_dim] + self.hidden_layers + [output_dim]
+        # the activation is one module object registered under several names, as in the reference
+        mods = [("0", nn.Linear(w[0], w[1])), ("1", activation), ("act", activation)]
+        for i in range(1, len(self.hidden_layers)):
+            mods += [(str(2 * i + 1), nn.Linear(w[i], w[i + 1])), (str(2 * i + 2), activation)]
+        mods.append((str(2 * len(self.hidden_layers) + 1), nn.Linear(w[-2], w[-1])))
+        super().__init__(collections.OrderedDict(mods))
+        self.act = activation
+        self._dmip = None
+
+    # -------------------------------------------------------------- packed HIP weights
+    def linear_layers(self):
+        return [(m.weight, m.bias) for m in self if isinstance(m, nn.Linear)]
+
+    def _snapshot_key(self, device):
+        return (str(device),) + tuple((p.data_ptr(), p._version) for p in self.parameters())
+
+    def dmip_handle(self, device, xdim):
+        key = self._snapshot_key(device) + (xdim,)
+        if self._dmip is None or self._dmip[0] != key:
+            handle = _lib.MlpHandle(self.linear_layers(), self.input_dim, self.output_dim, xdim,
+                                    self.input_layout, device)
+            self._dmip = (key, handle)
+        return self._dmip[1]
+
+    def _wants_autograd(self, *tensors):
+        if not torch.is_grad_enabled():
+            return False
+        return any(t.requires_grad for t in tensors) or any(p.requires_grad for p in self.parameters())
+
+    def _hip_forward(self, x, y, t, xdim):
+        n = x.shape[0]
+        dev = x.device
+        h = self.dmip_handle(dev, xdim)
+        xc = x.detach().to(torch.float32).contiguous()
+        tt = t.detach().to(device=dev, dtype=torch.float32).reshape(-1).contiguous()
+        t_stride = 1 if tt.numel() == n else 0
+        if t_stride == 0 and tt.numel() != 1:
+            raise ValueError("t must have one entry per row or a single entry")
+        yc, y_stride = None, 0
+        if y is not None:
+            yc = y.detach().to(device=dev, dtype=torch.float32)
+            if yc.ndim == 1:
+                yc = yc.reshape(1, -1)
+            y_stride = yc.shape[1] if yc.shape[0] == n and n != 1 else 0
+            yc = yc.contiguous()
+        out = torch.empty(n, self.output_dim, device=dev, dtype=torch.float32)
+        _lib.mlp_forward(h, xc, yc, tt, out, y_stride, t_stride)
+        return out
+
+
+class MLP(_TanhChainMLP):
+    """Score network a(x, y, t) on cat[x, y, t] (nets.py:17-35)."""
+
+    def forward(self, x, y, t):
+        if x.is_cuda and not self._wants_autograd(x, y, t):
+            return self._hip_forward(x, y, t, x.shape[1])
+        inp = torch.cat([x, y, t.view(len(x), 1)], dim=1)
+        assert inp.ndim == 2, 'Input Tensor is expected to be 2D with shape (batch_size, ydim+ydim+embeddim)'
+        return super().forward(inp)
+
+
+class MLP2(_TanhChainMLP):
+    """Prior score network a(x, t) on cat[x, t] (nets.py:37-57)."""
+    input_layout = _lib.DMIP_INPUT_X_T
+
+    def forward(self, x, t):
+        if x.is_cuda and not self._wants_autograd(x, t):
+            return self._hip_forward(x, None, t, x.shape[1])
+        inp = torch.cat([x, t.view(len(x), 1)], dim=1)
+        assert inp.ndim == 2, 'Input Tensor is expected to be 2D with shape (batch_size, ydim+ydim+embeddim)'
+        return super().forward(inp)
+
+
+class PosteriorScore(nn.Module):
+    """g(t) * (prior(x, t) + likelihood(x, y, t)) (nets.py:143-157)."""
+
+    def __init__(self, prior_net, likelihood_net, forward_process):
+        super().__init__()
+        self.prior_net = prior_net
+        self.likelihood_net = likelihood_net
+        self.forward_sde = forward_process
+
+    def forward(self, x, y, t):
+        return self.forward_sde.g(t, x) * (self.prior_net(x, t) + self.likelihood_net(x, y, t))

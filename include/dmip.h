@@ -1,0 +1,109 @@
+/* dmip.h -- C ABI of libdmip.so, the MI355X (gfx950) conditional score-diffusion posterior
+ * sampler. Plain pointers and sizes only; every device pointer is caller-owned HIP device memory
+ * and every call is asynchronous on the given hipStream_t (passed as void*; NULL = default stream).
+ *
+ * The reference (maffos/Diffusion-Modelling-for-inverse-problems) has no FFI: its boundary is the
+ * Python object API. Each entry point below states the reference interface it replaces; the
+ * Python host package (diffusion-modelling-for-inverse-problems_amd/) binds these with ctypes
+ *  behind the reference's own class and function names.
+ *
+ * Errors: every function returns a dmip_status; on failure dmip_last_error() (thread-local)
+ * describes it. Handles are immutable after creation and may be shared between threads.
+ */
+#ifndef DMIP_H_
+#define DMIP_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DMIP_ABI_VERSION 1
+
+typedef enum {
+  DMIP_OK = 0,
+  DMIP_ERR_INVALID = 1,     /* bad argument (maps to ValueError)                  */
+  DMIP_ERR_UNSUPPORTED = 2, /* shape with no compiled kernel (maps to ValueError) */
+  DMIP_ERR_HIP = 3,         /* HIP runtime failure (maps to RuntimeError)          */
+  DMIP_ERR_ALLOC = 4        /* device allocation failure (maps to RuntimeError)    */
+} dmip_status;
+
+/* Column layout of the network input (nets.py:33 MLP: cat[x, y, t]; nets.py:54 MLP2: cat[x, t]). */
+typedef enum { DMIP_INPUT_X_Y_T = 0, DMIP_INPUT_X_T = 1 } dmip_input_layout;
+
+/* Activation chain (nets.py:17-30): Linear -> Tanh -> Tanh -> [Linear -> Tanh]*(L-1) -> Linear.
+ * The first hidden layer applies tanh twice because MLP registers its activation module a second
+ * time as `self.act` (nets.py:26). DMIP_ACT_TANH is the single-tanh chain. */
+typedef enum { DMIP_ACT_TANH_TWICE_FIRST = 0, DMIP_ACT_TANH = 1 } dmip_act;
+
+/* Arithmetic of the network GEMMs: bf16 MFMA operands with fp32 accumulation (layer 1 takes its
+ * inputs as split hi+lo bf16, i.e. ~fp32); the chain state and the SDE update are always fp32. */
+typedef enum { DMIP_PREC_BF16 = 0 } dmip_precision;
+
+/* VariancePreservingSDE (sdes.py:9-19): beta(t) = beta_min + (beta_max - beta_min) t. */
+typedef struct {
+  double beta_min; /* python floats of the reference; rounded to fp32 exactly where torch rounds */
+  double beta_max;
+  double T;
+} dmip_vpsde;
+
+typedef struct dmip_mlp dmip_mlp;
+
+/* Create a score-network handle from fp32 host weights (nn.Linear layout W[out][in], b[out]).
+ * Replaces: constructing nets.MLP / nets.MLP2 (nets.py:17-57) and moving it to the device
+ * (models/diffusion.py:66-71, 187-199); weights in the reference state_dict order 0,3,5,7.
+ *   in_dim       network input width (x + y + 1 for X_Y_T, x + 1 for X_T)
+ *   out_dim      network output width (the `a` drift, xdim for CDE)
+ *   n_hidden     number of hidden layers L (len(hidden_layers))
+ *   widths       L hidden widths (all equal; 64, 128 or 256 compiled)
+ *   weights[i]   layer i weight, i = 0..L (L+1 linear layers)
+ *   biases[i]    layer i bias
+ * The handle owns packed device copies (bf16 MFMA fragments in the kernels' layouts). */
+int dmip_mlp_create(int in_dim, int out_dim, int n_hidden, const int* widths, int act_mode, int input_layout,
+                    int xdim, const float* const* weights, const float* const* biases, dmip_mlp** out);
+
+int dmip_mlp_destroy(dmip_mlp* net);
+
+/* out[n][out_dim] = net(cat[x, y, t]) for arbitrary rows.
+ * Replaces: MLP.forward / MLP2.forward (nets.py:32-35, 52-57), i.e. model.sde.a(x, y, t) as used by
+ * the evaluate() score-MSE (main_diffusion_scatterometry.py:65-67) and the losses.
+ *   y_stride  0: one y row broadcast to all rows; ydim: per-row y      (ignored for X_T)
+ *   t_stride  0: one t broadcast;                 1: per-row t */
+int dmip_mlp_forward(const dmip_mlp* net, const float* x_dev, const float* y_dev, int64_t y_stride,
+                     const float* t_dev, int t_stride, int64_t n, float* out_dev, int precision, void* stream);
+
+/* Fused reverse-time Euler-Maruyama posterior sampler (one launch for all num_steps).
+ * Replaces: BaseClassDiffusionModel.forward (models/diffusion.py:27-46) for CDE, i.e.
+ * x0 = randn*std + mean; for i < S: x <- x + delta*mu(t_i, x, y) + sqrt(delta)*sigma*xi_i with
+ * mu = g(T-t) a(x, y, T-t) + 0.5 beta(T-t) x and sigma = g(T-t) (sdes.py:77-87), ts = linspace(0,1,S+1)*T.
+ *   y_dev       [n_y][ydim] conditioning observations; chains of y index k go to x_out[k]
+ *   n_chains    chains per y;  chain_offset: global index of chain 0 (keys the RNG, so a shard of a
+ *               larger run draws exactly the chains it would draw in the full run)
+ *   seed        RNG seed; the chain-c stream of y index k is a function of (seed, chain_offset + c, k)
+ *   noise_dev   NULL for the internal RNG, or injected standard normals [S+1][n_y][n_chains][xdim]
+ *               (slot 0 -> x0) to replay a captured reference trajectory
+ *   x_out_dev   [n_y][n_chains][xdim] fp32 */
+int dmip_em_sample(const dmip_mlp* net, const dmip_vpsde* sde, const float* y_dev, int n_y, int ydim, int xdim,
+                   int64_t n_chains, int64_t chain_offset, int num_steps, float mean, float stdv, uint64_t seed,
+                   int precision, const float* noise_dev, float* x_out_dev, void* stream);
+
+/* Test hooks for the parity suite (integer RNG stream, normals, schedule). */
+int dmip_rng_words(uint64_t seed, int64_t chain_offset, uint64_t stream_id, int64_t n_chains, int n_words,
+                   uint32_t* out_dev, void* stream);
+int dmip_rng_normals(uint64_t seed, int64_t chain_offset, uint64_t stream_id, int64_t n_chains, int n_pairs,
+                     float* out_dev, void* stream);
+/* out[(S+1)][4] = (ts_i, T - ts_i, beta(T - ts_i), sqrt(beta)) exactly as the sampler computes them
+ * (models/diffusion.py:34, sdes.py:21-35). */
+int dmip_schedule(int num_steps, const dmip_vpsde* sde, float* out_dev, void* stream);
+
+const char* dmip_last_error(void);
+int dmip_abi_version(void);
+/* Non-zero when this build has a kernel for the given sampler shape. */
+int dmip_sampler_supported(int width, int n_hidden, int xdim);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DMIP_H_ */

@@ -1,0 +1,300 @@
+"""CPU oracle for the conditional score-diffusion posterior sampler -- TEST INFRASTRUCTURE.
+
+Restates, in numpy float32 and in the reference's operation order, every function on the hot
+path. Each function cites the reference file:line it follows. It is pinned
+against golden vectors captured from the reference (tests/golden/make_golden.py) by
+tests/test_oracle_golden.py; it is never called by the product path.
+
+RNG note: the reference draws from torch's mt19937 (CPU) stream, which cannot be reproduced by a
+counter-keyed parallel sampler. Two parity modes therefore exist:
+  * injected noise -- the oracle/kernel consume a captured (x0, xi) sequence (fixture G3) and
+    must match the reference trajectory to fp tolerance;
+  * chain-keyed RNG -- the oracle restates the product RNG (splitmix64-seeded xoshiro128**,
+    Box-Muller), so the kernel's integer stream is checked bit-exactly and its normals to ulps.
+"""
+import numpy as np
+
+F32 = np.float32
+
+# ------------------------------------------------------------------------------------------
+# A1  schedule -- models/diffusion.py:31,34-35,40-41
+# ------------------------------------------------------------------------------------------
+
+def linspace_f32(num_steps):
+    """torch.linspace(0, 1, S+1) in float32 (models/diffusion.py:34).
+
+    Restates ATen's CPU linspace: step = fl32(1/S); the first (S+1)//2 points are fl32(i*step),
+    the rest are 1 - (S-i)*step with a single rounding (fused multiply-add).
+    """
+    S = int(num_steps)
+    n = S + 1
+    step = F32(1.0) / F32(S)
+    i = np.arange(n, dtype=np.int64)
+    half = n // 2
+    out = np.empty(n, dtype=F32)
+    out[:half] = (i[:half].astype(F32) * step).astype(F32)
+    # single-rounding 1 - (S-i)*step: evaluate exactly in float64, round once to float32
+    k = (S - i[half:]).astype(np.float64)
+    out[half:] = (1.0 - k * np.float64(step)).astype(F32)
+    return out
+
+
+def schedule(num_steps, T=1.0):
+    """ts = linspace*T; the net and the coefficients see tau_i = T - ts[i] (sdes.py:78)."""
+    ts = (linspace_f32(num_steps) * F32(T)).astype(F32)
+    tau = (F32(T) - ts).astype(F32)
+    return ts, tau
+
+
+# ------------------------------------------------------------------------------------------
+# A7  VariancePreservingSDE -- sdes.py:9-57
+# ------------------------------------------------------------------------------------------
+BETA_MIN = 0.1
+BETA_MAX = 20.0
+
+
+def vp_beta(t, beta_min=BETA_MIN, beta_max=BETA_MAX):
+    """sdes.py:21-22: beta_min + (beta_max-beta_min)*t, python scalars rounded to fp32."""
+    t = np.asarray(t, dtype=F32)
+    return (F32(beta_min) + (F32(beta_max - beta_min) * t).astype(F32)).astype(F32)
+
+
+def vp_g(t, beta_min=BETA_MIN, beta_max=BETA_MAX):
+    """sdes.py:33-35: ones_like(y) * beta(t)**0.5 (pow 0.5 == correctly rounded sqrt)."""
+    return np.sqrt(vp_beta(t, beta_min, beta_max)).astype(F32)
+
+
+def vp_mean_weight(t, beta_min=BETA_MIN, beta_max=BETA_MAX):
+    """sdes.py:24-25: exp(-0.25 t^2 (bmax-bmin) - 0.5 t bmin)."""
+    t = np.asarray(t, dtype=F32)
+    a = (F32(-0.25) * (t * t).astype(F32)).astype(F32) * F32(beta_max - beta_min)
+    b = (F32(0.5) * t).astype(F32) * F32(beta_min)
+    return np.exp((a.astype(F32) - b.astype(F32)).astype(F32)).astype(F32)
+
+
+def vp_var(t, beta_min=BETA_MIN, beta_max=BETA_MAX):
+    """sdes.py:27-28: 1 - exp(-0.5 t^2 (bmax-bmin) - t bmin)."""
+    t = np.asarray(t, dtype=F32)
+    a = (F32(-0.5) * (t * t).astype(F32)).astype(F32) * F32(beta_max - beta_min)
+    b = (t * F32(beta_min)).astype(F32)
+    return (F32(1.0) - np.exp((a.astype(F32) - b).astype(F32))).astype(F32)
+
+
+# ------------------------------------------------------------------------------------------
+# A9/A10  MLP / MLP2 / PosteriorScore -- nets.py:17-57,143-157
+# ------------------------------------------------------------------------------------------
+
+def mlp_params_from_state(state, prefix=""):
+    """Ordered [(W, b), ...] from a reference MLP state_dict (keys 0,3,5,7 -- nets.py:21-30;
+    the Tanh children '1', 'act', '4', '6' hold no parameters)."""
+    idx = sorted({int(k[len(prefix):].split("_")[0]) for k in state.keys()
+                  if k.startswith(prefix) and k[len(prefix):].split("_")[0].isdigit()
+                  and k.endswith("weight")})
+    return [(np.asarray(state[f"{prefix}{i}_weight"], F32), np.asarray(state[f"{prefix}{i}_bias"], F32))
+            for i in idx]
+
+
+def mlp_forward(params, inp, tanh_twice_first=True):
+    """nets.py:17-35. Forward chain is Linear -> Tanh -> Tanh(act, the quirk of nets.py:26) ->
+    [Linear -> Tanh] * (L-1) -> Linear."""
+    h = np.asarray(inp, F32)
+    L = len(params)
+    for li, (W, b) in enumerate(params):
+        h = (h @ W.T + b).astype(F32)
+        if li < L - 1:
+            h = np.tanh(h).astype(F32)
+            if li == 0 and tanh_twice_first:
+                h = np.tanh(h).astype(F32)
+    return h
+
+
+def cde_a(params, x, y, t):
+    """MLP.forward (nets.py:32-35): cat[x, y, t.view(N,1)]."""
+    x = np.asarray(x, F32)
+    n = x.shape[0]
+    y = np.broadcast_to(np.asarray(y, F32), (n, np.asarray(y).shape[-1]))
+    t = np.broadcast_to(np.asarray(t, F32).reshape(-1, 1), (n, 1))
+    return mlp_forward(params, np.concatenate([x, y, t], axis=1))
+
+
+def mlp2_a(params, x, t):
+    """MLP2.forward (nets.py:52-57): cat[x, t]."""
+    x = np.asarray(x, F32)
+    t = np.broadcast_to(np.asarray(t, F32).reshape(-1, 1), (x.shape[0], 1))
+    return mlp_forward(params, np.concatenate([x, t], axis=1))
+
+
+def posterior_a(prior_params, lik_params, x, y, t):
+    """PosteriorScore.forward (nets.py:155-157): g(t) * (prior(x,t) + lik(x,y,t))."""
+    s = (mlp2_a(prior_params, x, t) + cde_a(lik_params, x, y, t)).astype(F32)
+    tt = np.broadcast_to(np.asarray(t, F32).reshape(-1, 1), s.shape)
+    return (vp_g(tt) * s).astype(F32)
+
+
+# ------------------------------------------------------------------------------------------
+# A19  LinearForwardProblem.score_posterior -- linear_problem.py:61-65
+# ------------------------------------------------------------------------------------------
+LIN_A = np.array([[1.0, 0.5], [0.0, 1.0]], F32)
+LIN_B = np.array([0.3, 0.5], F32)
+LIN_SCALE = F32(0.3)
+
+
+def linear_score_posterior(x, y):
+    x = np.asarray(x, F32)
+    y = np.asarray(y, F32)
+    y_res = (y - (x @ LIN_A.T + LIN_B)).astype(F32)
+    sig_inv = (F32(1.0) / LIN_SCALE) * np.eye(2, dtype=F32)
+    return (-x + (y_res @ sig_inv.T) @ LIN_A).astype(F32)
+
+
+# ------------------------------------------------------------------------------------------
+# product RNG restated: splitmix64-seeded xoshiro128** per chain + Box-Muller
+# (the kernel's generator; see include/dmip.h dmip_rng_normals)
+# ------------------------------------------------------------------------------------------
+_M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+GOLDEN = np.uint64(0x9E3779B97F4A7C15)
+CHAIN_MUL = np.uint64(0xD1B54A32D192ED03)
+STREAM_MUL = np.uint64(0x8CB92BA72F3D8DD7)
+
+
+def _splitmix_next(state):
+    with np.errstate(over="ignore"):
+        state = state + GOLDEN
+        z = state.copy()
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return state, z
+
+
+def rng_init(seed, chain_ids, stream=0):
+    """Per-chain state: splitmix64 seeded with seed + chain*CHAIN_MUL + stream*STREAM_MUL.
+    Keyed by the GLOBAL chain index, so a chain's draws do not depend on how the chains are
+    sharded over workgroups or GPUs."""
+    c = np.asarray(chain_ids, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        sm = np.uint64(seed) + c * CHAIN_MUL + np.uint64(stream) * STREAM_MUL
+    sm, z0 = _splitmix_next(sm)
+    sm, z1 = _splitmix_next(sm)
+    s = np.stack([z0 & np.uint64(0xFFFFFFFF), z0 >> np.uint64(32),
+                  z1 & np.uint64(0xFFFFFFFF), z1 >> np.uint64(32)]).astype(np.uint32)
+    zero = (s == 0).all(axis=0)
+    s[0, zero] = np.uint32(1)
+    return s  # (4, n) uint32
+
+
+def _rotl(x, k):
+    return ((x << np.uint32(k)) | (x >> np.uint32(32 - k))).astype(np.uint32)
+
+
+def rng_next(s):
+    """xoshiro128** (Blackman & Vigna) on a (4, n) uint32 state, in place; returns n uint32."""
+    with np.errstate(over="ignore"):
+        result = (_rotl((s[1] * np.uint32(5)).astype(np.uint32), 7) * np.uint32(9)).astype(np.uint32)
+    t = (s[1] << np.uint32(9)).astype(np.uint32)
+    s[2] ^= s[0]
+    s[3] ^= s[1]
+    s[1] ^= s[2]
+    s[0] ^= s[3]
+    s[2] ^= t
+    s[3] = _rotl(s[3], 11)
+    return result
+
+
+def rng_normals(s, d):
+    """d normals per chain (ceil(d/2) Box-Muller pairs; the unused odd one is dropped).
+    u1 = 1 - (r>>8)*2^-24 in (0,1], u2 = (r>>8)*2^-24; n = sqrt(-2 ln u1) * (cos, sin)(2 pi u2)."""
+    n = s.shape[1]
+    out = np.empty((n, 2 * ((d + 1) // 2)), F32)
+    inv = F32(2.0 ** -24)
+    for p in range((d + 1) // 2):
+        r0 = rng_next(s)
+        r1 = rng_next(s)
+        u1 = (F32(1.0) - (r0 >> np.uint32(8)).astype(F32) * inv).astype(F32)
+        u2 = ((r1 >> np.uint32(8)).astype(F32) * inv).astype(F32)
+        rad = np.sqrt(F32(-2.0) * np.log(u1)).astype(F32)
+        th = (F32(2.0 * np.pi) * u2).astype(F32)
+        out[:, 2 * p] = rad * np.cos(th)
+        out[:, 2 * p + 1] = rad * np.sin(th)
+    return out[:, :d]
+
+
+def rng_uniform_words(seed, chain_ids, n_words, stream=0):
+    s = rng_init(seed, chain_ids, stream)
+    return np.stack([rng_next(s) for _ in range(n_words)], axis=1)
+
+
+# ------------------------------------------------------------------------------------------
+# A2/A8  Euler-Maruyama reverse-SDE loop -- models/diffusion.py:27-46, sdes.py:77-87
+# ------------------------------------------------------------------------------------------
+
+def em_step(x, a, tau, delta, beta_min=BETA_MIN, beta_max=BETA_MAX, xi=None):
+    """One EM update with the reference rounding order:
+    mu = fl(g*a) - fl(fl(-0.5*beta)*x)     (sdes.py:77-79, lambda = 0)
+    x <- fl(x + fl(delta*mu)) + fl(fl(sqrt(delta)*sigma)*xi), sigma = g (sdes.py:86-87)."""
+    beta = vp_beta(tau, beta_min, beta_max)
+    g = np.sqrt(beta).astype(F32)
+    mu = ((g * a).astype(F32) - ((F32(-0.5) * beta).astype(F32) * x).astype(F32)).astype(F32)
+    d32 = F32(delta)
+    sd32 = F32(np.sqrt(np.float64(delta)))
+    out = (x + (d32 * mu).astype(F32)).astype(F32)
+    return (out + ((sd32 * g).astype(F32) * xi).astype(F32)).astype(F32)
+
+
+def em_sample(a_fn, x0, num_steps, T=1.0, noise=None, rng_state=None, xdim=None,
+              beta_min=BETA_MIN, beta_max=BETA_MAX, snapshots=None):
+    """models/diffusion.py:27-46 with either an injected noise tensor (S, N, d) or the product
+    RNG state (consumed in place). a_fn(x, tau_scalar) returns the net output (N, d)."""
+    x = np.asarray(x0, F32).copy()
+    ts, tau = schedule(num_steps, T)
+    delta = float(T) / num_steps  # python double, rounded to fp32 inside em_step
+    snaps = {}
+    for i in range(num_steps):
+        a = a_fn(x, tau[i])
+        if noise is not None:
+            xi = np.asarray(noise[i], F32)
+        else:
+            xi = rng_normals(rng_state, xdim or x.shape[1])
+        x = em_step(x, a, tau[i], delta, beta_min, beta_max, xi)
+        if snapshots is not None and (i + 1) in snapshots:
+            snaps[i + 1] = x.copy()
+    return (x, snaps) if snapshots is not None else x
+
+
+def cde_sample(params, y, num_samples, num_steps, seed, mean=0.0, std=1.0, chain_offset=0,
+               stream=0, T=1.0):
+    """Product-RNG CDE sampler: x0 = normals*std + mean (models/diffusion.py:32-33), then EM."""
+    xdim = params[-1][0].shape[0]
+    st = rng_init(seed, np.arange(chain_offset, chain_offset + num_samples), stream)
+    x0 = (rng_normals(st, xdim) * F32(std) + F32(mean)).astype(F32)
+    y = np.asarray(y, F32)
+    return em_sample(lambda x, tau: cde_a(params, x, y, tau), x0, num_steps, T=T,
+                     rng_state=st, xdim=xdim)
+
+
+# ------------------------------------------------------------------------------------------
+# A11  evaluation metric -- main_diffusion_scatterometry.py:71-102
+# ------------------------------------------------------------------------------------------
+
+def hist_kl(samples_true, samples_model, nbins=75, lim=(-1.2, 1.2), eps=1e-10):
+    """KL2 = sum rel_entr(p_true+eps, p_model+eps) on a nbins^d histogram, renormalised."""
+    from scipy.special import rel_entr
+    d = samples_true.shape[1]
+    rng = [lim] * d
+    ht, _ = np.histogramdd(samples_true, bins=(nbins,) * d, range=rng)
+    hm, _ = np.histogramdd(samples_model, bins=(nbins,) * d, range=rng)
+    ht = ht / ht.sum() + eps
+    hm = hm / hm.sum() + eps
+    ht /= ht.sum()
+    hm /= hm.sum()
+    return float(np.sum(rel_entr(ht, hm))), float(np.sum(rel_entr(hm, ht)))
+
+
+def ks_2samp_stat(a, b):
+    """Two-sample Kolmogorov-Smirnov statistic (no p-value)."""
+    a = np.sort(np.asarray(a, np.float64))
+    b = np.sort(np.asarray(b, np.float64))
+    z = np.concatenate([a, b])
+    ca = np.searchsorted(a, z, side="right") / a.size
+    cb = np.searchsorted(b, z, side="right") / b.size
+    return float(np.max(np.abs(ca - cb)))

@@ -1,0 +1,70 @@
+"""The C-ABI library: loads without a GPU, exports every symbol include/dmip.h declares, and
+rejects bad arguments before touching the device. CPU only (no compute calls)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+
+
+def _header_symbols():
+    txt = open(os.path.join(ROOT, "include", "dmip.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(dmip_[a-z0-9_]+)\s*\(", txt)))
+
+
+@pytest.fixture(scope="module")
+def lib(dmip):
+    path = dmip._lib.LIB_PATH
+    if not os.path.exists(path):
+        pytest.skip("libdmip.so not built")
+    return dmip._lib.lib()
+
+
+def test_exports_every_declared_symbol(lib, dmip):
+    syms = _header_symbols()
+    assert len(syms) >= 10
+    for s in syms:
+        assert hasattr(lib, s), s
+    assert set(syms) == set(dmip._lib.EXPORTED)
+
+
+def test_abi_version(lib):
+    assert lib.dmip_abi_version() == 1
+
+
+def test_supported_shapes(lib, dmip):
+    sup = dmip._lib.sampler_supported
+    assert sup(256, 3, 3) and sup(64, 3, 2) and sup(128, 3, 3)
+    assert not sup(96, 3, 3)
+    assert not sup(256, 3, 9)
+
+
+def test_create_rejects_bad_arguments(lib, dmip):
+    L = dmip._lib
+    out = ctypes.c_void_p()
+    widths = (ctypes.c_int * 3)(64, 64, 64)
+    null = (ctypes.c_void_p * 4)()
+    # null weight pointers
+    rc = lib.dmip_mlp_create(5, 2, 3, widths, 0, 0, 2, null, null, ctypes.byref(out))
+    assert rc == L.DMIP_ERR_INVALID and b"null" in lib.dmip_last_error()
+    # unequal widths
+    w2 = (ctypes.c_int * 3)(64, 32, 64)
+    rc = lib.dmip_mlp_create(5, 2, 3, w2, 0, 0, 2, null, null, ctypes.byref(out))
+    assert rc == L.DMIP_ERR_UNSUPPORTED
+    # unsupported activation chain
+    rc = lib.dmip_mlp_create(5, 2, 3, widths, 1, 0, 2, null, null, ctypes.byref(out))
+    assert rc == L.DMIP_ERR_UNSUPPORTED
+    with pytest.raises(ValueError):
+        L.check(L.DMIP_ERR_INVALID)
+
+
+def test_sampler_rejects_null_handle(lib, dmip):
+    L = dmip._lib
+    sde = L.vpsde(0.1, 20.0, 1.0)
+    rc = lib.dmip_em_sample(None, ctypes.byref(sde), None, 1, 2, 2, 10, 0, 10, 0.0, 1.0, 1, 0, None, None, None)
+    assert rc == L.DMIP_ERR_INVALID
+    rc = lib.dmip_schedule(0, ctypes.byref(sde), None, None)
+    assert rc == L.DMIP_ERR_INVALID
