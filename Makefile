@@ -3,7 +3,7 @@ PKG := diffusion-modelling-for-inverse-problems_amd
 CSRC := $(PKG)/csrc
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
-HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-parameter
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-parameter
 OBJS := $(CSRC)/dmip_kernels.o $(CSRC)/dmip_capi.o
 HDRS := $(CSRC)/dmip_device.h $(CSRC)/dmip_internal.h include/dmip.h
 

@@ -88,6 +88,9 @@ __device__ __forceinline__ void rng_normals(Rng& r, float (&n)[D]) {
 }
 
 // ------------------------------------------------------------------------------ schedule
+// NOTE: HIP's __fmul_rn/__fadd_rn are plain operators; libdmip is compiled with
+// -ffp-contract=off so they are not fused into FMAs (which would change the last bit of
+// beta / the EM update vs the reference). Intended FMAs are written as explicit builtins.
 // torch.linspace(0,1,S+1)[i] in fp32 (ATen CPU kernel: first half i*step, second half
 // 1-(S-i)*step with a single rounding) -- models/diffusion.py:34.
 __device__ __forceinline__ float linspace_at(int i, int S) {

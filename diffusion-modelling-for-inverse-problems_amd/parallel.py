@@ -49,8 +49,9 @@ def gather_shards(local, n, device):
     dev = device if backend == "nccl" else torch.device("cpu")
     pad = torch.zeros(n_y, width, d, dtype=local.dtype, device=dev)
     pad[:, :local.shape[1]] = local.to(dev)
-    out = torch.empty(ws, n_y, width, d, dtype=local.dtype, device=dev)
+    out = torch.empty(ws * n_y, width, d, dtype=local.dtype, device=dev)
     dist.all_gather_into_tensor(out, pad)
+    out = out.view(ws, n_y, width, d)
     parts = [out[r, :, :hi - lo] for r, (lo, hi) in enumerate(sizes)]
     return torch.cat(parts, dim=1).to(device)
 
