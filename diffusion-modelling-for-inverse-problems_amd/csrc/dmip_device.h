@@ -110,7 +110,9 @@ __device__ __forceinline__ StepCoef step_coef(int i, int S, float T, float bmin,
   const float ts = __fmul_rn(linspace_at(i, S), T);
   c.tau = __fsub_rn(T, ts);
   c.beta = __fadd_rn(bmin, __fmul_rn(bdiff, c.tau));
-  c.g = __fsqrt_rn(c.beta);
+  // correctly rounded sqrt: the f64 square root is correctly rounded and rounding it to f32 is
+  // innocuous (53 >= 2*24 + 2); hipcc's f32 __fsqrt_rn is not correctly rounded on gfx950
+  c.g = (float)__dsqrt_rn((double)c.beta);
   return c;
 }
 

@@ -17,6 +17,8 @@
 #include "dmip_device.h"
 #include "dmip_internal.h"
 
+#include <cstdlib>
+
 namespace dmip {
 
 template <int W, int NL, int K1S, int R, bool RES>
@@ -56,6 +58,21 @@ __device__ __forceinline__ void ring_issue(char* ring, const char* hidden, long 
   for (int q = 0; q < PPW; ++q) {
     const int p = w * PPW + q;
     glds16(hidden + (size_t)chunk * CHUNK + p * 1024, ring + slot * CHUNK + p * 1024, lane);
+  }
+}
+
+// acc += sum_s A[s] * H[s] over one 32-row tile: A fragments streamed from LDS (1 KiB apart)
+// with an explicit prefetch distance of PF reads, so the MFMA chain does not wait on each
+// fragment's LDS latency.
+template <int KS, int PF = 3>
+__device__ __forceinline__ void mfma_row_tile(const char* a_lane, const bf16x8 (&H)[KS], f32x16& acc) {
+  bf16x8 a[PF + 1];
+#pragma unroll
+  for (int s = 0; s < PF && s < KS; ++s) a[s] = *(const bf16x8*)(a_lane + s * 1024);
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    if (s + PF < KS) a[(s + PF) % (PF + 1)] = *(const bf16x8*)(a_lane + (s + PF) * 1024);
+    acc = mfma32(a[s % (PF + 1)], H[s], acc);
   }
 }
 
@@ -111,11 +128,7 @@ struct Net {
         wb = chunk_sync();
       }
       f32x16 acc = bias_tile(L::BH_OFF + ((LI * T + rt) * 2) * 64);
-#pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        const bf16x8 a = *(const bf16x8*)(wb + s * 1024 + lane * 16);
-        acc = mfma32(a, Hin[s], acc);
-      }
+      mfma_row_tile<KS>(wb + lane * 16, Hin, acc);
       // activation of the previous tile overlaps this tile's MFMAs
       if (rt > 0) act_pack<false>(pend, Hout[2 * (rt - 1)], Hout[2 * (rt - 1) + 1]);
       pend = acc;
@@ -128,11 +141,7 @@ struct Net {
     if constexpr (LI == NL - 1) {  // all W x W layers done: output layer
       asm volatile("" ::: "memory");
       out = bias_tile(L::BO_OFF);
-#pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        const bf16x8 a = *(const bf16x8*)(lds + L::AO_OFF + s * 1024 + lane * 16);
-        out = mfma32(a, Ha[s], out);
-      }
+      mfma_row_tile<KS>(lds + L::AO_OFF + lane * 16, Ha, out);
     } else {
       hidden_layer<LI>(Ha, Hb);
       hidden_chain<LI + 1>(Hb, Ha, out);
@@ -446,9 +455,20 @@ static hipError_t launch_forward_t(const ForwardParams& p, hipStream_t st) {
   X(128, NL, D, 8, 0, true)    \
   X(256, NL, D, 8, 4, false)
 
+// Development knob (not part of the ABI): DMIP_SAMPLER_VARIANT=1 runs width 256 as two
+// independent 4-wave workgroups per CU (each with its own 3-slot ring) instead of one 8-wave one.
+static int sampler_variant() {
+  const char* e = getenv("DMIP_SAMPLER_VARIANT");
+  return e ? atoi(e) : 0;
+}
+
 hipError_t launch_sampler(const SamplerParams& p, int width, int n_hidden, int xdim, int n_y, hipStream_t st,
                           bool* supported) {
   *supported = true;
+  if (width == 256 && sampler_variant() == 1) {
+    if (n_hidden == 3 && xdim == 3) return launch_sampler_t<256, 3, 3, 4, 3, false>(p, n_y, st);
+    if (n_hidden == 3 && xdim == 2) return launch_sampler_t<256, 3, 2, 4, 3, false>(p, n_y, st);
+  }
 #define X(Wv, NLv, Dv, NWv, Rv, RESv) \
   if (width == Wv && n_hidden == NLv && xdim == Dv) return launch_sampler_t<Wv, NLv, Dv, NWv, Rv, RESv>(p, n_y, st);
   DMIP_W_CASES(X, 3, 2)
