@@ -24,6 +24,7 @@ DMIP_PREC_BF16 = 0
 EXPORTED = (
     "dmip_mlp_create", "dmip_mlp_destroy", "dmip_mlp_forward", "dmip_em_sample", "dmip_rng_words",
     "dmip_rng_normals", "dmip_schedule", "dmip_last_error", "dmip_abi_version", "dmip_sampler_supported",
+    "dmip_em_sample_stamps",
 )
 
 
@@ -53,11 +54,14 @@ def _declare(lib):
     lib.dmip_em_sample.argtypes = [_c_void_p, ctypes.POINTER(DmipVpsde), _c_void_p, _i32, _i32, _i32,
                                    _i64, _i64, _i32, _f32, _f32, _u64, _i32, _c_void_p, _c_void_p,
                                    _c_void_p]
+    lib.dmip_em_sample_stamps.argtypes = [_c_void_p, ctypes.POINTER(DmipVpsde), _c_void_p, _i32, _i32, _i32,
+                                          _i64, _i32, _u64, _c_void_p, _c_void_p, _c_void_p]
     lib.dmip_rng_words.argtypes = [_u64, _i64, _u64, _i64, _i32, _c_void_p, _c_void_p]
     lib.dmip_rng_normals.argtypes = [_u64, _i64, _u64, _i64, _i32, _c_void_p, _c_void_p]
     lib.dmip_schedule.argtypes = [_i32, ctypes.POINTER(DmipVpsde), _c_void_p, _c_void_p]
     for name in ("dmip_mlp_create", "dmip_mlp_destroy", "dmip_mlp_forward", "dmip_em_sample",
-                 "dmip_rng_words", "dmip_rng_normals", "dmip_schedule", "dmip_sampler_supported"):
+                 "dmip_rng_words", "dmip_rng_normals", "dmip_schedule", "dmip_sampler_supported",
+                 "dmip_em_sample_stamps"):
         getattr(lib, name).restype = _i32
 
 

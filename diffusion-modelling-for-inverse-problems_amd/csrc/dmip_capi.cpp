@@ -272,9 +272,30 @@ int dmip_mlp_forward(const dmip_mlp* net, const float* x_dev, const float* y_dev
   return DMIP_OK;
 }
 
+static int em_sample_impl(const dmip_mlp* net, const dmip_vpsde* sde, const float* y_dev, int n_y, int ydim,
+                          int xdim, int64_t n_chains, int64_t chain_offset, int num_steps, float mean, float stdv,
+                          uint64_t seed, int precision, const float* noise_dev, float* x_out_dev, void* stream,
+                          uint64_t* stamps);
+
 int dmip_em_sample(const dmip_mlp* net, const dmip_vpsde* sde, const float* y_dev, int n_y, int ydim, int xdim,
                    int64_t n_chains, int64_t chain_offset, int num_steps, float mean, float stdv, uint64_t seed,
                    int precision, const float* noise_dev, float* x_out_dev, void* stream) {
+  return em_sample_impl(net, sde, y_dev, n_y, ydim, xdim, n_chains, chain_offset, num_steps, mean, stdv, seed,
+                        precision, noise_dev, x_out_dev, stream, nullptr);
+}
+
+int dmip_em_sample_stamps(const dmip_mlp* net, const dmip_vpsde* sde, const float* y_dev, int n_y, int ydim,
+                          int xdim, int64_t n_chains, int num_steps, uint64_t seed, float* x_out_dev,
+                          uint64_t* stamps_dev, void* stream) {
+  if (!stamps_dev) return fail(DMIP_ERR_INVALID, "null stamps buffer");
+  return em_sample_impl(net, sde, y_dev, n_y, ydim, xdim, n_chains, 0, num_steps, 0.0f, 1.0f, seed, DMIP_PREC_BF16,
+                        nullptr, x_out_dev, stream, stamps_dev);
+}
+
+static int em_sample_impl(const dmip_mlp* net, const dmip_vpsde* sde, const float* y_dev, int n_y, int ydim,
+                          int xdim, int64_t n_chains, int64_t chain_offset, int num_steps, float mean, float stdv,
+                          uint64_t seed, int precision, const float* noise_dev, float* x_out_dev, void* stream,
+                          uint64_t* stamps) {
   if (!net || !sde || !y_dev || !x_out_dev) return fail(DMIP_ERR_INVALID, "null argument");
   if (precision != DMIP_PREC_BF16) return fail(DMIP_ERR_UNSUPPORTED, "unknown precision");
   if (net->layout != DMIP_INPUT_X_Y_T) return fail(DMIP_ERR_INVALID, "sampler needs an x,y,t network (CDE)");
@@ -333,6 +354,7 @@ int dmip_em_sample(const dmip_mlp* net, const dmip_vpsde* sde, const float* y_de
   p.mean = mean;
   p.stdv = stdv;
   p.seed = seed;
+  p.stamps = (unsigned long long*)stamps;
   bool ok = false;
   e = dmip::launch_sampler(p, net->width, net->n_hidden, xdim, n_y, st, &ok);
   (void)hipFreeAsync(a1, st);

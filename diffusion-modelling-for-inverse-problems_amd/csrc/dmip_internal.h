@@ -18,6 +18,7 @@ struct SamplerParams {
   int num_steps;
   float T, bmin, bdiff, delta, sqrt_delta, mean, stdv;
   unsigned long long seed;
+  unsigned long long* stamps; // diagnostic build only: [n_wg * NW][3] phase cycle sums, else null
 };
 
 struct ForwardParams {

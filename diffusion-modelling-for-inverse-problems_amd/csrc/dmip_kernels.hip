@@ -230,7 +230,17 @@ __device__ __forceinline__ void build_b1(const float (&x)[D], float tau, int h, 
 }
 
 // ------------------------------------------------------------------------- sampler kernel
-template <int W, int NL, int D, int NW, int R, bool RES, bool NOISE>
+__device__ __forceinline__ unsigned long long stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+
+// STAMP: diagnostic build only (dmip_em_sample_stamps) -- per-wave cycle sums of the step phases
+// [layer 1 + B1, hidden layers, output layer + RNG + EM update], written to p.stamps.
+template <int W, int NL, int D, int NW, int R, bool RES, bool NOISE, bool STAMP = false>
 __global__ void __launch_bounds__(NW * 64, (NW * 64 + 255) / 256)
 em_sampler_kernel(SamplerParams p) {
   constexpr int K1S = (3 * (D + 1) + 2 + 15) / 16;
@@ -266,11 +276,19 @@ em_sampler_kernel(SamplerParams p) {
   }
   const size_t noise_step = (size_t)gridDim.y * p.n_chains * D;
 
+  unsigned long long ph[3] = {0, 0, 0};
   for (int i = 0; i < p.num_steps; ++i) {
+    unsigned long long t0 = 0, t1 = 0, t2 = 0;
+    if constexpr (STAMP) t0 = stamp();
     const StepCoef cf = step_coef(i, p.num_steps, p.T, p.bmin, p.bdiff);
     bf16x8 B1[K1S];
     build_b1<D, K1S>(x, cf.tau, h, B1);
-    const f32x16 out = net.eval(B1);
+    bf16x8 Ha[L::KS], Hb[L::KS];
+    net.layer1(B1, Ha);
+    if constexpr (STAMP) t1 = stamp();
+    f32x16 out;
+    net.template hidden_chain<0>(Ha, Hb, out);
+    if constexpr (STAMP) t2 = stamp();
     float xi[D];
     if constexpr (NOISE) {
       const float* src = p.noise + noise_step * (i + 1) + (((size_t)yi * p.n_chains + (valid ? c_local : 0)) * D);
@@ -281,8 +299,22 @@ em_sampler_kernel(SamplerParams p) {
     }
 #pragma unroll
     for (int k = 0; k < D; ++k) x[k] = em_update(x[k], out[k], xi[k], cf, p.delta, p.sqrt_delta);
+    if constexpr (STAMP) {
+      const unsigned long long t3 = stamp();
+      ph[0] += t1 - t0;
+      ph[1] += t2 - t1;
+      ph[2] += t3 - t2;
+    }
   }
   net.epilogue();
+  if constexpr (STAMP) {
+    if (lane == 0) {
+      unsigned long long* o = p.stamps + ((size_t)(blockIdx.y * gridDim.x + blockIdx.x) * NW + w) * 3;
+      o[0] = ph[0];
+      o[1] = ph[1];
+      o[2] = ph[2];
+    }
+  }
   if (valid && h == 0) {
     float* dst = p.x_out + ((size_t)yi * p.n_chains + c_local) * D;
 #pragma unroll
@@ -433,7 +465,8 @@ template <int W, int NL, int D, int NW, int R, bool RES>
 static hipError_t launch_sampler_t(const SamplerParams& p, int n_y, hipStream_t st) {
   const long long per_wg = NW * 32;
   dim3 grid((unsigned)((p.n_chains + per_wg - 1) / per_wg), (unsigned)n_y);
-  if (p.noise) hipLaunchKernelGGL((em_sampler_kernel<W, NL, D, NW, R, RES, true>), grid, dim3(NW * 64), 0, st, p);
+  if (p.stamps) hipLaunchKernelGGL((em_sampler_kernel<W, NL, D, NW, R, RES, false, true>), grid, dim3(NW * 64), 0, st, p);
+  else if (p.noise) hipLaunchKernelGGL((em_sampler_kernel<W, NL, D, NW, R, RES, true>), grid, dim3(NW * 64), 0, st, p);
   else hipLaunchKernelGGL((em_sampler_kernel<W, NL, D, NW, R, RES, false>), grid, dim3(NW * 64), 0, st, p);
   return hipGetLastError();
 }

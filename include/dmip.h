@@ -97,6 +97,14 @@ int dmip_rng_normals(uint64_t seed, int64_t chain_offset, uint64_t stream_id, in
  * (models/diffusion.py:34, sdes.py:21-35). */
 int dmip_schedule(int num_steps, const dmip_vpsde* sde, float* out_dev, void* stream);
 
+/* Diagnostic build of the sampler (same math, internal RNG, chain_offset 0) that also writes per-wave
+ * cycle sums of the three step phases [layer 1, hidden layers, output layer + EM update] to
+ * stamps_dev[(workgroup * waves_per_workgroup + wave) * 3 + phase] (s_memtime ticks). Never used on the
+ * product path; its run time is not representative (the stamps serialise the phases). */
+int dmip_em_sample_stamps(const dmip_mlp* net, const dmip_vpsde* sde, const float* y_dev, int n_y, int ydim,
+                          int xdim, int64_t n_chains, int num_steps, uint64_t seed, float* x_out_dev,
+                          uint64_t* stamps_dev, void* stream);
+
 const char* dmip_last_error(void);
 int dmip_abi_version(void);
 /* Non-zero when this build has a kernel for the given sampler shape. */
