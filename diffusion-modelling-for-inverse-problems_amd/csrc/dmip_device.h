@@ -139,12 +139,12 @@ __device__ __forceinline__ float act_r_twice(float zs) {
   return act_r(__builtin_fmaf(-2.0f * kTanhScale, q, kTanhScale));
 }
 
-template <bool TWICE>
+template <bool TWICE, bool CAST_ONLY = false>
 __device__ __forceinline__ void act_pack(const f32x16& acc, bf16x8& lo, bf16x8& hi) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const float a = TWICE ? act_r_twice(acc[j]) : act_r(acc[j]);
-    const float b = TWICE ? act_r_twice(acc[8 + j]) : act_r(acc[8 + j]);
+    const float a = CAST_ONLY ? acc[j] : (TWICE ? act_r_twice(acc[j]) : act_r(acc[j]));
+    const float b = CAST_ONLY ? acc[8 + j] : (TWICE ? act_r_twice(acc[8 + j]) : act_r(acc[8 + j]));
     lo[j] = (__bf16)a;
     hi[j] = (__bf16)b;
   }

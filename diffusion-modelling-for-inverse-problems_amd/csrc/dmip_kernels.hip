@@ -79,7 +79,9 @@ __device__ __forceinline__ void mfma_row_tile(const char* a_lane, const bf16x8 (
 // ------------------------------------------------------------------- one network evaluation
 // Hidden W x W layers + output layer, given layer-1 activations in H0. Returns the output
 // accumulator tile (rows = output dims, see the host packers for the row maps).
-template <int W, int NL, int K1S, int NW, int R, bool RES, bool CONSERVATIVE>
+// DIAG (timing ablations only, never on the product path): bit 0 = no ring barrier/DMA,
+// bit 1 = hidden activations replaced by a bf16 cast, bit 2 = layer-1 activation replaced by a cast.
+template <int W, int NL, int K1S, int NW, int R, bool RES, bool CONSERVATIVE, int DIAG = 0>
 struct Net {
   using L = Lay<W, NL, K1S, R, RES>;
   static constexpr int T = L::T;
@@ -94,6 +96,9 @@ struct Net {
   __device__ __forceinline__ const char* chunk_sync() {
     if constexpr (RES) {
       return nullptr;
+    } else if constexpr (DIAG & 1) {
+      asm volatile("" ::: "memory");
+      return lds + L::W_OFF + (int)((gc++) % R) * L::CHUNK;
     } else {
       if constexpr (CONSERVATIVE) wait_vmcnt<0>();
       else wait_vmcnt<(R - 2) * PPW>();
@@ -130,10 +135,10 @@ struct Net {
       f32x16 acc = bias_tile(L::BH_OFF + ((LI * T + rt) * 2) * 64);
       mfma_row_tile<KS>(wb + lane * 16, Hin, acc);
       // activation of the previous tile overlaps this tile's MFMAs
-      if (rt > 0) act_pack<false>(pend, Hout[2 * (rt - 1)], Hout[2 * (rt - 1) + 1]);
+      if (rt > 0) act_pack<false, (DIAG & 2) != 0>(pend, Hout[2 * (rt - 1)], Hout[2 * (rt - 1) + 1]);
       pend = acc;
     }
-    act_pack<false>(pend, Hout[2 * (T - 1)], Hout[2 * (T - 1) + 1]);
+    act_pack<false, (DIAG & 2) != 0>(pend, Hout[2 * (T - 1)], Hout[2 * (T - 1) + 1]);
   }
 
   template <int LI>
@@ -160,10 +165,10 @@ struct Net {
         const bf16x8 a = *(const bf16x8*)(lds + L::A1_OFF + (rt * K1S + s) * 1024 + lane * 16);
         acc = mfma32(a, B1[s], acc);
       }
-      if (rt > 0) act_pack<true>(pend, H[2 * (rt - 1)], H[2 * (rt - 1) + 1]);
+      if (rt > 0) act_pack<true, (DIAG & 4) != 0>(pend, H[2 * (rt - 1)], H[2 * (rt - 1) + 1]);
       pend = acc;
     }
-    act_pack<true>(pend, H[2 * (T - 1)], H[2 * (T - 1) + 1]);
+    act_pack<true, (DIAG & 4) != 0>(pend, H[2 * (T - 1)], H[2 * (T - 1) + 1]);
   }
 
   __device__ __forceinline__ f32x16 eval(const bf16x8 (&B1)[K1S]) {
@@ -240,7 +245,7 @@ __device__ __forceinline__ unsigned long long stamp() {
 
 // STAMP: diagnostic build only (dmip_em_sample_stamps) -- per-wave cycle sums of the step phases
 // [layer 1 + B1, hidden layers, output layer + RNG + EM update], written to p.stamps.
-template <int W, int NL, int D, int NW, int R, bool RES, bool NOISE, bool STAMP = false>
+template <int W, int NL, int D, int NW, int R, bool RES, bool NOISE, bool STAMP = false, int DIAG = 0>
 __global__ void __launch_bounds__(NW * 64, (NW * 64 + 255) / 256)
 em_sampler_kernel(SamplerParams p) {
   constexpr int K1S = (3 * (D + 1) + 2 + 15) / 16;
@@ -257,7 +262,7 @@ em_sampler_kernel(SamplerParams p) {
   const long long c_local = (long long)blockIdx.x * (NW * 32) + w * 32 + (lane & 31);
   const bool valid = c_local < p.n_chains;
 
-  Net<W, NL, K1S, NW, R, RES, NOISE> net{lds, p.hidden, 0, w, lane};
+  Net<W, NL, K1S, NW, R, RES, NOISE, DIAG> net{lds, p.hidden, 0, w, lane};
   net.prologue(p.a1 + (size_t)yi * L::T * K1S * 1024, p.ao, p.bias_hidden, p.bias_out);
 
   float x[D];
@@ -498,9 +503,20 @@ static int sampler_variant() {
 hipError_t launch_sampler(const SamplerParams& p, int width, int n_hidden, int xdim, int n_y, hipStream_t st,
                           bool* supported) {
   *supported = true;
-  if (width == 256 && sampler_variant() == 1) {
+  const int var = sampler_variant();
+  if (width == 256 && var == 1) {
     if (n_hidden == 3 && xdim == 3) return launch_sampler_t<256, 3, 3, 4, 3, false>(p, n_y, st);
     if (n_hidden == 3 && xdim == 2) return launch_sampler_t<256, 3, 2, 4, 3, false>(p, n_y, st);
+  }
+  if (width == 256 && n_hidden == 3 && xdim == 3 && var >= 100 && var < 108) {
+    dim3 grid((unsigned)((p.n_chains + 255) / 256), (unsigned)n_y);
+    switch (var - 100) {
+#define DG(d) case d: hipLaunchKernelGGL((em_sampler_kernel<256, 3, 3, 8, 4, false, false, false, d>), grid, dim3(512), 0, st, p); break;
+      DG(1) DG(2) DG(3) DG(4) DG(5) DG(6) DG(7)
+#undef DG
+      default: break;
+    }
+    return hipGetLastError();
   }
 #define X(Wv, NLv, Dv, NWv, Rv, RESv) \
   if (width == Wv && n_hidden == NLv && xdim == Dv) return launch_sampler_t<Wv, NLv, Dv, NWv, Rv, RESv>(p, n_y, st);
