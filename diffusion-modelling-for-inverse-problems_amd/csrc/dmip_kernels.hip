@@ -81,7 +81,7 @@ __device__ __forceinline__ void mfma_row_tile(const char* a_lane, const bf16x8 (
 // accumulator tile (rows = output dims, see the host packers for the row maps).
 // DIAG (timing ablations only, never on the product path): bit 0 = no ring barrier/DMA,
 // bit 1 = hidden activations replaced by a bf16 cast, bit 2 = layer-1 activation replaced by a cast.
-template <int W, int NL, int K1S, int NW, int R, bool RES, bool CONSERVATIVE, int DIAG = 0>
+template <int W, int NL, int K1S, int NW, int R, bool RES, bool CONSERVATIVE, int DIAG = 0, int ORD_MODE = 0>
 struct Net {
   using L = Lay<W, NL, K1S, R, RES>;
   static constexpr int T = L::T;
@@ -118,7 +118,11 @@ struct Net {
     return acc;
   }
 
-  template <int LI>
+  // ORDER 0: a chunk's MFMAs are issued first and the previous tile's activation after them;
+  // ORDER 1: activation first, then the MFMAs. Waves 0-3 and 4-7 (one of each per SIMD) use
+  // opposite orders, so a SIMD's matrix pipe and VALU are busy at the same time instead of both
+  // waves wanting the same pipe in lockstep.
+  template <int LI, int ORDER>
   __device__ __forceinline__ void hidden_layer(const bf16x8 (&Hin)[KS], bf16x8 (&Hout)[KS]) {
     f32x16 pend;
 #pragma unroll
@@ -132,24 +136,32 @@ struct Net {
       } else {
         wb = chunk_sync();
       }
+      if constexpr (ORDER == 1) {
+        if (rt > 0) act_pack<false, (DIAG & 2) != 0>(pend, Hout[2 * (rt - 1)], Hout[2 * (rt - 1) + 1]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
       f32x16 acc = bias_tile(L::BH_OFF + ((LI * T + rt) * 2) * 64);
       mfma_row_tile<KS>(wb + lane * 16, Hin, acc);
-      // activation of the previous tile overlaps this tile's MFMAs
-      if (rt > 0) act_pack<false, (DIAG & 2) != 0>(pend, Hout[2 * (rt - 1)], Hout[2 * (rt - 1) + 1]);
+      if constexpr (ORDER == 0) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (rt > 0) act_pack<false, (DIAG & 2) != 0>(pend, Hout[2 * (rt - 1)], Hout[2 * (rt - 1) + 1]);
+      } else if constexpr (ORDER == 2) {  // compiler-scheduled interleave (previous behaviour)
+        if (rt > 0) act_pack<false, (DIAG & 2) != 0>(pend, Hout[2 * (rt - 1)], Hout[2 * (rt - 1) + 1]);
+      }
       pend = acc;
     }
     act_pack<false, (DIAG & 2) != 0>(pend, Hout[2 * (T - 1)], Hout[2 * (T - 1) + 1]);
   }
 
-  template <int LI>
+  template <int LI, int ORDER>
   __device__ __forceinline__ void hidden_chain(bf16x8 (&Ha)[KS], bf16x8 (&Hb)[KS], f32x16& out) {
     if constexpr (LI == NL - 1) {  // all W x W layers done: output layer
       asm volatile("" ::: "memory");
       out = bias_tile(L::BO_OFF);
       mfma_row_tile<KS>(lds + L::AO_OFF + lane * 16, Ha, out);
     } else {
-      hidden_layer<LI>(Ha, Hb);
-      hidden_chain<LI + 1>(Hb, Ha, out);
+      hidden_layer<LI, ORDER>(Ha, Hb);
+      hidden_chain<LI + 1, ORDER>(Hb, Ha, out);
     }
   }
 
@@ -171,11 +183,21 @@ struct Net {
     act_pack<true, (DIAG & 4) != 0>(pend, H[2 * (T - 1)], H[2 * (T - 1) + 1]);
   }
 
+  // hidden layers + output with the wave-group instruction order (see hidden_layer)
+  __device__ __forceinline__ void hidden_all(bf16x8 (&Ha)[KS], bf16x8 (&Hb)[KS], f32x16& out) {
+    if constexpr (ORD_MODE == 2) {
+      hidden_chain<0, 2>(Ha, Hb, out);
+    } else {
+      if (w >= NW / 2) hidden_chain<0, 1>(Ha, Hb, out);
+      else hidden_chain<0, 0>(Ha, Hb, out);
+    }
+  }
+
   __device__ __forceinline__ f32x16 eval(const bf16x8 (&B1)[K1S]) {
     bf16x8 Ha[KS], Hb[KS];
     layer1(B1, Ha);
     f32x16 out;
-    hidden_chain<0>(Ha, Hb, out);
+    hidden_all(Ha, Hb, out);
     return out;
   }
 
@@ -245,7 +267,7 @@ __device__ __forceinline__ unsigned long long stamp() {
 
 // STAMP: diagnostic build only (dmip_em_sample_stamps) -- per-wave cycle sums of the step phases
 // [layer 1 + B1, hidden layers, output layer + RNG + EM update], written to p.stamps.
-template <int W, int NL, int D, int NW, int R, bool RES, bool NOISE, bool STAMP = false, int DIAG = 0>
+template <int W, int NL, int D, int NW, int R, bool RES, bool NOISE, bool STAMP = false, int DIAG = 0, int ORD = 0>
 __global__ void __launch_bounds__(NW * 64, (NW * 64 + 255) / 256)
 em_sampler_kernel(SamplerParams p) {
   constexpr int K1S = (3 * (D + 1) + 2 + 15) / 16;
@@ -262,7 +284,7 @@ em_sampler_kernel(SamplerParams p) {
   const long long c_local = (long long)blockIdx.x * (NW * 32) + w * 32 + (lane & 31);
   const bool valid = c_local < p.n_chains;
 
-  Net<W, NL, K1S, NW, R, RES, NOISE, DIAG> net{lds, p.hidden, 0, w, lane};
+  Net<W, NL, K1S, NW, R, RES, NOISE, DIAG, ORD> net{lds, p.hidden, 0, w, lane};
   net.prologue(p.a1 + (size_t)yi * L::T * K1S * 1024, p.ao, p.bias_hidden, p.bias_out);
 
   float x[D];
@@ -292,7 +314,7 @@ em_sampler_kernel(SamplerParams p) {
     net.layer1(B1, Ha);
     if constexpr (STAMP) t1 = stamp();
     f32x16 out;
-    net.template hidden_chain<0>(Ha, Hb, out);
+    net.hidden_all(Ha, Hb, out);
     if constexpr (STAMP) t2 = stamp();
     float xi[D];
     if constexpr (NOISE) {
@@ -516,6 +538,11 @@ hipError_t launch_sampler(const SamplerParams& p, int width, int n_hidden, int x
 #undef DG
       default: break;
     }
+    return hipGetLastError();
+  }
+  if (width == 256 && n_hidden == 3 && xdim == 3 && var == 2) {  // previous compiler-interleaved order
+    dim3 grid((unsigned)((p.n_chains + 255) / 256), (unsigned)n_y);
+    hipLaunchKernelGGL((em_sampler_kernel<256, 3, 3, 8, 4, false, false, false, 0, 2>), grid, dim3(512), 0, st, p);
     return hipGetLastError();
   }
 #define X(Wv, NLv, Dv, NWv, Rv, RESv) \
