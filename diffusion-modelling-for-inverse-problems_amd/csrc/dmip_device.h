@@ -161,11 +161,15 @@ __device__ __forceinline__ void wait_vmcnt() {
 
 __device__ __forceinline__ void lds_barrier() {
   // all of this wave's LDS reads have returned, then a raw workgroup barrier. The asm memory
-  // clobbers keep the compiler from moving LDS accesses across it; no vmcnt(0) is implied, so
+  // clobbers keep the compiler from moving LDS accesses across it and the sched_barriers keep
+  // register-only instructions (MFMAs) on their side too -- otherwise the last MFMAs of a tile
+  // slide past the barrier and the next activation stalls on them. No vmcnt(0) is implied, so
   // LDS-DMA weight prefetches stay in flight across the barrier.
+  __builtin_amdgcn_sched_barrier(0);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
 }
 
 typedef __attribute__((address_space(3))) void lds_void;

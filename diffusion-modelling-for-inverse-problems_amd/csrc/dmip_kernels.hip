@@ -147,6 +147,18 @@ struct Net {
         if (rt > 0) act_pack<false, (DIAG & 2) != 0>(pend, Hout[2 * (rt - 1)], Hout[2 * (rt - 1) + 1]);
       } else if constexpr (ORDER == 2) {  // compiler-scheduled interleave (previous behaviour)
         if (rt > 0) act_pack<false, (DIAG & 2) != 0>(pend, Hout[2 * (rt - 1)], Hout[2 * (rt - 1) + 1]);
+      } else if constexpr (ORDER >= 3) {
+        // pinned interleave: the bias / first fragment reads, then per MFMA one LDS read and VPM
+        // VALU instructions of the previous tile's activation (ORDER 3: 4, ORDER 4: 6, ORDER 5: 3)
+        if (rt > 0) act_pack<false, (DIAG & 2) != 0>(pend, Hout[2 * (rt - 1)], Hout[2 * (rt - 1) + 1]);
+        constexpr int VPM = ORDER == 3 ? 4 : (ORDER == 4 ? 6 : 3);
+        __builtin_amdgcn_sched_group_barrier(0x100, 7, 0);
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, VPM, 0);
+        }
       }
       pend = acc;
     }
@@ -185,8 +197,8 @@ struct Net {
 
   // hidden layers + output with the wave-group instruction order (see hidden_layer)
   __device__ __forceinline__ void hidden_all(bf16x8 (&Ha)[KS], bf16x8 (&Hb)[KS], f32x16& out) {
-    if constexpr (ORD_MODE == 2) {
-      hidden_chain<0, 2>(Ha, Hb, out);
+    if constexpr (ORD_MODE >= 2) {
+      hidden_chain<0, ORD_MODE>(Ha, Hb, out);
     } else {
       if (w >= NW / 2) hidden_chain<0, 1>(Ha, Hb, out);
       else hidden_chain<0, 0>(Ha, Hb, out);
@@ -540,9 +552,12 @@ hipError_t launch_sampler(const SamplerParams& p, int width, int n_hidden, int x
     }
     return hipGetLastError();
   }
-  if (width == 256 && n_hidden == 3 && xdim == 3 && var == 2) {  // previous compiler-interleaved order
+  if (width == 256 && n_hidden == 3 && xdim == 3 && var >= 2 && var <= 5) {  // instruction-order variants
     dim3 grid((unsigned)((p.n_chains + 255) / 256), (unsigned)n_y);
-    hipLaunchKernelGGL((em_sampler_kernel<256, 3, 3, 8, 4, false, false, false, 0, 2>), grid, dim3(512), 0, st, p);
+    if (var == 2) hipLaunchKernelGGL((em_sampler_kernel<256, 3, 3, 8, 4, false, false, false, 0, 2>), grid, dim3(512), 0, st, p);
+    if (var == 3) hipLaunchKernelGGL((em_sampler_kernel<256, 3, 3, 8, 4, false, false, false, 0, 3>), grid, dim3(512), 0, st, p);
+    if (var == 4) hipLaunchKernelGGL((em_sampler_kernel<256, 3, 3, 8, 4, false, false, false, 0, 4>), grid, dim3(512), 0, st, p);
+    if (var == 5) hipLaunchKernelGGL((em_sampler_kernel<256, 3, 3, 8, 4, false, false, false, 0, 5>), grid, dim3(512), 0, st, p);
     return hipGetLastError();
   }
 #define X(Wv, NLv, Dv, NWv, Rv, RESv) \
