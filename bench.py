@@ -55,6 +55,19 @@ def synthetic_y():
     return np.abs(np.random.default_rng(13).normal(0.3, 0.4, YDIM)).astype(np.float32)
 
 
+def pmc_traffic(kernel_match="em_sampler"):
+    """HBM bytes per launch of the sampler kernel from the committed rocprofv3 PMC summary
+    (profiles/pmc_summary_latest.json, written by scripts/pmc_summary.py from separate --pmc
+    passes on the same workload), or None."""
+    p = os.path.join(ROOT, "profiles", "pmc_summary_latest.json")
+    if not os.path.exists(p):
+        return None
+    z = json.load(open(p))
+    if kernel_match not in z.get("kernel_match", "") or "hbm_bytes_per_launch" not in z:
+        return None
+    return z["hbm_bytes_per_launch"]
+
+
 def cpu_baseline(num_steps, n_chains):
     """Reference-order torch-CPU sampler (oracle/torch_cpu.py) on a bounded sample."""
     from oracle import torch_cpu
@@ -163,7 +176,7 @@ def main():
                    "parallelism": f"sample-parallel x{world}" + (" + RCCL all_gather" if world > 1 else ""),
                    "arith": "bf16 MFMA operands, fp32 accumulate; fp32 chain state / SDE update"},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / PEAK_BF16_TFLOPS, "traffic": None,
+                     "frac": achieved / PEAK_BF16_TFLOPS, "traffic": pmc_traffic(),
                      "kernel": "em_sampler_kernel<256,3,3,8,4> (+a1_prep, inside the events)",
                      "launch_ms": launch_ms, "flops_per_launch": flops_launch},
     }

@@ -316,6 +316,11 @@ em_sampler_kernel(SamplerParams p) {
   const size_t noise_step = (size_t)gridDim.y * p.n_chains * D;
 
   unsigned long long ph[3] = {0, 0, 0};
+  unsigned long long clk0 = 0, rt0 = 0;
+  if constexpr (STAMP) {
+    clk0 = stamp();
+    rt0 = __builtin_amdgcn_s_memrealtime();
+  }
   for (int i = 0; i < p.num_steps; ++i) {
     unsigned long long t0 = 0, t1 = 0, t2 = 0;
     if constexpr (STAMP) t0 = stamp();
@@ -347,11 +352,15 @@ em_sampler_kernel(SamplerParams p) {
   }
   net.epilogue();
   if constexpr (STAMP) {
+    const unsigned long long clk1 = stamp();
+    const unsigned long long rt1 = __builtin_amdgcn_s_memrealtime();
     if (lane == 0) {
-      unsigned long long* o = p.stamps + ((size_t)(blockIdx.y * gridDim.x + blockIdx.x) * NW + w) * 3;
+      unsigned long long* o = p.stamps + ((size_t)(blockIdx.y * gridDim.x + blockIdx.x) * NW + w) * 5;
       o[0] = ph[0];
       o[1] = ph[1];
       o[2] = ph[2];
+      o[3] = clk1 - clk0;  // shader clock ticks over the step loop
+      o[4] = rt1 - rt0;    // 100 MHz constant clock over the same span
     }
   }
   if (valid && h == 0) {

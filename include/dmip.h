@@ -98,9 +98,10 @@ int dmip_rng_normals(uint64_t seed, int64_t chain_offset, uint64_t stream_id, in
 int dmip_schedule(int num_steps, const dmip_vpsde* sde, float* out_dev, void* stream);
 
 /* Diagnostic build of the sampler (same math, internal RNG, chain_offset 0) that also writes per-wave
- * cycle sums of the three step phases [layer 1, hidden layers, output layer + EM update] to
- * stamps_dev[(workgroup * waves_per_workgroup + wave) * 3 + phase] (s_memtime ticks). Never used on the
- * product path; its run time is not representative (the stamps serialise the phases). */
+ * cycle sums of the three step phases [layer 1, hidden layers, output layer + EM update], then the
+ * s_memtime and s_memrealtime (100 MHz) spans of the whole step loop, to
+ * stamps_dev[(workgroup * waves_per_workgroup + wave) * 5 + k]. Never used on the product path; its
+ * run time is not representative (the stamps serialise the phases). */
 int dmip_em_sample_stamps(const dmip_mlp* net, const dmip_vpsde* sde, const float* y_dev, int n_y, int ydim,
                           int xdim, int64_t n_chains, int num_steps, uint64_t seed, float* x_out_dev,
                           uint64_t* stamps_dev, void* stream);

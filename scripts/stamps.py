@@ -29,18 +29,20 @@ def main():
     y = torch.from_numpy(np.load(os.path.join(ROOT, "tests/golden/data_scat.npz"))["y_test"][0]).to(dev).reshape(1, -1)
     h = m.sde.a.dmip_handle(dev, 3)
     n_wave = ((a.chains + 255) // 256) * 8
-    st = torch.zeros(n_wave, 3, dtype=torch.int64, device=dev)
+    st = torch.zeros(n_wave, 5, dtype=torch.int64, device=dev)
     out = torch.empty(1, a.chains, 3, device=dev)
     sde = L.vpsde(0.1, 20.0, 1.0)
     for _ in range(2):
         L.check(L.lib().dmip_em_sample_stamps(h.h, ctypes.byref(sde), L.ptr(y), 1, 23, 3, a.chains, a.steps, 1,
                                               L.ptr(out), L.ptr(st), L.stream_of(dev)))
     torch.cuda.synchronize()
-    s = st.cpu().numpy().astype(np.float64) / a.steps
+    raw = st.cpu().numpy().astype(np.float64)
+    s = raw[:, :3] / a.steps
     names = ["layer1+B1", "hidden+output", "rng+em"]
     res = {n: {"mean_cycles_per_step": float(s[:, i].mean()), "p10": float(np.percentile(s[:, i], 10)),
                "p90": float(np.percentile(s[:, i], 90))} for i, n in enumerate(names)}
     res["total_mean"] = float(s.sum(1).mean())
+    res["shader_clock_GHz"] = float(np.median(raw[:, 3] / raw[:, 4] * 0.1))
     print(json.dumps(res, indent=1))
 
 
