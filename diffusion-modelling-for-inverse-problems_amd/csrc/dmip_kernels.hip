@@ -81,7 +81,7 @@ __device__ __forceinline__ void mfma_row_tile(const char* a_lane, const bf16x8 (
 // accumulator tile (rows = output dims, see the host packers for the row maps).
 // DIAG (timing ablations only, never on the product path): bit 0 = no ring barrier/DMA,
 // bit 1 = hidden activations replaced by a bf16 cast, bit 2 = layer-1 activation replaced by a cast.
-template <int W, int NL, int K1S, int NW, int R, bool RES, bool CONSERVATIVE, int DIAG = 0, int ORD_MODE = 0>
+template <int W, int NL, int K1S, int NW, int R, bool RES, bool CONSERVATIVE, int DIAG = 0, int ORD_MODE = 2>
 struct Net {
   using L = Lay<W, NL, K1S, R, RES>;
   static constexpr int T = L::T;
@@ -279,7 +279,7 @@ __device__ __forceinline__ unsigned long long stamp() {
 
 // STAMP: diagnostic build only (dmip_em_sample_stamps) -- per-wave cycle sums of the step phases
 // [layer 1 + B1, hidden layers, output layer + RNG + EM update], written to p.stamps.
-template <int W, int NL, int D, int NW, int R, bool RES, bool NOISE, bool STAMP = false, int DIAG = 0, int ORD = 0>
+template <int W, int NL, int D, int NW, int R, bool RES, bool NOISE, bool STAMP = false, int DIAG = 0, int ORD = 2>
 __global__ void __launch_bounds__(NW * 64, (NW * 64 + 255) / 256)
 em_sampler_kernel(SamplerParams p) {
   constexpr int K1S = (3 * (D + 1) + 2 + 15) / 16;
@@ -563,7 +563,7 @@ hipError_t launch_sampler(const SamplerParams& p, int width, int n_hidden, int x
   }
   if (width == 256 && n_hidden == 3 && xdim == 3 && var >= 2 && var <= 5) {  // instruction-order variants
     dim3 grid((unsigned)((p.n_chains + 255) / 256), (unsigned)n_y);
-    if (var == 2) hipLaunchKernelGGL((em_sampler_kernel<256, 3, 3, 8, 4, false, false, false, 0, 2>), grid, dim3(512), 0, st, p);
+    if (var == 2) hipLaunchKernelGGL((em_sampler_kernel<256, 3, 3, 8, 4, false, false, false, 0, 0>), grid, dim3(512), 0, st, p);
     if (var == 3) hipLaunchKernelGGL((em_sampler_kernel<256, 3, 3, 8, 4, false, false, false, 0, 3>), grid, dim3(512), 0, st, p);
     if (var == 4) hipLaunchKernelGGL((em_sampler_kernel<256, 3, 3, 8, 4, false, false, false, 0, 4>), grid, dim3(512), 0, st, p);
     if (var == 5) hipLaunchKernelGGL((em_sampler_kernel<256, 3, 3, 8, 4, false, false, false, 0, 5>), grid, dim3(512), 0, st, p);
