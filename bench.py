@@ -102,7 +102,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--chains", type=int, default=100000, help="chains per GPU")
     ap.add_argument("--num-steps", type=int, default=1000, help="SDE steps per sample")
-    ap.add_argument("--cpu-chains", type=int, default=4096)
+    ap.add_argument("--cpu-chains", type=int, default=16384)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
