@@ -1,0 +1,53 @@
+"""The reference-name shim: the reference's own driver scripts import and resolve every name to this
+package (CPU only; needs the reference checkout, which exists only in the build container)."""
+import os
+import runpy
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+REF = os.environ.get("DMIP_REFERENCE", "/root/reference")
+SHIM = os.path.join(ROOT, "diffusion-modelling-for-inverse-problems_amd", "refapi")
+
+
+@pytest.fixture()
+def shim_path(monkeypatch):
+    monkeypatch.syspath_prepend(SHIM)
+    for name in ["utils", "nets", "sdes", "losses", "linear_problem", "utils_scatterometry", "datasets",
+                 "models", "models.diffusion", "models.SNF", "_base"]:
+        sys.modules.pop(name, None)
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import run_reference_driver
+    run_reference_driver.install_tensorboard_stub()
+    yield
+    for name in ["utils", "nets", "sdes", "losses", "linear_problem", "utils_scatterometry", "datasets",
+                 "models", "models.diffusion", "models.SNF", "_base"]:
+        sys.modules.pop(name, None)
+
+
+def test_shim_modules_resolve_to_package(shim_path, dmip):
+    import utils
+    import models.diffusion as md
+    from models.SNF import energy_grad
+    import linear_problem
+    import losses
+    assert md.CDE is dmip.CDE and md.PosteriorDiffusionEstimator is dmip.PosteriorDiffusionEstimator
+    assert utils.get_model_from_args is dmip.get_model_from_args
+    assert losses.PINNLoss is dmip.PINNLoss and losses.DSMLoss is dmip.DSMLoss
+    assert linear_problem.LinearForwardProblem().xdim == 2
+    assert callable(energy_grad)
+
+
+@pytest.mark.parametrize("script", ["main_diffusion_linear.py", "main_diffusion_scatterometry.py"])
+def test_reference_drivers_import_against_shim(shim_path, dmip, script, monkeypatch):
+    path = os.path.join(REF, script)
+    if not os.path.exists(path):
+        pytest.skip("reference checkout not present (GPU box)")
+    monkeypatch.chdir(REF)
+    ns = runpy.run_path(path, run_name="not_main")  # defines train/evaluate, does not run them
+    assert callable(ns["train"]) and callable(ns["evaluate"])
+    assert ns["utils"].get_model_from_args is dmip.get_model_from_args
+    if "CDE" in ns:
+        assert ns["CDE"] is dmip.CDE
