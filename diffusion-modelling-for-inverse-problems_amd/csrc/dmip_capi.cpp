@@ -192,23 +192,30 @@ int dmip_mlp_create(int in_dim, int out_dim, int n_hidden, const int* widths, in
   const float* W1 = weights[0];
   const float* b1 = biases[0];
   const int IN = in_dim;
-  net->k1s_full = k1s_for(3 * IN + 2);
+  const bool split = dmip::forward_split(W, IN);
+  net->k1s_full = split ? k1s_for(3 * IN + 2) : k1s_for(IN + 2);
   const int K1S = net->k1s_full;
   std::vector<uint16_t> a1f((size_t)T * K1S * 512, 0);
   for (int jr = 0; jr < W; ++jr) {
     const int rt = jr / 32, i = jr % 32;
     for (int k = 0; k < K1S * 16; ++k) {
       float val = 0.0f;
-      auto split = [&](double v, bool lo) {
+      auto hilo = [&](double v, bool lo) {
         const float f = (float)v;
         const uint16_t hi = f2bf(f);
         return lo ? bf2f(f2bf(f - bf2f(hi))) : bf2f(hi);
       };
-      if (k < IN) val = split(kC * W1[(size_t)jr * IN + k], false);
-      else if (k < 2 * IN) val = split(kC * W1[(size_t)jr * IN + k - IN], false);
-      else if (k < 3 * IN) val = split(kC * W1[(size_t)jr * IN + k - 2 * IN], true);
-      else if (k == 3 * IN) val = split(kC * b1[jr], false);
-      else if (k == 3 * IN + 1) val = split(kC * b1[jr], true);
+      if (split) {
+        if (k < IN) val = hilo(kC * W1[(size_t)jr * IN + k], false);
+        else if (k < 2 * IN) val = hilo(kC * W1[(size_t)jr * IN + k - IN], false);
+        else if (k < 3 * IN) val = hilo(kC * W1[(size_t)jr * IN + k - 2 * IN], true);
+        else if (k == 3 * IN) val = hilo(kC * b1[jr], false);
+        else if (k == 3 * IN + 1) val = hilo(kC * b1[jr], true);
+      } else {  // [v | 1 | 1] x [W | b_hi | b_lo]
+        if (k < IN) val = hilo(kC * W1[(size_t)jr * IN + k], false);
+        else if (k == IN) val = hilo(kC * b1[jr], false);
+        else if (k == IN + 1) val = hilo(kC * b1[jr], true);
+      }
       const int s = k / 16, hh = (k % 16) / 8, jj = k % 8;
       a1f[(((size_t)(rt * K1S + s)) * 64 + i + 32 * hh) * 8 + jj] = f2bf(val);
     }

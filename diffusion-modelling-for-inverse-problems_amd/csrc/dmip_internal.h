@@ -48,6 +48,7 @@ struct A1PrepParams {
 hipError_t launch_sampler(const SamplerParams& p, int width, int n_hidden, int xdim, int n_y, hipStream_t st,
                           bool* supported);
 bool sampler_shape_supported(int width, int n_hidden, int xdim);
+bool forward_split(int width, int in_dim);
 hipError_t launch_forward(const ForwardParams& p, int width, int n_hidden, int in_dim, hipStream_t st,
                           bool* supported);
 hipError_t launch_a1_prep(const A1PrepParams& p, int n_y, hipStream_t st);

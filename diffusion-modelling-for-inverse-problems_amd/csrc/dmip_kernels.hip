@@ -373,10 +373,12 @@ em_sampler_kernel(SamplerParams p) {
 // ---------------------------------------------------------------------- MLP forward kernel
 // out[n] = MLP(cat[x, y, t]) for arbitrary rows (model.sde.a(x, y, t), nets.py:32-35); every
 // input column varies per row, so layer 1 takes the whole row as split-bf16 slots.
-template <int W, int NL, int IN, int NW, int R, bool RES>
+template <int W, int NL, int IN, int NW, int R, bool RES, bool SPLIT = true>
 __global__ void __launch_bounds__(NW * 64, (NW * 64 + 255) / 256)
 mlp_forward_kernel(ForwardParams p) {
-  constexpr int K1S = (3 * IN + 2 + 15) / 16;
+  // SPLIT: layer-1 slots [hi(v) | lo(v) | hi(v) | 1 | 1] (~fp32); otherwise [v | 1 | 1] (bf16 inputs,
+  // used where the split image does not fit the LDS budget: width 512 with wide inputs)
+  constexpr int K1S = SPLIT ? (3 * IN + 2 + 15) / 16 : (IN + 2 + 15) / 16;
   using L = Lay<W, NL, K1S, R, RES>;
   static_assert(L::TOTAL <= 160 * 1024, "LDS budget");
   __shared__ __attribute__((aligned(16))) char lds[L::TOTAL];
@@ -414,10 +416,15 @@ mlp_forward_kernel(ForwardParams p) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         auto slot = [&](int k) -> __bf16 {
-          if (k < IN) return vh[k];
-          if (k < 2 * IN) return vl[k - IN];
-          if (k < 3 * IN) return vh[k - 2 * IN];
-          if (k < 3 * IN + 2) return (__bf16)1.0f;
+          if constexpr (SPLIT) {
+            if (k < IN) return vh[k];
+            if (k < 2 * IN) return vl[k - IN];
+            if (k < 3 * IN) return vh[k - 2 * IN];
+            if (k < 3 * IN + 2) return (__bf16)1.0f;
+          } else {
+            if (k < IN) return vh[k];
+            if (k < IN + 2) return (__bf16)1.0f;
+          }
           return (__bf16)0.0f;
         };
         B1[s][j] = h ? slot(16 * s + 8 + j) : slot(16 * s + j);
@@ -519,13 +526,13 @@ static hipError_t launch_sampler_t(const SamplerParams& p, int n_y, hipStream_t 
   return hipGetLastError();
 }
 
-template <int W, int NL, int IN, int NW, int R, bool RES>
+template <int W, int NL, int IN, int NW, int R, bool RES, bool SPLIT = true>
 static hipError_t launch_forward_t(const ForwardParams& p, hipStream_t st) {
   const long long tiles = (p.n + 31) / 32;
   long long wgs = (tiles + NW - 1) / NW;
   if (wgs > 2048) wgs = 2048;
   if (wgs < 1) wgs = 1;
-  hipLaunchKernelGGL((mlp_forward_kernel<W, NL, IN, NW, R, RES>), dim3((unsigned)wgs), dim3(NW * 64), 0, st, p);
+  hipLaunchKernelGGL((mlp_forward_kernel<W, NL, IN, NW, R, RES, SPLIT>), dim3((unsigned)wgs), dim3(NW * 64), 0, st, p);
   return hipGetLastError();
 }
 
@@ -534,7 +541,8 @@ static hipError_t launch_forward_t(const ForwardParams& p, hipStream_t st) {
 #define DMIP_W_CASES(X, NL, D) \
   X(64, NL, D, 8, 0, true)     \
   X(128, NL, D, 8, 0, true)    \
-  X(256, NL, D, 8, 4, false)
+  X(256, NL, D, 8, 4, false)   \
+  X(512, NL, D, 4, 3, false)
 
 // Development knob (not part of the ABI): DMIP_SAMPLER_VARIANT=1 runs width 256 as two
 // independent 4-wave workgroups per CU (each with its own 3-slot ring) instead of one 8-wave one.
@@ -591,11 +599,25 @@ bool sampler_shape_supported(int width, int n_hidden, int xdim) {
   return false;
 }
 
+constexpr bool forward_split_c(int width, int in_dim) { return width < 512 || 3 * in_dim + 2 <= 32; }
+bool forward_split(int width, int in_dim) { return forward_split_c(width, in_dim); }
+
 hipError_t launch_forward(const ForwardParams& p, int width, int n_hidden, int in_dim, hipStream_t st,
                           bool* supported) {
   *supported = true;
-#define X(Wv, NLv, INv, NWv, Rv, RESv) \
-  if (width == Wv && n_hidden == NLv && in_dim == INv) return launch_forward_t<Wv, NLv, INv, NWv, Rv, RESv>(p, st);
+  if (width == 512) {
+    // 32 KiB ring slots: two slots, and layer 1 split only while its image stays at 32 KiB
+#define X5(NLv, INv)              \
+    if (n_hidden == NLv && in_dim == INv) \
+      return launch_forward_t<512, NLv, INv, 4, 2, false, forward_split_c(512, INv)>(p, st);
+    X5(3, 5) X5(3, 27) X5(3, 3) X5(3, 4)
+#undef X5
+    *supported = false;
+    return hipSuccess;
+  }
+#define X(Wv, NLv, INv, NWv, Rv, RESv)                          \
+  if constexpr (Wv != 512)                                        \
+    if (width == Wv && n_hidden == NLv && in_dim == INv) return launch_forward_t<Wv, NLv, INv, NWv, Rv, RESv>(p, st);
   DMIP_W_CASES(X, 3, 5)   // linear CDE: x(2) y(2) t
   DMIP_W_CASES(X, 3, 27)  // scatterometry CDE: x(3) y(23) t
   DMIP_W_CASES(X, 3, 3)   // linear prior MLP2: x(2) t

@@ -238,3 +238,44 @@ def test_sampler_rejects_cpu_only(dmip):
     m.sde.a.to("cpu")
     with pytest.raises(RuntimeError):
         m.sample_device(torch.tensor([0.5, 1.0], device=DEV), 10, 2)
+
+
+# ----------------------------------------------------------- every compiled width vs the oracle
+def _seeded_cde(dmip, xd, yd, W, seed=0):
+    torch.manual_seed(seed)
+    m = dmip.CDE(xd, yd, [W] * 3)
+    return m, [(l.weight.detach().cpu().numpy(), l.bias.detach().cpu().numpy())
+               for l in m.sde.a if isinstance(l, torch.nn.Linear)]
+
+
+@pytest.mark.parametrize("W", [64, 128, 256, 512])
+@pytest.mark.parametrize("xd,yd", [(2, 2), (3, 23)])
+def test_forward_all_widths_vs_oracle(dmip, W, xd, yd):
+    m, params = _seeded_cde(dmip, xd, yd, W)
+    g = np.random.default_rng(W + xd)
+    n = 1000  # ragged: not a multiple of 32 x waves
+    x = g.normal(size=(n, xd)).astype(np.float32)
+    y = g.normal(size=(n, yd)).astype(np.float32)
+    t = g.uniform(size=(n, 1)).astype(np.float32)
+    with torch.no_grad():
+        a = m.sde.a(torch.from_numpy(x).to(DEV), torch.from_numpy(y).to(DEV), torch.from_numpy(t).to(DEV)).cpu().numpy()
+    ref = O.cde_a(params, x, y, t)
+    scale = _bf16_bound(params, np.concatenate([x, y, t], 1))
+    tol = 2.0 ** -7 * scale + 1e-5
+    if W == 512 and 3 * (xd + yd + 1) + 2 > 32:
+        tol = 2.0 ** -6 * scale + 1e-5  # width 512, wide input: layer-1 inputs in plain bf16
+    assert np.all(np.abs(a - ref) <= tol), np.abs(a - ref).max()
+
+
+@pytest.mark.parametrize("W", [64, 128, 256, 512])
+def test_sampler_all_widths_vs_oracle_product_rng(dmip, W):
+    """Same chains as the oracle (it restates the product RNG); 6 steps of an untrained net."""
+    xd, yd = 3, 23
+    m, params = _seeded_cde(dmip, xd, yd, W, seed=1)
+    y = np.random.default_rng(5).uniform(0, 1, yd).astype(np.float32)
+    n, S, seed = 700, 6, 99
+    x = m.sample_device(torch.from_numpy(y).to(DEV), n, S, seed=seed)[0].cpu().numpy()
+    ref = O.cde_sample(params, y, n, S, seed)
+    err = np.abs(x - ref)
+    assert np.all(np.isfinite(x))
+    assert err.max() < 0.02 * max(1.0, np.abs(ref).max()), err.max()
