@@ -19,12 +19,14 @@ DMIP_OK, DMIP_ERR_INVALID, DMIP_ERR_UNSUPPORTED, DMIP_ERR_HIP, DMIP_ERR_ALLOC = 
 DMIP_INPUT_X_Y_T, DMIP_INPUT_X_T = 0, 1
 DMIP_ACT_TANH_TWICE_FIRST, DMIP_ACT_TANH = 0, 1
 DMIP_PREC_BF16 = 0
+DMIP_SAMPLER_CDE, DMIP_SAMPLER_POSTERIOR, DMIP_SAMPLER_CDIFFE = 0, 1, 2
+ABI_VERSION = 2
 
 # every symbol include/dmip.h declares (checked by tests/test_capi.py)
 EXPORTED = (
     "dmip_mlp_create", "dmip_mlp_destroy", "dmip_mlp_forward", "dmip_em_sample", "dmip_rng_words",
     "dmip_rng_normals", "dmip_schedule", "dmip_last_error", "dmip_abi_version", "dmip_sampler_supported",
-    "dmip_em_sample_stamps",
+    "dmip_em_sample_stamps", "dmip_em_sample_posterior", "dmip_em_sample_cdiffe",
 )
 
 
@@ -38,13 +40,13 @@ _f32 = ctypes.c_float
 
 _lib = None
 _lock = threading.Lock()
-calls = {"em_sample": 0, "mlp_forward": 0}  # instrumentation: proves the HIP path ran
+calls = {"em_sample": 0, "mlp_forward": 0, "em_sample_posterior": 0, "em_sample_cdiffe": 0}  # instrumentation: proves the HIP path ran
 
 
 def _declare(lib):
     lib.dmip_last_error.restype = ctypes.c_char_p
     lib.dmip_abi_version.restype = _i32
-    lib.dmip_sampler_supported.argtypes = [_i32, _i32, _i32]
+    lib.dmip_sampler_supported.argtypes = [_i32, _i32, _i32, _i32, _i32]
     lib.dmip_mlp_create.argtypes = [_i32, _i32, _i32, ctypes.POINTER(_i32), _i32, _i32, _i32,
                                     ctypes.POINTER(_c_void_p), ctypes.POINTER(_c_void_p),
                                     ctypes.POINTER(_c_void_p)]
@@ -54,6 +56,11 @@ def _declare(lib):
     lib.dmip_em_sample.argtypes = [_c_void_p, ctypes.POINTER(DmipVpsde), _c_void_p, _i32, _i32, _i32,
                                    _i64, _i64, _i32, _f32, _f32, _u64, _i32, _c_void_p, _c_void_p,
                                    _c_void_p]
+    lib.dmip_em_sample_posterior.argtypes = [_c_void_p, _c_void_p, ctypes.POINTER(DmipVpsde), _c_void_p, _i32,
+                                             _i32, _i32, _i64, _i64, _i32, _f32, _f32, _u64, _i32, _c_void_p,
+                                             _c_void_p]
+    lib.dmip_em_sample_cdiffe.argtypes = [_c_void_p, ctypes.POINTER(DmipVpsde), _c_void_p, _i32, _i32, _i32,
+                                          _i64, _i64, _i32, _f32, _f32, _u64, _i32, _c_void_p, _c_void_p]
     lib.dmip_em_sample_stamps.argtypes = [_c_void_p, ctypes.POINTER(DmipVpsde), _c_void_p, _i32, _i32, _i32,
                                           _i64, _i32, _u64, _c_void_p, _c_void_p, _c_void_p]
     lib.dmip_rng_words.argtypes = [_u64, _i64, _u64, _i64, _i32, _c_void_p, _c_void_p]
@@ -61,7 +68,7 @@ def _declare(lib):
     lib.dmip_schedule.argtypes = [_i32, ctypes.POINTER(DmipVpsde), _c_void_p, _c_void_p]
     for name in ("dmip_mlp_create", "dmip_mlp_destroy", "dmip_mlp_forward", "dmip_em_sample",
                  "dmip_rng_words", "dmip_rng_normals", "dmip_schedule", "dmip_sampler_supported",
-                 "dmip_em_sample_stamps"):
+                 "dmip_em_sample_stamps", "dmip_em_sample_posterior", "dmip_em_sample_cdiffe"):
         getattr(lib, name).restype = _i32
 
 
@@ -154,5 +161,23 @@ def em_sample(handle, sde, y, n_chains, chain_offset, num_steps, mean, std, seed
                                DMIP_PREC_BF16, ptr(noise), ptr(out), stream_of(y.device)))
 
 
-def sampler_supported(width, n_hidden, xdim):
-    return bool(lib().dmip_sampler_supported(width, n_hidden, xdim))
+def em_sample_posterior(prior, likelihood, sde, y, n_chains, chain_offset, num_steps, mean, std, seed, out):
+    calls["em_sample_posterior"] += 1
+    n_y, ydim = y.shape
+    check(lib().dmip_em_sample_posterior(prior.h, likelihood.h, ctypes.byref(sde), ptr(y), n_y, ydim,
+                                         likelihood.xdim, int(n_chains), int(chain_offset), int(num_steps),
+                                         float(mean), float(std), ctypes.c_uint64(int(seed) & 0xFFFFFFFFFFFFFFFF),
+                                         DMIP_PREC_BF16, ptr(out), stream_of(y.device)))
+
+
+def em_sample_cdiffe(handle, sde, y, n_chains, chain_offset, num_steps, mean, std, seed, out):
+    calls["em_sample_cdiffe"] += 1
+    n_y, ydim = y.shape
+    check(lib().dmip_em_sample_cdiffe(handle.h, ctypes.byref(sde), ptr(y), n_y, ydim, handle.xdim,
+                                      int(n_chains), int(chain_offset), int(num_steps), float(mean), float(std),
+                                      ctypes.c_uint64(int(seed) & 0xFFFFFFFFFFFFFFFF), DMIP_PREC_BF16, ptr(out),
+                                      stream_of(y.device)))
+
+
+def sampler_supported(width, n_hidden, xdim, ydim=0, mode=DMIP_SAMPLER_CDE):
+    return bool(lib().dmip_sampler_supported(mode, width, n_hidden, xdim, ydim))

@@ -92,8 +92,8 @@ const char* dmip_last_error(void) { return g_err.c_str(); }
 
 int dmip_abi_version(void) { return DMIP_ABI_VERSION; }
 
-int dmip_sampler_supported(int width, int n_hidden, int xdim) {
-  return dmip::sampler_shape_supported(width, n_hidden, xdim) ? 1 : 0;
+int dmip_sampler_supported(int mode, int width, int n_hidden, int xdim, int ydim) {
+  return dmip::sampler_shape_supported(mode, width, n_hidden, xdim, ydim) ? 1 : 0;
 }
 
 int dmip_mlp_create(int in_dim, int out_dim, int n_hidden, const int* widths, int act_mode, int input_layout,
@@ -279,95 +279,148 @@ int dmip_mlp_forward(const dmip_mlp* net, const float* x_dev, const float* y_dev
   return DMIP_OK;
 }
 
-static int em_sample_impl(const dmip_mlp* net, const dmip_vpsde* sde, const float* y_dev, int n_y, int ydim,
-                          int xdim, int64_t n_chains, int64_t chain_offset, int num_steps, float mean, float stdv,
-                          uint64_t seed, int precision, const float* noise_dev, float* x_out_dev, void* stream,
-                          uint64_t* stamps);
+struct SampleArgs {
+  const dmip_vpsde* sde;
+  const float* y_dev;
+  int n_y, ydim, xdim;
+  int64_t n_chains, chain_offset;
+  int num_steps;
+  float mean, stdv;
+  uint64_t seed;
+  int precision;
+  const float* noise_dev;
+  float* x_out_dev;
+  void* stream;
+  uint64_t* stamps;
+};
+
+// net0: the CDE / CDiffE network or the Posterior likelihood; net1: the Posterior prior (else null)
+static int em_sample_impl(int mode, const dmip_mlp* net0, const dmip_mlp* net1, const SampleArgs& a) {
+  const int xdim = a.xdim, ydim = a.ydim;
+  if (!net0 || !a.sde || !a.y_dev || !a.x_out_dev || (mode == DMIP_SAMPLER_POSTERIOR && !net1))
+    return fail(DMIP_ERR_INVALID, "null argument");
+  if (a.precision != DMIP_PREC_BF16) return fail(DMIP_ERR_UNSUPPORTED, "unknown precision");
+  if (net0->layout != DMIP_INPUT_X_Y_T) return fail(DMIP_ERR_INVALID, "sampler needs an x,y,t network");
+  const int out_expected = mode == DMIP_SAMPLER_CDIFFE ? xdim + ydim : xdim;
+  if (xdim != net0->xdim || net0->out_dim != out_expected)
+    return fail(DMIP_ERR_INVALID, "xdim does not match the network");
+  if (ydim != net0->in_dim - xdim - 1) return fail(DMIP_ERR_INVALID, "ydim does not match the network");
+  if (mode == DMIP_SAMPLER_POSTERIOR) {
+    if (net1->layout != DMIP_INPUT_X_T || net1->xdim != xdim || net1->out_dim != xdim)
+      return fail(DMIP_ERR_INVALID, "prior must be an x,t network with out_dim == xdim");
+    if (net1->width != net0->width || net1->n_hidden != net0->n_hidden)
+      return fail(DMIP_ERR_UNSUPPORTED, "prior and likelihood networks must have the same hidden layers");
+  }
+  if (a.n_y < 1 || a.n_y > 65535) return fail(DMIP_ERR_INVALID, "n_y must be in [1, 65535]");
+  if (a.n_chains < 0 || a.chain_offset < 0) return fail(DMIP_ERR_INVALID, "negative chain count/offset");
+  if (a.num_steps < 1) return fail(DMIP_ERR_INVALID, "num_steps must be >= 1");
+  if (!(a.sde->T > 0.0)) return fail(DMIP_ERR_INVALID, "T must be > 0");
+  if (a.n_chains == 0) return DMIP_OK;
+  if (!dmip::sampler_shape_supported(mode, net0->width, net0->n_hidden, xdim, ydim))
+    return fail(DMIP_ERR_UNSUPPORTED, "no compiled sampler (mode " + std::to_string(mode) + ") for width " +
+                                          std::to_string(net0->width) + ", layers " + std::to_string(net0->n_hidden) +
+                                          ", xdim " + std::to_string(xdim) + ", ydim " + std::to_string(ydim));
+  hipStream_t st = (hipStream_t)a.stream;
+  dmip::SamplerParams p{};
+  char* a1 = nullptr;
+  if (mode == DMIP_SAMPLER_CDIFFE) {
+    // y_t varies per chain: layer 1 takes every input column (the forward kernel's image)
+    p.a1 = net0->a1_full;
+    p.a1_per_y = 0;
+  } else {
+    // y is constant per y index: fold W1_y y + b1 into a per-y layer-1 bias
+    const int T = net0->width / 32;
+    const int k1s = k1s_for(3 * (xdim + 1) + 2);
+    hipError_t e = hipMallocAsync((void**)&a1, (size_t)a.n_y * T * k1s * 1024, st);
+    if (e != hipSuccess) return fail(DMIP_ERR_ALLOC, std::string("hipMallocAsync: ") + hipGetErrorString(e));
+    dmip::A1PrepParams ap{};
+    ap.w1 = net0->w1;
+    ap.b1 = net0->b1;
+    ap.y = a.y_dev;
+    ap.a1 = a1;
+    ap.width = net0->width;
+    ap.in_dim = net0->in_dim;
+    ap.xdim = xdim;
+    ap.ydim = ydim;
+    ap.y_col0 = xdim;
+    ap.t_col = net0->in_dim - 1;
+    ap.k1s = k1s;
+    e = dmip::launch_a1_prep(ap, a.n_y, st);
+    if (e != hipSuccess) {
+      (void)hipFreeAsync(a1, st);
+      return hip_fail(e, "a1_prep launch");
+    }
+    p.a1 = a1;
+    p.a1_per_y = 1;
+  }
+  p.hidden = net0->hidden;
+  p.ao = net0->ao_samp;
+  p.bias_hidden = net0->bias_hidden;
+  p.bias_out = net0->bias_out_samp;
+  if (mode == DMIP_SAMPLER_POSTERIOR) {
+    // the prior's (x, t) layer-1 image is the sampler's B1 slot layout over (x, tau)
+    p.hidden2 = net1->hidden;
+    p.a1_2 = net1->a1_full;
+    p.ao2 = net1->ao_samp;
+    p.bias_hidden2 = net1->bias_hidden;
+    p.bias_out2 = net1->bias_out_samp;
+  }
+  p.y_obs = a.y_dev;
+  p.noise = a.noise_dev;
+  p.x_out = a.x_out_dev;
+  p.n_chains = a.n_chains;
+  p.chain_offset = a.chain_offset;
+  p.num_steps = a.num_steps;
+  p.T = (float)a.sde->T;
+  p.bmin = (float)a.sde->beta_min;
+  p.bdiff = (float)(a.sde->beta_max - a.sde->beta_min);
+  p.delta = (float)(a.sde->T / (double)a.num_steps);
+  p.sqrt_delta = (float)std::sqrt(a.sde->T / (double)a.num_steps);
+  p.mean = a.mean;
+  p.stdv = a.stdv;
+  p.seed = a.seed;
+  p.stamps = (unsigned long long*)a.stamps;
+  bool ok = false;
+  hipError_t e = dmip::launch_sampler(p, mode, net0->width, net0->n_hidden, xdim, ydim, a.n_y, st, &ok);
+  if (a1) (void)hipFreeAsync(a1, st);
+  if (!ok) return fail(DMIP_ERR_UNSUPPORTED, "no compiled sampler");
+  if (e != hipSuccess) return hip_fail(e, "em_sampler launch");
+  return DMIP_OK;
+}
 
 int dmip_em_sample(const dmip_mlp* net, const dmip_vpsde* sde, const float* y_dev, int n_y, int ydim, int xdim,
                    int64_t n_chains, int64_t chain_offset, int num_steps, float mean, float stdv, uint64_t seed,
                    int precision, const float* noise_dev, float* x_out_dev, void* stream) {
-  return em_sample_impl(net, sde, y_dev, n_y, ydim, xdim, n_chains, chain_offset, num_steps, mean, stdv, seed,
-                        precision, noise_dev, x_out_dev, stream, nullptr);
+  const SampleArgs a{sde,  y_dev, n_y,       ydim,      xdim,      n_chains, chain_offset, num_steps,
+                     mean, stdv,  seed,      precision, noise_dev, x_out_dev, stream,      nullptr};
+  return em_sample_impl(DMIP_SAMPLER_CDE, net, nullptr, a);
+}
+
+int dmip_em_sample_posterior(const dmip_mlp* prior, const dmip_mlp* likelihood, const dmip_vpsde* sde,
+                             const float* y_dev, int n_y, int ydim, int xdim, int64_t n_chains, int64_t chain_offset,
+                             int num_steps, float mean, float stdv, uint64_t seed, int precision, float* x_out_dev,
+                             void* stream) {
+  if (!prior) return fail(DMIP_ERR_INVALID, "null argument");
+  const SampleArgs a{sde,  y_dev, n_y,       ydim,      xdim,    n_chains, chain_offset, num_steps,
+                     mean, stdv,  seed,      precision, nullptr, x_out_dev, stream,      nullptr};
+  return em_sample_impl(DMIP_SAMPLER_POSTERIOR, likelihood, prior, a);
+}
+
+int dmip_em_sample_cdiffe(const dmip_mlp* net, const dmip_vpsde* sde, const float* y_dev, int n_y, int ydim, int xdim,
+                          int64_t n_chains, int64_t chain_offset, int num_steps, float mean, float stdv, uint64_t seed,
+                          int precision, float* x_out_dev, void* stream) {
+  const SampleArgs a{sde,  y_dev, n_y,       ydim,      xdim,    n_chains, chain_offset, num_steps,
+                     mean, stdv,  seed,      precision, nullptr, x_out_dev, stream,      nullptr};
+  return em_sample_impl(DMIP_SAMPLER_CDIFFE, net, nullptr, a);
 }
 
 int dmip_em_sample_stamps(const dmip_mlp* net, const dmip_vpsde* sde, const float* y_dev, int n_y, int ydim,
                           int xdim, int64_t n_chains, int num_steps, uint64_t seed, float* x_out_dev,
                           uint64_t* stamps_dev, void* stream) {
   if (!stamps_dev) return fail(DMIP_ERR_INVALID, "null stamps buffer");
-  return em_sample_impl(net, sde, y_dev, n_y, ydim, xdim, n_chains, 0, num_steps, 0.0f, 1.0f, seed, DMIP_PREC_BF16,
-                        nullptr, x_out_dev, stream, stamps_dev);
-}
-
-static int em_sample_impl(const dmip_mlp* net, const dmip_vpsde* sde, const float* y_dev, int n_y, int ydim,
-                          int xdim, int64_t n_chains, int64_t chain_offset, int num_steps, float mean, float stdv,
-                          uint64_t seed, int precision, const float* noise_dev, float* x_out_dev, void* stream,
-                          uint64_t* stamps) {
-  if (!net || !sde || !y_dev || !x_out_dev) return fail(DMIP_ERR_INVALID, "null argument");
-  if (precision != DMIP_PREC_BF16) return fail(DMIP_ERR_UNSUPPORTED, "unknown precision");
-  if (net->layout != DMIP_INPUT_X_Y_T) return fail(DMIP_ERR_INVALID, "sampler needs an x,y,t network (CDE)");
-  if (xdim != net->xdim || net->out_dim != xdim) return fail(DMIP_ERR_INVALID, "xdim does not match the network");
-  if (ydim != net->in_dim - xdim - 1) return fail(DMIP_ERR_INVALID, "ydim does not match the network");
-  if (n_y < 1 || n_y > 65535) return fail(DMIP_ERR_INVALID, "n_y must be in [1, 65535]");
-  if (n_chains < 0 || chain_offset < 0) return fail(DMIP_ERR_INVALID, "negative chain count/offset");
-  if (num_steps < 1) return fail(DMIP_ERR_INVALID, "num_steps must be >= 1");
-  if (!(sde->T > 0.0)) return fail(DMIP_ERR_INVALID, "T must be > 0");
-  if (n_chains == 0) return DMIP_OK;
-  if (!dmip::sampler_shape_supported(net->width, net->n_hidden, xdim))
-    return fail(DMIP_ERR_UNSUPPORTED, "no compiled sampler for width " + std::to_string(net->width) + ", layers " +
-                                          std::to_string(net->n_hidden) + ", xdim " + std::to_string(xdim));
-  hipStream_t st = (hipStream_t)stream;
-  const int T = net->width / 32;
-  const int k1s = k1s_for(3 * (xdim + 1) + 2);
-  const size_t a1_bytes = (size_t)n_y * T * k1s * 1024;
-  char* a1 = nullptr;
-  hipError_t e = hipMallocAsync((void**)&a1, a1_bytes, st);
-  if (e != hipSuccess) return fail(DMIP_ERR_ALLOC, std::string("hipMallocAsync: ") + hipGetErrorString(e));
-
-  dmip::A1PrepParams ap{};
-  ap.w1 = net->w1;
-  ap.b1 = net->b1;
-  ap.y = y_dev;
-  ap.a1 = a1;
-  ap.width = net->width;
-  ap.in_dim = net->in_dim;
-  ap.xdim = xdim;
-  ap.ydim = ydim;
-  ap.y_col0 = xdim;
-  ap.t_col = net->in_dim - 1;
-  ap.k1s = k1s;
-  e = dmip::launch_a1_prep(ap, n_y, st);
-  if (e != hipSuccess) {
-    (void)hipFreeAsync(a1, st);
-    return hip_fail(e, "a1_prep launch");
-  }
-
-  dmip::SamplerParams p{};
-  p.hidden = net->hidden;
-  p.a1 = a1;
-  p.ao = net->ao_samp;
-  p.bias_hidden = net->bias_hidden;
-  p.bias_out = net->bias_out_samp;
-  p.noise = noise_dev;
-  p.x_out = x_out_dev;
-  p.n_chains = n_chains;
-  p.chain_offset = chain_offset;
-  p.num_steps = num_steps;
-  p.T = (float)sde->T;
-  p.bmin = (float)sde->beta_min;
-  p.bdiff = (float)(sde->beta_max - sde->beta_min);
-  p.delta = (float)(sde->T / (double)num_steps);
-  p.sqrt_delta = (float)std::sqrt(sde->T / (double)num_steps);
-  p.mean = mean;
-  p.stdv = stdv;
-  p.seed = seed;
-  p.stamps = (unsigned long long*)stamps;
-  bool ok = false;
-  e = dmip::launch_sampler(p, net->width, net->n_hidden, xdim, n_y, st, &ok);
-  (void)hipFreeAsync(a1, st);
-  if (!ok) return fail(DMIP_ERR_UNSUPPORTED, "no compiled sampler");
-  if (e != hipSuccess) return hip_fail(e, "em_sampler launch");
-  return DMIP_OK;
+  const SampleArgs a{sde,  y_dev, n_y,  ydim,           xdim,    n_chains,  0,      num_steps,
+                     0.0f, 1.0f,  seed, DMIP_PREC_BF16, nullptr, x_out_dev, stream, stamps_dev};
+  return em_sample_impl(DMIP_SAMPLER_CDE, net, nullptr, a);
 }
 
 int dmip_rng_words(uint64_t seed, int64_t chain_offset, uint64_t stream_id, int64_t n_chains, int n_words,

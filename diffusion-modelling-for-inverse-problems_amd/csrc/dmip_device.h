@@ -116,6 +116,18 @@ __device__ __forceinline__ StepCoef step_coef(int i, int S, float T, float bmin,
   return c;
 }
 
+// mean_weight(t) = exp(-0.25 t^2 (bmax-bmin) - 0.5 t bmin) and var(t) = 1 - exp(-0.5 t^2 (bmax-bmin)
+// - t bmin) in the reference's evaluation order (sdes.py:24-28); exp within 1 ulp.
+__device__ __forceinline__ float vp_mean_weight(float t, float bmin, float bdiff) {
+  const float a = __fmul_rn(__fmul_rn(-0.25f, __fmul_rn(t, t)), bdiff);
+  return expf(__fsub_rn(a, __fmul_rn(__fmul_rn(0.5f, t), bmin)));
+}
+__device__ __forceinline__ float vp_std(float t, float bmin, float bdiff) {
+  const float a = __fmul_rn(__fmul_rn(-0.5f, __fmul_rn(t, t)), bdiff);
+  const float var = __fsub_rn(1.0f, expf(__fsub_rn(a, __fmul_rn(t, bmin))));
+  return (float)__dsqrt_rn((double)var);  // var ** 0.5, correctly rounded
+}
+
 // x <- fl(x + fl(delta*mu)) + fl(fl(sqrt(delta)*g)*xi),  mu = fl(g*a) - fl(fl(-0.5*beta)*x)
 // (models/diffusion.py:40-42 with sdes.py:77-79,86-87 at lambda = 0).
 __device__ __forceinline__ float em_update(float x, float a, float xi, const StepCoef& c,

@@ -5,12 +5,24 @@
 
 namespace dmip {
 
+// Sampler modes (dmip_kernels.hip em_sampler_kernel)
+enum { SAMPLER_CDE = 0, SAMPLER_POSTERIOR = 1, SAMPLER_CDIFFE = 2 };
+
 struct SamplerParams {
+  // network 0: the CDE / CDiffE network, or the Posterior estimator's likelihood network
   const char* hidden;         // (NL-1)*(W/32) row-tile chunks of (W/16) KiB bf16 fragments
-  const char* a1;             // per-y layer-1 blocks [n_y][W/32][K1S] KiB (a1_prep_kernel)
+  const char* a1;             // layer-1 blocks [W/32][K1S] KiB, per y ([n_y][...]) when a1_per_y
   const char* ao;             // output layer blocks [W/16] KiB (rows duplicated into both lane halves)
   const float* bias_hidden;   // [NL-1][W/32][2][16] accumulator init per lane half
   const float* bias_out;      // [2][16]
+  int a1_per_y;
+  // network 1 (Posterior only): the prior network (x, t); its layer 1 is shared by all y
+  const char* hidden2;
+  const char* a1_2;
+  const char* ao2;
+  const float* bias_hidden2;
+  const float* bias_out2;
+  const float* y_obs;         // CDiffE: observations [n_y][ydim] (re-diffused every step)
   const float* noise;         // injected normals [S+1][n_y][n_chains][D] (slot 0 -> x0) or null
   float* x_out;               // [n_y][n_chains][D]
   long long n_chains;         // chains per y
@@ -45,9 +57,9 @@ struct A1PrepParams {
   int width, in_dim, xdim, ydim, y_col0, t_col, k1s;
 };
 
-hipError_t launch_sampler(const SamplerParams& p, int width, int n_hidden, int xdim, int n_y, hipStream_t st,
-                          bool* supported);
-bool sampler_shape_supported(int width, int n_hidden, int xdim);
+hipError_t launch_sampler(const SamplerParams& p, int mode, int width, int n_hidden, int xdim, int ydim, int n_y,
+                          hipStream_t st, bool* supported);
+bool sampler_shape_supported(int mode, int width, int n_hidden, int xdim, int ydim);
 bool forward_split(int width, int in_dim);
 hipError_t launch_forward(const ForwardParams& p, int width, int n_hidden, int in_dim, hipStream_t st,
                           bool* supported);

@@ -21,22 +21,25 @@
 
 namespace dmip {
 
-template <int W, int NL, int K1S, int R, bool RES>
+// LDS layout of one workgroup: NNET networks (net 0 = the CDE / CDiffE / likelihood net, net 1 =
+// the prior net of the Posterior estimator) share one weight ring.
+template <int W, int NL, int K1S, int NNET, int R, bool RES>
 struct Lay {
   static constexpr int T = W / 32;            // 32-row tiles per layer
   static constexpr int KS = W / 16;           // 16-deep k-steps over a hidden layer
   static constexpr int CHUNK = KS * 1024;     // one row tile of a W x W layer, bf16 fragments
   static constexpr int NC = (NL - 1) * T;     // hidden chunks per network evaluation
-  static constexpr int A1_OFF = 0;
+  static constexpr int NCT = NC * NNET;       // hidden chunks per step (all networks)
   static constexpr int A1_BYTES = T * K1S * 1024;
-  static constexpr int AO_OFF = A1_OFF + A1_BYTES;
   static constexpr int AO_BYTES = KS * 1024;
-  static constexpr int BH_OFF = AO_OFF + AO_BYTES;
   static constexpr int BH_BYTES = (NL - 1) * T * 2 * 16 * 4;
-  static constexpr int BO_OFF = BH_OFF + BH_BYTES;
-  static constexpr int BO_BYTES = 2 * 16 * 4;
+  static constexpr int BO_BYTES = 2 * 16 * 4;  // output bias, summed over the networks
+  static constexpr int A1_OFF = 0;
+  static constexpr int AO_OFF = A1_OFF + NNET * A1_BYTES;
+  static constexpr int BH_OFF = AO_OFF + NNET * AO_BYTES;
+  static constexpr int BO_OFF = BH_OFF + NNET * BH_BYTES;
   static constexpr int W_OFF = BO_OFF + BO_BYTES;
-  static constexpr int SLOTS = RES ? NC : R;
+  static constexpr int SLOTS = RES ? NCT : R;
   static constexpr int TOTAL = W_OFF + SLOTS * CHUNK;
 };
 
@@ -48,17 +51,6 @@ __device__ __forceinline__ void stage_blocks(char* lds, const char* g, int n_blo
 
 __device__ __forceinline__ void stage_floats(float* lds, const float* g, int n, int tid, int nthreads) {
   for (int i = tid; i < n; i += nthreads) lds[i] = g[i];
-}
-
-template <int NW, int PPW, int CHUNK, int NC, int R>
-__device__ __forceinline__ void ring_issue(char* ring, const char* hidden, long long gc, int w, int lane) {
-  const int chunk = (int)(gc % NC);
-  const int slot = (int)(gc % R);
-#pragma unroll
-  for (int q = 0; q < PPW; ++q) {
-    const int p = w * PPW + q;
-    glds16(hidden + (size_t)chunk * CHUNK + p * 1024, ring + slot * CHUNK + p * 1024, lane);
-  }
 }
 
 // acc += sum_s A[s] * H[s] over one 32-row tile: A fragments streamed from LDS (1 KiB apart)
@@ -76,34 +68,47 @@ __device__ __forceinline__ void mfma_row_tile(const char* a_lane, const bf16x8 (
   }
 }
 
-// ------------------------------------------------------------------- one network evaluation
-// Hidden W x W layers + output layer, given layer-1 activations in H0. Returns the output
-// accumulator tile (rows = output dims, see the host packers for the row maps).
+// ------------------------------------------------------------------- network evaluation engine
+// Evaluates NNET networks on one 32-chain tile per wave and sums their output layers into one
+// accumulator tile (rows = output dims; the host packers define the row maps).
 // DIAG (timing ablations only, never on the product path): bit 0 = no ring barrier/DMA,
 // bit 1 = hidden activations replaced by a bf16 cast, bit 2 = layer-1 activation replaced by a cast.
-template <int W, int NL, int K1S, int NW, int R, bool RES, bool CONSERVATIVE, int DIAG = 0, int ORD_MODE = 2>
-struct Net {
-  using L = Lay<W, NL, K1S, R, RES>;
+template <int W, int NL, int K1S, int NNET, int NW, int R, bool RES, bool CONSERVATIVE, int DIAG = 0>
+struct Engine {
+  using L = Lay<W, NL, K1S, NNET, R, RES>;
   static constexpr int T = L::T;
   static constexpr int KS = L::KS;
   static constexpr int PPW = RES ? 1 : KS / NW;
 
   char* lds;
-  const char* hidden;
+  const char* hidden[2];
   long long gc;  // global chunk counter (ring mode)
   int w, lane;
 
+  __device__ __forceinline__ void ring_issue(long long g) {
+    const int c = (int)(g % L::NCT);
+    const char* src = hidden[c / L::NC] + (size_t)(c % L::NC) * L::CHUNK;
+    char* dst = lds + L::W_OFF + (int)(g % R) * L::CHUNK;
+#pragma unroll
+    for (int q = 0; q < PPW; ++q) {
+      const int piece = w * PPW + q;
+      // opaque wave-uniform base: otherwise the compiler hoists every chunk's 64-bit per-lane source
+      // address out of the step loop and holds them all in VGPRs (2 per chunk)
+      const char* g = src + piece * 1024;
+      asm volatile("" : "+s"(g));
+      glds16(g, dst + piece * 1024, lane);
+    }
+  }
+
   __device__ __forceinline__ const char* chunk_sync() {
-    if constexpr (RES) {
-      return nullptr;
-    } else if constexpr (DIAG & 1) {
+    if constexpr (DIAG & 1) {
       asm volatile("" ::: "memory");
       return lds + L::W_OFF + (int)((gc++) % R) * L::CHUNK;
     } else {
       if constexpr (CONSERVATIVE) wait_vmcnt<0>();
       else wait_vmcnt<(R - 2) * PPW>();
       lds_barrier();
-      ring_issue<NW, PPW, L::CHUNK, L::NC, R>(lds + L::W_OFF, hidden, gc + R - 1, w, lane);
+      ring_issue(gc + R - 1);
       const char* slot = lds + L::W_OFF + (int)(gc % R) * L::CHUNK;
       ++gc;
       return slot;
@@ -118,11 +123,9 @@ struct Net {
     return acc;
   }
 
-  // ORDER 0: a chunk's MFMAs are issued first and the previous tile's activation after them;
-  // ORDER 1: activation first, then the MFMAs. Waves 0-3 and 4-7 (one of each per SIMD) use
-  // opposite orders, so a SIMD's matrix pipe and VALU are busy at the same time instead of both
-  // waves wanting the same pipe in lockstep.
-  template <int LI, int ORDER>
+  // one W x W layer; the activation of tile rt-1 is issued in tile rt's block so it overlaps the
+  // MFMAs (the compiler interleaves them; explicit orders measured slower, profiles/README.md)
+  template <int NI, int LI>
   __device__ __forceinline__ void hidden_layer(const bf16x8 (&Hin)[KS], bf16x8 (&Hout)[KS]) {
     f32x16 pend;
 #pragma unroll
@@ -132,52 +135,32 @@ struct Net {
         // keep the resident weights in LDS: without this the compiler hoists every fragment
         // read out of the step loop into (spilled) registers
         asm volatile("" ::: "memory");
-        wb = lds + L::W_OFF + (LI * T + rt) * L::CHUNK;
+        wb = lds + L::W_OFF + ((NI * (NL - 1) + LI) * T + rt) * L::CHUNK;
       } else {
         wb = chunk_sync();
       }
-      if constexpr (ORDER == 1) {
-        if (rt > 0) act_pack<false, (DIAG & 2) != 0>(pend, Hout[2 * (rt - 1)], Hout[2 * (rt - 1) + 1]);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      f32x16 acc = bias_tile(L::BH_OFF + ((LI * T + rt) * 2) * 64);
+      f32x16 acc = bias_tile(L::BH_OFF + NI * L::BH_BYTES + ((LI * T + rt) * 2) * 64);
       mfma_row_tile<KS>(wb + lane * 16, Hin, acc);
-      if constexpr (ORDER == 0) {
-        __builtin_amdgcn_sched_barrier(0);
-        if (rt > 0) act_pack<false, (DIAG & 2) != 0>(pend, Hout[2 * (rt - 1)], Hout[2 * (rt - 1) + 1]);
-      } else if constexpr (ORDER == 2) {  // compiler-scheduled interleave (previous behaviour)
-        if (rt > 0) act_pack<false, (DIAG & 2) != 0>(pend, Hout[2 * (rt - 1)], Hout[2 * (rt - 1) + 1]);
-      } else if constexpr (ORDER >= 3) {
-        // pinned interleave: the bias / first fragment reads, then per MFMA one LDS read and VPM
-        // VALU instructions of the previous tile's activation (ORDER 3: 4, ORDER 4: 6, ORDER 5: 3)
-        if (rt > 0) act_pack<false, (DIAG & 2) != 0>(pend, Hout[2 * (rt - 1)], Hout[2 * (rt - 1) + 1]);
-        constexpr int VPM = ORDER == 3 ? 4 : (ORDER == 4 ? 6 : 3);
-        __builtin_amdgcn_sched_group_barrier(0x100, 7, 0);
-#pragma unroll
-        for (int s = 0; s < KS; ++s) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x002, VPM, 0);
-        }
-      }
+      if (rt > 0) act_pack<false, (DIAG & 2) != 0>(pend, Hout[2 * (rt - 1)], Hout[2 * (rt - 1) + 1]);
       pend = acc;
     }
     act_pack<false, (DIAG & 2) != 0>(pend, Hout[2 * (T - 1)], Hout[2 * (T - 1) + 1]);
   }
 
-  template <int LI, int ORDER>
-  __device__ __forceinline__ void hidden_chain(bf16x8 (&Ha)[KS], bf16x8 (&Hb)[KS], f32x16& out) {
-    if constexpr (LI == NL - 1) {  // all W x W layers done: output layer
+  // hidden layers LI.. of net NI, then its output layer accumulated into `out`
+  template <int NI, int LI>
+  __device__ __forceinline__ void hidden_stack(bf16x8 (&Ha)[KS], bf16x8 (&Hb)[KS], f32x16& out) {
+    if constexpr (LI == NL - 1) {
       asm volatile("" ::: "memory");
-      out = bias_tile(L::BO_OFF);
-      mfma_row_tile<KS>(lds + L::AO_OFF + lane * 16, Ha, out);
+      mfma_row_tile<KS>(lds + L::AO_OFF + NI * L::AO_BYTES + lane * 16, Ha, out);
     } else {
-      hidden_layer<LI, ORDER>(Ha, Hb);
-      hidden_chain<LI + 1, ORDER>(Hb, Ha, out);
+      hidden_layer<NI, LI>(Ha, Hb);
+      hidden_stack<NI, LI + 1>(Hb, Ha, out);
     }
   }
 
-  // layer 1 from the B1 operand (split-bf16 inputs), double tanh (nets.py:21-26)
+  // layer 1 of net NI from the B1 operand (split-bf16 inputs), double tanh (nets.py:21-26)
+  template <int NI>
   __device__ __forceinline__ void layer1(const bf16x8 (&B1)[K1S], bf16x8 (&H)[KS]) {
     f32x16 pend;
 #pragma unroll
@@ -186,7 +169,7 @@ struct Net {
       f32x16 acc = {};
 #pragma unroll
       for (int s = 0; s < K1S; ++s) {
-        const bf16x8 a = *(const bf16x8*)(lds + L::A1_OFF + (rt * K1S + s) * 1024 + lane * 16);
+        const bf16x8 a = *(const bf16x8*)(lds + L::A1_OFF + NI * L::A1_BYTES + (rt * K1S + s) * 1024 + lane * 16);
         acc = mfma32(a, B1[s], acc);
       }
       if (rt > 0) act_pack<true, (DIAG & 4) != 0>(pend, H[2 * (rt - 1)], H[2 * (rt - 1) + 1]);
@@ -195,38 +178,50 @@ struct Net {
     act_pack<true, (DIAG & 4) != 0>(pend, H[2 * (T - 1)], H[2 * (T - 1) + 1]);
   }
 
-  // hidden layers + output with the wave-group instruction order (see hidden_layer)
-  __device__ __forceinline__ void hidden_all(bf16x8 (&Ha)[KS], bf16x8 (&Hb)[KS], f32x16& out) {
-    if constexpr (ORD_MODE >= 2) {
-      hidden_chain<0, ORD_MODE>(Ha, Hb, out);
-    } else {
-      if (w >= NW / 2) hidden_chain<0, 1>(Ha, Hb, out);
-      else hidden_chain<0, 0>(Ha, Hb, out);
-    }
+  template <int NI>
+  __device__ __forceinline__ void eval_net(const bf16x8 (&B1)[K1S], f32x16& out) {
+    bf16x8 Ha[KS], Hb[KS];
+    layer1<NI>(B1, Ha);
+    hidden_stack<NI, 0>(Ha, Hb, out);
   }
 
+  // sum over the networks of their outputs (+ the summed output bias)
   __device__ __forceinline__ f32x16 eval(const bf16x8 (&B1)[K1S]) {
-    bf16x8 Ha[KS], Hb[KS];
-    layer1(B1, Ha);
-    f32x16 out;
-    hidden_all(Ha, Hb, out);
+    asm volatile("" ::: "memory");
+    f32x16 out = bias_tile(L::BO_OFF);
+    eval_net<0>(B1, out);
+    if constexpr (NNET > 1) {
+      // only accumulator registers 0-3 carry output rows in the sampler's row map (rows 0-3, duplicated
+      // into lanes 32-63); carry just those through the second network
+      float keep[4] = {out[0], out[1], out[2], out[3]};
+      __builtin_amdgcn_sched_barrier(0);
+      f32x16 out2 = {};
+      eval_net<1>(B1, out2);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) out2[r] += keep[r];
+      return out2;
+    }
     return out;
   }
 
-  // load the resident parts (and the whole hidden stack in resident mode); then start the ring
-  __device__ __forceinline__ void prologue(const char* a1, const char* ao, const float* bias_hidden,
-                                           const float* bias_out) {
+  // resident parts (and the whole hidden stack in resident mode); then start the ring.
+  // The output bias is the sum of the networks' output biases.
+  __device__ __forceinline__ void prologue(const char* const (&a1)[2], const char* const (&ao)[2],
+                                           const float* const (&bh)[2], const float* const (&bo)[2]) {
     const int tid = threadIdx.x;
-    stage_blocks<NW>(lds + L::A1_OFF, a1, T * K1S, w, lane);
-    stage_blocks<NW>(lds + L::AO_OFF, ao, KS, w, lane);
-    if constexpr (RES) stage_blocks<NW>(lds + L::W_OFF, hidden, L::NC * KS, w, lane);
-    stage_floats((float*)(lds + L::BH_OFF), bias_hidden, L::BH_BYTES / 4, tid, NW * 64);
-    stage_floats((float*)(lds + L::BO_OFF), bias_out, L::BO_BYTES / 4, tid, NW * 64);
+#pragma unroll
+    for (int ni = 0; ni < NNET; ++ni) {
+      stage_blocks<NW>(lds + L::A1_OFF + ni * L::A1_BYTES, a1[ni], T * K1S, w, lane);
+      stage_blocks<NW>(lds + L::AO_OFF + ni * L::AO_BYTES, ao[ni], KS, w, lane);
+      if constexpr (RES) stage_blocks<NW>(lds + L::W_OFF + ni * L::NC * L::CHUNK, hidden[ni], L::NC * KS, w, lane);
+      stage_floats((float*)(lds + L::BH_OFF + ni * L::BH_BYTES), bh[ni], L::BH_BYTES / 4, tid, NW * 64);
+    }
+    for (int i = tid; i < L::BO_BYTES / 4; i += NW * 64)
+      ((float*)(lds + L::BO_OFF))[i] = NNET > 1 ? bo[0][i] + bo[1][i] : bo[0][i];
     wait_vmcnt<0>();
     __syncthreads();
     if constexpr (!RES) {
-      for (int q = 0; q < R - 1; ++q)
-        ring_issue<NW, PPW, L::CHUNK, L::NC, R>(lds + L::W_OFF, hidden, (long long)q, w, lane);
+      for (int q = 0; q < R - 1; ++q) ring_issue(q);
     }
   }
 
@@ -235,15 +230,10 @@ struct Net {
   }
 };
 
-// B1 operand of layer 1 for the sampler: u = [hi(v) | lo(v) | hi(v) | 1 | 1 | 0...],
-// v = (x_0..x_{D-1}, tau); lane half h supplies u[16 s + 8 h + j].
-template <int D, int K1S>
-__device__ __forceinline__ void build_b1(const float (&x)[D], float tau, int h, bf16x8 (&B1)[K1S]) {
-  constexpr int NV = D + 1;
-  float v[NV];
-#pragma unroll
-  for (int k = 0; k < D; ++k) v[k] = x[k];
-  v[D] = tau;
+// B1 operand of layer 1: u = [hi(v) | lo(v) | hi(v) | 1 | 1 | 0...] over NV varying inputs;
+// lane half h supplies u[16 s + 8 h + j].
+template <int NV, int K1S>
+__device__ __forceinline__ void build_b1(const float (&v)[NV], int h, bf16x8 (&B1)[K1S]) {
   __bf16 vh[NV], vl[NV];
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
@@ -255,7 +245,6 @@ __device__ __forceinline__ void build_b1(const float (&x)[D], float tau, int h, 
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       // both candidate slot values (h = 0 and h = 1) are compile-time; select by lane half
-      const int k0 = 16 * s + j, k1 = 16 * s + 8 + j;
       auto slot = [&](int k) -> __bf16 {
         if (k < NV) return vh[k];
         if (k < 2 * NV) return vl[k - NV];
@@ -263,7 +252,7 @@ __device__ __forceinline__ void build_b1(const float (&x)[D], float tau, int h, 
         if (k < 3 * NV + 2) return (__bf16)1.0f;
         return (__bf16)0.0f;
       };
-      B1[s][j] = h ? slot(k1) : slot(k0);
+      B1[s][j] = h ? slot(16 * s + 8 + j) : slot(16 * s + j);
     }
   }
 }
@@ -277,16 +266,30 @@ __device__ __forceinline__ unsigned long long stamp() {
   return t;
 }
 
+constexpr int MODE_CDE = SAMPLER_CDE, MODE_POSTERIOR = SAMPLER_POSTERIOR, MODE_CDIFFE = SAMPLER_CDIFFE;
+
+constexpr int k1s_of(int slots) { return (slots + 15) / 16; }
+
+// The fused reverse-SDE sampler (all num_steps in one launch).
+//   MODE_CDE:       a = net(x, y, T-t)                          (models/diffusion.py:27-46)
+//   MODE_POSTERIOR: a = g (lik(x, y, T-t) + prior(x, T-t))      (nets.py:155-157 via the same loop)
+//   MODE_CDIFFE:    y_t ~ q(y_t | y) at T-t, a = net(x, y_t, T-t)[:xdim]   (repaired
+//                   models/diffusion.py:158-180; the y part of the joint update is discarded)
+// then mu = g a + 0.5 beta x, x <- x + delta mu + sqrt(delta) g xi.
 // STAMP: diagnostic build only (dmip_em_sample_stamps) -- per-wave cycle sums of the step phases
 // [layer 1 + B1, hidden layers, output layer + RNG + EM update], written to p.stamps.
-template <int W, int NL, int D, int NW, int R, bool RES, bool NOISE, bool STAMP = false, int DIAG = 0, int ORD = 2>
+template <int MODE, int W, int NL, int D, int M, int NW, int R, bool RES, bool NOISE, bool STAMP = false,
+          int DIAG = 0>
 __global__ void __launch_bounds__(NW * 64, (NW * 64 + 255) / 256)
 em_sampler_kernel(SamplerParams p) {
-  constexpr int K1S = (3 * (D + 1) + 2 + 15) / 16;
-  using L = Lay<W, NL, K1S, R, RES>;
+  constexpr int NNET = MODE == MODE_POSTERIOR ? 2 : 1;
+  constexpr int NV = MODE == MODE_CDIFFE ? D + M + 1 : D + 1;  // inputs that vary per chain
+  constexpr int K1S = k1s_of(3 * NV + 2);
+  using L = Lay<W, NL, K1S, NNET, R, RES>;
   static_assert(L::TOTAL <= 160 * 1024, "LDS budget");
   static_assert(RES || (L::KS % NW == 0), "ring pieces per wave");
   static_assert(D <= 4, "sampler output rows are duplicated into both lane halves (D <= 4)");
+  static_assert(!(NOISE && MODE != MODE_CDE), "noise injection: CDE only");
   __shared__ __attribute__((aligned(16))) char lds[L::TOTAL];
 
   const int lane = threadIdx.x & 63;
@@ -296,8 +299,15 @@ em_sampler_kernel(SamplerParams p) {
   const long long c_local = (long long)blockIdx.x * (NW * 32) + w * 32 + (lane & 31);
   const bool valid = c_local < p.n_chains;
 
-  Net<W, NL, K1S, NW, R, RES, NOISE, DIAG, ORD> net{lds, p.hidden, 0, w, lane};
-  net.prologue(p.a1 + (size_t)yi * L::T * K1S * 1024, p.ao, p.bias_hidden, p.bias_out);
+  Engine<W, NL, K1S, NNET, NW, R, RES, NOISE, DIAG> eng{lds, {p.hidden, p.hidden2}, 0, w, lane};
+  {
+    const size_t a1_stride = (size_t)L::T * K1S * 1024;
+    const char* const a1[2] = {p.a1 + (p.a1_per_y ? yi * a1_stride : 0), p.a1_2};
+    const char* const ao[2] = {p.ao, p.ao2};
+    const float* const bh[2] = {p.bias_hidden, p.bias_hidden2};
+    const float* const bo[2] = {p.bias_out, p.bias_out2};
+    eng.prologue(a1, ao, bh, bo);
+  }
 
   float x[D];
   Rng rng = rng_init(p.seed, (uint64_t)(p.chain_offset + c_local), (uint64_t)yi);
@@ -314,6 +324,12 @@ em_sampler_kernel(SamplerParams p) {
     for (int k = 0; k < D; ++k) x[k] = __fadd_rn(__fmul_rn(n[k], p.stdv), p.mean);
   }
   const size_t noise_step = (size_t)gridDim.y * p.n_chains * D;
+  // CDiffE: this workgroup's observation, read from LDS every step (wave-uniform broadcast)
+  __shared__ float yobs[M > 0 ? M : 1];
+  if constexpr (MODE == MODE_CDIFFE) {
+    stage_floats(yobs, p.y_obs + (size_t)yi * M, M, threadIdx.x, NW * 64);
+    __syncthreads();
+  }
 
   unsigned long long ph[3] = {0, 0, 0};
   unsigned long long clk0 = 0, rt0 = 0;
@@ -325,13 +341,25 @@ em_sampler_kernel(SamplerParams p) {
     unsigned long long t0 = 0, t1 = 0, t2 = 0;
     if constexpr (STAMP) t0 = stamp();
     const StepCoef cf = step_coef(i, p.num_steps, p.T, p.bmin, p.bdiff);
+    float v[NV];
+#pragma unroll
+    for (int k = 0; k < D; ++k) v[k] = x[k];
+    if constexpr (MODE == MODE_CDIFFE) {
+      // y_t = eps * std(T-t) + mean_weight(T-t) * y  (sdes.py:37-44, on the observation part of z_0)
+      const float mw = vp_mean_weight(cf.tau, p.bmin, p.bdiff);
+      const float sd = vp_std(cf.tau, p.bmin, p.bdiff);
+      float eps[M];
+      rng_normals<M>(rng, eps);
+#pragma unroll
+      for (int k = 0; k < M; ++k) v[D + k] = __fadd_rn(__fmul_rn(eps[k], sd), __fmul_rn(mw, yobs[k]));
+      asm volatile("" ::: "memory");  // keep the observation in LDS, not in registers across the step
+    }
+    v[NV - 1] = cf.tau;
     bf16x8 B1[K1S];
-    build_b1<D, K1S>(x, cf.tau, h, B1);
-    bf16x8 Ha[L::KS], Hb[L::KS];
-    net.layer1(B1, Ha);
+    build_b1<NV, K1S>(v, h, B1);
+    if constexpr (MODE != MODE_CDE) __builtin_amdgcn_sched_barrier(0);
     if constexpr (STAMP) t1 = stamp();
-    f32x16 out;
-    net.hidden_all(Ha, Hb, out);
+    f32x16 out = eng.eval(B1);
     if constexpr (STAMP) t2 = stamp();
     float xi[D];
     if constexpr (NOISE) {
@@ -342,7 +370,11 @@ em_sampler_kernel(SamplerParams p) {
       rng_normals<D>(rng, xi);
     }
 #pragma unroll
-    for (int k = 0; k < D; ++k) x[k] = em_update(x[k], out[k], xi[k], cf, p.delta, p.sqrt_delta);
+    for (int k = 0; k < D; ++k) {
+      // PosteriorScore returns g * (prior + likelihood) (nets.py:155-157)
+      const float a = MODE == MODE_POSTERIOR ? __fmul_rn(cf.g, out[k]) : out[k];
+      x[k] = em_update(x[k], a, xi[k], cf, p.delta, p.sqrt_delta);
+    }
     if constexpr (STAMP) {
       const unsigned long long t3 = stamp();
       ph[0] += t1 - t0;
@@ -350,7 +382,7 @@ em_sampler_kernel(SamplerParams p) {
       ph[2] += t3 - t2;
     }
   }
-  net.epilogue();
+  eng.epilogue();
   if constexpr (STAMP) {
     const unsigned long long clk1 = stamp();
     const unsigned long long rt1 = __builtin_amdgcn_s_memrealtime();
@@ -379,14 +411,20 @@ mlp_forward_kernel(ForwardParams p) {
   // SPLIT: layer-1 slots [hi(v) | lo(v) | hi(v) | 1 | 1] (~fp32); otherwise [v | 1 | 1] (bf16 inputs,
   // used where the split image does not fit the LDS budget: width 512 with wide inputs)
   constexpr int K1S = SPLIT ? (3 * IN + 2 + 15) / 16 : (IN + 2 + 15) / 16;
-  using L = Lay<W, NL, K1S, R, RES>;
+  using L = Lay<W, NL, K1S, 1, R, RES>;
   static_assert(L::TOTAL <= 160 * 1024, "LDS budget");
   __shared__ __attribute__((aligned(16))) char lds[L::TOTAL];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int h = lane >> 5;
-  Net<W, NL, K1S, NW, R, RES, true> net{lds, p.hidden, 0, w, lane};
-  net.prologue(p.a1, p.ao, p.bias_hidden, p.bias_out);
+  Engine<W, NL, K1S, 1, NW, R, RES, true> net{lds, {p.hidden, p.hidden}, 0, w, lane};
+  {
+    const char* const a1[2] = {p.a1, p.a1};
+    const char* const ao[2] = {p.ao, p.ao};
+    const float* const bh[2] = {p.bias_hidden, p.bias_hidden};
+    const float* const bo[2] = {p.bias_out, p.bias_out};
+    net.prologue(a1, ao, bh, bo);
+  }
 
   const long long n_tiles = (p.n + 31) / 32;
   const long long rounds = (n_tiles + (long long)gridDim.x * NW - 1) / ((long long)gridDim.x * NW);
@@ -516,13 +554,20 @@ __global__ void schedule_kernel(int S, float T, float bmin, float bdiff, float* 
 }
 
 // ------------------------------------------------------------------------------ dispatch
-template <int W, int NL, int D, int NW, int R, bool RES>
+template <int MODE, int W, int NL, int D, int M, int NW, int R, bool RES>
 static hipError_t launch_sampler_t(const SamplerParams& p, int n_y, hipStream_t st) {
   const long long per_wg = NW * 32;
   dim3 grid((unsigned)((p.n_chains + per_wg - 1) / per_wg), (unsigned)n_y);
-  if (p.stamps) hipLaunchKernelGGL((em_sampler_kernel<W, NL, D, NW, R, RES, false, true>), grid, dim3(NW * 64), 0, st, p);
-  else if (p.noise) hipLaunchKernelGGL((em_sampler_kernel<W, NL, D, NW, R, RES, true>), grid, dim3(NW * 64), 0, st, p);
-  else hipLaunchKernelGGL((em_sampler_kernel<W, NL, D, NW, R, RES, false>), grid, dim3(NW * 64), 0, st, p);
+  if constexpr (MODE == MODE_CDE) {
+    if (p.stamps)
+      hipLaunchKernelGGL((em_sampler_kernel<MODE, W, NL, D, M, NW, R, RES, false, true>), grid, dim3(NW * 64), 0, st, p);
+    else if (p.noise)
+      hipLaunchKernelGGL((em_sampler_kernel<MODE, W, NL, D, M, NW, R, RES, true>), grid, dim3(NW * 64), 0, st, p);
+    else
+      hipLaunchKernelGGL((em_sampler_kernel<MODE, W, NL, D, M, NW, R, RES, false>), grid, dim3(NW * 64), 0, st, p);
+  } else {
+    hipLaunchKernelGGL((em_sampler_kernel<MODE, W, NL, D, M, NW, R, RES, false>), grid, dim3(NW * 64), 0, st, p);
+  }
   return hipGetLastError();
 }
 
@@ -536,65 +581,60 @@ static hipError_t launch_forward_t(const ForwardParams& p, hipStream_t st) {
   return hipGetLastError();
 }
 
-// Supported shapes: the BASELINE widths (64 linear, 256 scatterometry) plus 128; three hidden
-// layers (config_*.yml use [W]*3). Width 512 is not instantiated yet.
-#define DMIP_W_CASES(X, NL, D) \
-  X(64, NL, D, 8, 0, true)     \
-  X(128, NL, D, 8, 0, true)    \
-  X(256, NL, D, 8, 4, false)   \
-  X(512, NL, D, 4, 3, false)
+// Compiled shapes: widths 64 / 128 (hidden layers LDS-resident), 256 (4-slot ring) and 512 (4-wave
+// workgroups, 3 x 32 KiB ring slots; CDE only); 2 or 3 hidden layers; xdim 2 or 3. The CDE and
+// Posterior kernels take any ydim (y is folded into the per-y layer-1 bias, M = 0); CDiffE feeds y_t
+// through layer 1 and is compiled for the two problems' (xdim, ydim) = (2, 2) and (3, 23).
+#define DMIP_W_CASES(X, MODE, NL, D, M) \
+  X(MODE, 64, NL, D, M, 8, 0, true)     \
+  X(MODE, 128, NL, D, M, 8, 0, true)    \
+  X(MODE, 256, NL, D, M, 8, 4, false)
+#define DMIP_W512_CASE(X, MODE, NL, D, M) X(MODE, 512, NL, D, M, 4, 3, false)
+#define DMIP_NO_W512(X, MODE, NL, D, M)
+#define DMIP_SHAPES(X, MODE, W512, M2, M3)                              \
+  DMIP_W_CASES(X, MODE, 3, 2, M2) DMIP_W_CASES(X, MODE, 3, 3, M3)      \
+  DMIP_W_CASES(X, MODE, 2, 2, M2) DMIP_W_CASES(X, MODE, 2, 3, M3)      \
+  W512(X, MODE, 3, 2, M2) W512(X, MODE, 3, 3, M3) W512(X, MODE, 2, 2, M2) W512(X, MODE, 2, 3, M3)
+#define DMIP_ALL_SHAPES(X)                                \
+  DMIP_SHAPES(X, MODE_CDE, DMIP_W512_CASE, 0, 0)          \
+  DMIP_SHAPES(X, MODE_POSTERIOR, DMIP_NO_W512, 0, 0)      \
+  DMIP_SHAPES(X, MODE_CDIFFE, DMIP_NO_W512, 2, 23)
 
-// Development knob (not part of the ABI): DMIP_SAMPLER_VARIANT=1 runs width 256 as two
-// independent 4-wave workgroups per CU (each with its own 3-slot ring) instead of one 8-wave one.
+// Development knob (not part of the ABI): DMIP_SAMPLER_VARIANT=10x runs the timing ablations
+// (DIAG = x) of the width-256 CDE sampler; see profiles/README.md.
 static int sampler_variant() {
   const char* e = getenv("DMIP_SAMPLER_VARIANT");
   return e ? atoi(e) : 0;
 }
 
-hipError_t launch_sampler(const SamplerParams& p, int width, int n_hidden, int xdim, int n_y, hipStream_t st,
-                          bool* supported) {
+hipError_t launch_sampler(const SamplerParams& p, int mode, int width, int n_hidden, int xdim, int ydim, int n_y,
+                          hipStream_t st, bool* supported) {
   *supported = true;
   const int var = sampler_variant();
-  if (width == 256 && var == 1) {
-    if (n_hidden == 3 && xdim == 3) return launch_sampler_t<256, 3, 3, 4, 3, false>(p, n_y, st);
-    if (n_hidden == 3 && xdim == 2) return launch_sampler_t<256, 3, 2, 4, 3, false>(p, n_y, st);
-  }
-  if (width == 256 && n_hidden == 3 && xdim == 3 && var >= 100 && var < 108) {
+  if (mode == MODE_CDE && width == 256 && n_hidden == 3 && xdim == 3 && var >= 101 && var <= 107) {
     dim3 grid((unsigned)((p.n_chains + 255) / 256), (unsigned)n_y);
     switch (var - 100) {
-#define DG(d) case d: hipLaunchKernelGGL((em_sampler_kernel<256, 3, 3, 8, 4, false, false, false, d>), grid, dim3(512), 0, st, p); break;
+#define DG(d) \
+  case d: hipLaunchKernelGGL((em_sampler_kernel<MODE_CDE, 256, 3, 3, 0, 8, 4, false, false, false, d>), grid, dim3(512), 0, st, p); break;
       DG(1) DG(2) DG(3) DG(4) DG(5) DG(6) DG(7)
 #undef DG
       default: break;
     }
     return hipGetLastError();
   }
-  if (width == 256 && n_hidden == 3 && xdim == 3 && var >= 2 && var <= 5) {  // instruction-order variants
-    dim3 grid((unsigned)((p.n_chains + 255) / 256), (unsigned)n_y);
-    if (var == 2) hipLaunchKernelGGL((em_sampler_kernel<256, 3, 3, 8, 4, false, false, false, 0, 0>), grid, dim3(512), 0, st, p);
-    if (var == 3) hipLaunchKernelGGL((em_sampler_kernel<256, 3, 3, 8, 4, false, false, false, 0, 3>), grid, dim3(512), 0, st, p);
-    if (var == 4) hipLaunchKernelGGL((em_sampler_kernel<256, 3, 3, 8, 4, false, false, false, 0, 4>), grid, dim3(512), 0, st, p);
-    if (var == 5) hipLaunchKernelGGL((em_sampler_kernel<256, 3, 3, 8, 4, false, false, false, 0, 5>), grid, dim3(512), 0, st, p);
-    return hipGetLastError();
-  }
-#define X(Wv, NLv, Dv, NWv, Rv, RESv) \
-  if (width == Wv && n_hidden == NLv && xdim == Dv) return launch_sampler_t<Wv, NLv, Dv, NWv, Rv, RESv>(p, n_y, st);
-  DMIP_W_CASES(X, 3, 2)
-  DMIP_W_CASES(X, 3, 3)
-  DMIP_W_CASES(X, 2, 2)
-  DMIP_W_CASES(X, 2, 3)
+#define X(MODEv, Wv, NLv, Dv, Mv, NWv, Rv, RESv)                                                  \
+  if (mode == MODEv && width == Wv && n_hidden == NLv && xdim == Dv && (Mv == 0 || ydim == Mv)) \
+    return launch_sampler_t<MODEv, Wv, NLv, Dv, Mv, NWv, Rv, RESv>(p, n_y, st);
+  DMIP_ALL_SHAPES(X)
 #undef X
   *supported = false;
   return hipSuccess;
 }
 
-bool sampler_shape_supported(int width, int n_hidden, int xdim) {
-#define X(Wv, NLv, Dv, NWv, Rv, RESv) \
-  if (width == Wv && n_hidden == NLv && xdim == Dv) return true;
-  DMIP_W_CASES(X, 3, 2)
-  DMIP_W_CASES(X, 3, 3)
-  DMIP_W_CASES(X, 2, 2)
-  DMIP_W_CASES(X, 2, 3)
+bool sampler_shape_supported(int mode, int width, int n_hidden, int xdim, int ydim) {
+#define X(MODEv, Wv, NLv, Dv, Mv, NWv, Rv, RESv) \
+  if (mode == MODEv && width == Wv && n_hidden == NLv && xdim == Dv && (Mv == 0 || ydim == Mv)) return true;
+  DMIP_ALL_SHAPES(X)
 #undef X
   return false;
 }
@@ -615,13 +655,12 @@ hipError_t launch_forward(const ForwardParams& p, int width, int n_hidden, int i
     *supported = false;
     return hipSuccess;
   }
-#define X(Wv, NLv, INv, NWv, Rv, RESv)                          \
-  if constexpr (Wv != 512)                                        \
-    if (width == Wv && n_hidden == NLv && in_dim == INv) return launch_forward_t<Wv, NLv, INv, NWv, Rv, RESv>(p, st);
-  DMIP_W_CASES(X, 3, 5)   // linear CDE: x(2) y(2) t
-  DMIP_W_CASES(X, 3, 27)  // scatterometry CDE: x(3) y(23) t
-  DMIP_W_CASES(X, 3, 3)   // linear prior MLP2: x(2) t
-  DMIP_W_CASES(X, 3, 4)   // scatterometry prior MLP2: x(3) t
+#define X(Wv, NWv, Rv, RESv, NLv, INv) \
+  if (width == Wv && n_hidden == NLv && in_dim == INv) return launch_forward_t<Wv, NLv, INv, NWv, Rv, RESv>(p, st);
+#define XW(NLv, INv) X(64, 8, 0, true, NLv, INv) X(128, 8, 0, true, NLv, INv) X(256, 8, 4, false, NLv, INv)
+  // CDE / likelihood nets x(2) y(2) t and x(3) y(23) t; prior MLP2 nets x t; CDiffE: same input widths
+  XW(3, 5) XW(3, 27) XW(3, 3) XW(3, 4) XW(2, 5) XW(2, 27) XW(2, 3) XW(2, 4)
+#undef XW
 #undef X
   *supported = false;
   return hipSuccess;

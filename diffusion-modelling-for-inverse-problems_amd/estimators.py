@@ -1,12 +1,13 @@
 """CDE / CDiffE / PosteriorDiffusionEstimator with the reference's construct-and-sample API
 (models/diffusion.py:14-229).
 
-Sampling is the hot path and runs on the HIP device only:
-  * CDE: one launch of the fused persistent reverse-SDE kernel for all num_steps
-    (libdmip dmip_em_sample). The chain state never leaves the registers.
-  * PosteriorDiffusionEstimator and the (repaired) CDiffE sampler: per-step launches of the fused
-    MFMA network kernel (dmip_mlp_forward) with the SDE update as device tensor ops; a fused
-    two-network / CDiffE kernel is the next step.
+Sampling is the hot path and runs on the HIP device only: one launch of the fused persistent
+reverse-SDE kernel for all num_steps, the chain state never leaving the registers --
+  * CDE: dmip_em_sample;
+  * PosteriorDiffusionEstimator: dmip_em_sample_posterior (prior + likelihood networks in one kernel);
+  * CDiffE (repaired sampler): dmip_em_sample_cdiffe.
+Shapes the library has no fused kernel for (dmip_sampler_supported) step through per-step launches
+of the MFMA network kernel (dmip_mlp_forward) with the SDE update as device tensor ops.
 There is no CPU sampling path: without a HIP device the samplers raise.
 
 RNG: the reference draws x0 and the per-step noise from torch's global generator. Here every chain
@@ -72,6 +73,19 @@ class BaseClassDiffusionModel:
         (num_steps + 1, n_y, num_samples, xdim) (slot 0 -> x0) in place of the internal RNG."""
         raise NotImplementedError
 
+    def _prepare(self, y, num_samples, num_steps, nets):
+        dev = self._exec_device(y)
+        ys = self._ys(y, dev)
+        for net in nets:
+            pdev = next(net.parameters()).device
+            if pdev != dev:
+                raise RuntimeError(f"dmip: score network is on {pdev}, y on {dev}")
+        base = self.sde.base_sde
+        if float(base.T) != float(self.sde.T):
+            raise ValueError("PluginReverseSDE.T must equal the base SDE's T")
+        out = torch.empty(ys.shape[0], int(num_samples), self.xdim, device=dev, dtype=torch.float32)
+        return dev, ys, _lib.vpsde(base.beta_min, base.beta_max, self.sde.T), out
+
     def sample_t(self, x, eps=1e-4):
         """Training times (models/diffusion.py:48-58)."""
         if self.sde.debias:
@@ -116,23 +130,15 @@ class CDE(BaseClassDiffusionModel):
 
     def sample_device(self, y, num_samples, num_steps=200, mean=0, std=1, seed=None, chain_offset=0,
                       noise=None):
-        dev = self._exec_device(y)
-        ys = self._ys(y, dev)
         net = self.sde.a
-        if next(net.parameters()).device != dev:
-            raise RuntimeError(f"dmip: score network is on {next(net.parameters()).device}, y on {dev}")
+        dev, ys, sde, out = self._prepare(y, num_samples, num_steps, [net])
         handle = net.dmip_handle(dev, self.xdim)
-        base = self.sde.base_sde
-        if float(base.T) != float(self.sde.T):
-            raise ValueError("PluginReverseSDE.T must equal the base SDE's T")
         seed = _draw_seed() if seed is None else seed
-        out = torch.empty(ys.shape[0], int(num_samples), self.xdim, device=dev, dtype=torch.float32)
         if noise is not None:
             noise = noise.to(device=dev, dtype=torch.float32).contiguous()
             if tuple(noise.shape) != (int(num_steps) + 1, ys.shape[0], int(num_samples), self.xdim):
                 raise ValueError("noise must have shape (num_steps+1, n_y, num_samples, xdim)")
-        _lib.em_sample(handle, _lib.vpsde(base.beta_min, base.beta_max, self.sde.T), ys, num_samples,
-                       chain_offset, num_steps, mean, std, seed, out, noise)
+        _lib.em_sample(handle, sde, ys, num_samples, chain_offset, num_steps, mean, std, seed, out, noise)
         return out
 
     def train_epoch(self, optimizer, loss_fn, epoch_data_loader):
@@ -147,7 +153,7 @@ class CDE(BaseClassDiffusionModel):
 
 def _em_device_loop(model, ys, num_samples, num_steps, mean, std, seed, chain_offset, drift, zdim,
                     keep, y_resample=None):
-    """Reverse-SDE EM loop on device tensors for the estimators without a fused kernel yet: the
+    """Reverse-SDE EM loop on device tensors for shapes without a compiled fused sampler: the
     network evaluations are dmip_mlp_forward launches, the update follows
     models/diffusion.py:40-42 (same rounding order as the fused kernel)."""
     dev = ys.device
@@ -194,9 +200,13 @@ class CDiffE(BaseClassDiffusionModel):
                       noise=None):
         if noise is not None:
             raise ValueError("noise injection is only implemented for the fused CDE sampler")
-        dev = self._exec_device(y)
-        ys = self._ys(y, dev)
+        net = self.sde.a
+        dev, ys, sde, out = self._prepare(y, num_samples, num_steps, [net])
         seed = _draw_seed() if seed is None else seed
+        handle = net.dmip_handle(dev, self.xdim)
+        if _lib.sampler_supported(handle.width, handle.n_hidden, self.xdim, self.ydim, _lib.DMIP_SAMPLER_CDIFFE):
+            _lib.em_sample_cdiffe(handle, sde, ys, num_samples, chain_offset, num_steps, mean, std, seed, out)
+            return out
         base = self.sde.base_sde
         xd = self.xdim
 
@@ -241,9 +251,16 @@ class PosteriorDiffusionEstimator(BaseClassDiffusionModel):
                       noise=None):
         if noise is not None:
             raise ValueError("noise injection is only implemented for the fused CDE sampler")
-        dev = self._exec_device(y)
-        ys = self._ys(y, dev)
+        score = self.sde.a
+        dev, ys, sde, out = self._prepare(y, num_samples, num_steps, [score.prior_net, score.likelihood_net])
         seed = _draw_seed() if seed is None else seed
+        prior = score.prior_net.dmip_handle(dev, self.xdim)
+        lik = score.likelihood_net.dmip_handle(dev, self.xdim)
+        if (prior.width, prior.n_hidden) == (lik.width, lik.n_hidden) and _lib.sampler_supported(
+                lik.width, lik.n_hidden, self.xdim, self.ydim, _lib.DMIP_SAMPLER_POSTERIOR):
+            _lib.em_sample_posterior(prior, lik, sde, ys, num_samples, chain_offset, num_steps, mean, std, seed,
+                                     out)
+            return out
         base = self.sde.base_sde
 
         def drift(x, y, tvec):

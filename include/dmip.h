@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define DMIP_ABI_VERSION 1
+#define DMIP_ABI_VERSION 2
 
 typedef enum {
   DMIP_OK = 0,
@@ -47,6 +47,9 @@ typedef struct {
   double beta_max;
   double T;
 } dmip_vpsde;
+
+/* The three estimators' reverse samplers (models/diffusion.py:59-229). */
+typedef enum { DMIP_SAMPLER_CDE = 0, DMIP_SAMPLER_POSTERIOR = 1, DMIP_SAMPLER_CDIFFE = 2 } dmip_sampler_mode;
 
 typedef struct dmip_mlp dmip_mlp;
 
@@ -88,6 +91,27 @@ int dmip_em_sample(const dmip_mlp* net, const dmip_vpsde* sde, const float* y_de
                    int64_t n_chains, int64_t chain_offset, int num_steps, float mean, float stdv, uint64_t seed,
                    int precision, const float* noise_dev, float* x_out_dev, void* stream);
 
+/* Fused sampler of the PosteriorDiffusionEstimator (models/diffusion.py:182-229): the same EM loop as
+ * dmip_em_sample with a = PosteriorScore(x, y, T-t) = g(T-t) (prior(x, T-t) + likelihood(x, y, T-t))
+ * (nets.py:143-157). Both networks are evaluated in the same kernel from one shared weight ring.
+ *   prior       MLP2 handle (DMIP_INPUT_X_T, in_dim = xdim + 1, out_dim = xdim)
+ *   likelihood  MLP handle (DMIP_INPUT_X_Y_T, in_dim = xdim + ydim + 1, out_dim = xdim)
+ * Both must have the same hidden width and depth. Other arguments as dmip_em_sample (no injection). */
+int dmip_em_sample_posterior(const dmip_mlp* prior, const dmip_mlp* likelihood, const dmip_vpsde* sde,
+                             const float* y_dev, int n_y, int ydim, int xdim, int64_t n_chains, int64_t chain_offset,
+                             int num_steps, float mean, float stdv, uint64_t seed, int precision, float* x_out_dev,
+                             void* stream);
+
+/* Fused sampler of CDiffE (models/diffusion.py:109-180; the reference's loop raises TypeError at
+ * :174, so this implements the repaired semantics consistent with its training, :129-137): every
+ * step re-diffuses the observation, y_t = eps std(T-t) + mean_weight(T-t) y (sdes.py:37-44), evaluates
+ * the joint score a(x, y_t, T-t) (out_dim = xdim + ydim) and takes the EM step on the x part.
+ *   net   MLP handle (DMIP_INPUT_X_Y_T, in_dim = xdim + ydim + 1, out_dim = xdim + ydim)
+ * Other arguments as dmip_em_sample (no injection). */
+int dmip_em_sample_cdiffe(const dmip_mlp* net, const dmip_vpsde* sde, const float* y_dev, int n_y, int ydim, int xdim,
+                          int64_t n_chains, int64_t chain_offset, int num_steps, float mean, float stdv, uint64_t seed,
+                          int precision, float* x_out_dev, void* stream);
+
 /* Test hooks for the parity suite (integer RNG stream, normals, schedule). */
 int dmip_rng_words(uint64_t seed, int64_t chain_offset, uint64_t stream_id, int64_t n_chains, int n_words,
                    uint32_t* out_dev, void* stream);
@@ -108,8 +132,8 @@ int dmip_em_sample_stamps(const dmip_mlp* net, const dmip_vpsde* sde, const floa
 
 const char* dmip_last_error(void);
 int dmip_abi_version(void);
-/* Non-zero when this build has a kernel for the given sampler shape. */
-int dmip_sampler_supported(int width, int n_hidden, int xdim);
+/* Non-zero when this build has a kernel for the given sampler (dmip_sampler_mode) and shape. */
+int dmip_sampler_supported(int mode, int width, int n_hidden, int xdim, int ydim);
 
 #ifdef __cplusplus
 }

@@ -272,6 +272,42 @@ def cde_sample(params, y, num_samples, num_steps, seed, mean=0.0, std=1.0, chain
                      rng_state=st, xdim=xdim)
 
 
+def posterior_sample(prior_params, lik_params, y, num_samples, num_steps, seed, mean=0.0, std=1.0,
+                     chain_offset=0, stream=0, T=1.0):
+    """Product-RNG PosteriorDiffusionEstimator sampler (models/diffusion.py:27-46 with the
+    PosteriorScore drift a = g (prior + lik), nets.py:155-157): same RNG consumption as CDE."""
+    xdim = lik_params[-1][0].shape[0]
+    st = rng_init(seed, np.arange(chain_offset, chain_offset + num_samples), stream)
+    x0 = (rng_normals(st, xdim) * F32(std) + F32(mean)).astype(F32)
+    y = np.asarray(y, F32)
+    return em_sample(lambda x, tau: posterior_a(prior_params, lik_params, x, y, tau), x0, num_steps, T=T,
+                     rng_state=st, xdim=xdim)
+
+
+def cdiffe_sample(params, y, num_samples, num_steps, seed, mean=0.0, std=1.0, chain_offset=0, stream=0,
+                  T=1.0, beta_min=BETA_MIN, beta_max=BETA_MAX):
+    """Product-RNG CDiffE sampler, repaired semantics of models/diffusion.py:158-180 (the reference
+    loop raises TypeError at :174): per step y_t = eps std(T-t) + mean_weight(T-t) y
+    (sdes.py:37-44, eps = ydim fresh normals), a = net(x, y_t, T-t)[:, :xdim], then the EM update of
+    the x part with xdim fresh normals. x0 as CDE."""
+    xdim = params[0][0].shape[1] - np.asarray(y).shape[-1] - 1
+    ydim = np.asarray(y).shape[-1]
+    st = rng_init(seed, np.arange(chain_offset, chain_offset + num_samples), stream)
+    x = (rng_normals(st, xdim) * F32(std) + F32(mean)).astype(F32)
+    y = np.asarray(y, F32).reshape(1, ydim)
+    ts, tau = schedule(num_steps, T)
+    delta = float(T) / num_steps
+    for i in range(num_steps):
+        mw = vp_mean_weight(tau[i], beta_min, beta_max)
+        sd = np.sqrt(vp_var(tau[i], beta_min, beta_max)).astype(F32)
+        eps = rng_normals(st, ydim)
+        y_t = ((eps * sd).astype(F32) + (mw * y).astype(F32)).astype(F32)
+        a = cde_a(params, x, y_t, tau[i])[:, :xdim]
+        xi = rng_normals(st, xdim)
+        x = em_step(x, a, tau[i], delta, beta_min, beta_max, xi)
+    return x
+
+
 # ------------------------------------------------------------------------------------------
 # A11  evaluation metric -- main_diffusion_scatterometry.py:71-102
 # ------------------------------------------------------------------------------------------

@@ -31,8 +31,8 @@ def test_exports_every_declared_symbol(lib, dmip):
     assert set(syms) == set(dmip._lib.EXPORTED)
 
 
-def test_abi_version(lib):
-    assert lib.dmip_abi_version() == 1
+def test_abi_version(lib, dmip):
+    assert lib.dmip_abi_version() == dmip._lib.ABI_VERSION == 2
 
 
 def test_supported_shapes(lib, dmip):
@@ -40,6 +40,11 @@ def test_supported_shapes(lib, dmip):
     assert sup(256, 3, 3) and sup(64, 3, 2) and sup(128, 3, 3)
     assert not sup(96, 3, 3)
     assert not sup(256, 3, 9)
+    assert sup(512, 3, 3, 23) and sup(256, 3, 3, 5)  # CDE: any ydim
+    P, C = dmip._lib.DMIP_SAMPLER_POSTERIOR, dmip._lib.DMIP_SAMPLER_CDIFFE
+    assert sup(256, 3, 2, 2, P) and sup(64, 2, 3, 23, P) and not sup(512, 3, 3, 23, P)
+    assert sup(256, 3, 3, 23, C) and sup(128, 3, 2, 2, C)
+    assert not sup(256, 3, 3, 5, C)  # CDiffE feeds y_t through layer 1: compiled ydim only
 
 
 def test_create_rejects_bad_arguments(lib, dmip):
@@ -65,6 +70,11 @@ def test_sampler_rejects_null_handle(lib, dmip):
     L = dmip._lib
     sde = L.vpsde(0.1, 20.0, 1.0)
     rc = lib.dmip_em_sample(None, ctypes.byref(sde), None, 1, 2, 2, 10, 0, 10, 0.0, 1.0, 1, 0, None, None, None)
+    assert rc == L.DMIP_ERR_INVALID
+    rc = lib.dmip_em_sample_posterior(None, None, ctypes.byref(sde), None, 1, 2, 2, 10, 0, 10, 0.0, 1.0, 1, 0,
+                                      None, None)
+    assert rc == L.DMIP_ERR_INVALID
+    rc = lib.dmip_em_sample_cdiffe(None, ctypes.byref(sde), None, 1, 2, 2, 10, 0, 10, 0.0, 1.0, 1, 0, None, None)
     assert rc == L.DMIP_ERR_INVALID
     rc = lib.dmip_schedule(0, ctypes.byref(sde), None, None)
     assert rc == L.DMIP_ERR_INVALID
