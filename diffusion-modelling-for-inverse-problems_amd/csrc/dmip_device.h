@@ -145,11 +145,16 @@ __device__ __forceinline__ float act_r(float zs) {
   return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(zs));
 }
 // tanh(tanh(z)) of the reference's first layer (nets.py:21-26 double Tanh) in r-form:
-// q = r(z); tanh(z) = 1 - 2q; r1 = r(2 log2e * (1 - 2q)). (An odd polynomial for the bounded outer
-// tanh measured no faster on gfx950: 6 dependent FMAs cost about what exp + rcp cost.)
+// q = r(z), tanh(z) = 1 - 2q, r1 = r(c (1 - 2q)) = 1 / (1 + 2^c 2^(-2cq)). The scale -2c is folded
+// into the first reciprocal (q' = 1 / fma(e, k, k) = -2c q with k = -1/(2c)) and 2^c into the second
+// denominator (fma(2^q', 2^c, 1)), so the two stages cost exp, fma, rcp, exp, fma, rcp.
+// (An odd polynomial for the bounded outer tanh costs as much VALU issue as exp + rcp on gfx950.)
 __device__ __forceinline__ float act_r_twice(float zs) {
-  const float q = act_r(zs);
-  return act_r(__builtin_fmaf(-2.0f * kTanhScale, q, kTanhScale));
+  constexpr float k = -1.0f / (2.0f * kTanhScale);
+  constexpr float two_c = 7.389056098930650f;  // 2^c = e^2
+  const float e = __builtin_amdgcn_exp2f(zs);
+  const float qs = __builtin_amdgcn_rcpf(__builtin_fmaf(e, k, k));
+  return __builtin_amdgcn_rcpf(__builtin_fmaf(__builtin_amdgcn_exp2f(qs), two_c, 1.0f));
 }
 
 template <bool TWICE, bool CAST_ONLY = false>

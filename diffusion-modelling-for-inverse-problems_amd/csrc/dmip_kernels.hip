@@ -73,7 +73,11 @@ __device__ __forceinline__ void mfma_row_tile(const char* a_lane, const bf16x8 (
 // accumulator tile (rows = output dims; the host packers define the row maps).
 // DIAG (timing ablations only, never on the product path): bit 0 = no ring barrier/DMA,
 // bit 1 = hidden activations replaced by a bf16 cast, bit 2 = layer-1 activation replaced by a cast.
-template <int W, int NL, int K1S, int NNET, int NW, int R, bool RES, bool CONSERVATIVE, int DIAG = 0>
+// SPLIT: the two waves of a SIMD (waves w and w + NW/2) issue a hidden tile in complementary orders
+// (MFMAs first / previous tile's activation first) so one wave's VALU work runs beside the other's
+// MFMAs instead of both waves wanting the same pipe in lockstep.
+template <int W, int NL, int K1S, int NNET, int NW, int R, bool RES, bool CONSERVATIVE, int DIAG = 0,
+          bool SPLIT = false>
 struct Engine {
   using L = Lay<W, NL, K1S, NNET, R, RES>;
   static constexpr int T = L::T;
@@ -139,10 +143,26 @@ struct Engine {
       } else {
         wb = chunk_sync();
       }
-      f32x16 acc = bias_tile(L::BH_OFF + NI * L::BH_BYTES + ((LI * T + rt) * 2) * 64);
-      mfma_row_tile<KS>(wb + lane * 16, Hin, acc);
-      if (rt > 0) act_pack<false, (DIAG & 2) != 0>(pend, Hout[2 * (rt - 1)], Hout[2 * (rt - 1) + 1]);
-      pend = acc;
+      if constexpr (SPLIT) {
+        if (w >= NW / 2) {  // activation first
+          if (rt > 0) act_pack<false, (DIAG & 2) != 0>(pend, Hout[2 * (rt - 1)], Hout[2 * (rt - 1) + 1]);
+          __builtin_amdgcn_sched_barrier(0);
+          f32x16 acc = bias_tile(L::BH_OFF + NI * L::BH_BYTES + ((LI * T + rt) * 2) * 64);
+          mfma_row_tile<KS>(wb + lane * 16, Hin, acc);
+          pend = acc;
+        } else {  // MFMAs first
+          f32x16 acc = bias_tile(L::BH_OFF + NI * L::BH_BYTES + ((LI * T + rt) * 2) * 64);
+          mfma_row_tile<KS>(wb + lane * 16, Hin, acc);
+          __builtin_amdgcn_sched_barrier(0);
+          if (rt > 0) act_pack<false, (DIAG & 2) != 0>(pend, Hout[2 * (rt - 1)], Hout[2 * (rt - 1) + 1]);
+          pend = acc;
+        }
+      } else {
+        f32x16 acc = bias_tile(L::BH_OFF + NI * L::BH_BYTES + ((LI * T + rt) * 2) * 64);
+        mfma_row_tile<KS>(wb + lane * 16, Hin, acc);
+        if (rt > 0) act_pack<false, (DIAG & 2) != 0>(pend, Hout[2 * (rt - 1)], Hout[2 * (rt - 1) + 1]);
+        pend = acc;
+      }
     }
     act_pack<false, (DIAG & 2) != 0>(pend, Hout[2 * (T - 1)], Hout[2 * (T - 1) + 1]);
   }
@@ -278,8 +298,10 @@ constexpr int k1s_of(int slots) { return (slots + 15) / 16; }
 // then mu = g a + 0.5 beta x, x <- x + delta mu + sqrt(delta) g xi.
 // STAMP: diagnostic build only (dmip_em_sample_stamps) -- per-wave cycle sums of the step phases
 // [layer 1 + B1, hidden layers, output layer + RNG + EM update], written to p.stamps.
+// TUNE (development variants): bit 0 = complementary tile order per wave half (Engine SPLIT),
+// bit 1 = s_setprio 1 for the second-dispatched wave half.
 template <int MODE, int W, int NL, int D, int M, int NW, int R, bool RES, bool NOISE, bool STAMP = false,
-          int DIAG = 0>
+          int DIAG = 0, int TUNE = 0>
 __global__ void __launch_bounds__(NW * 64, (NW * 64 + 255) / 256)
 em_sampler_kernel(SamplerParams p) {
   constexpr int NNET = MODE == MODE_POSTERIOR ? 2 : 1;
@@ -299,7 +321,10 @@ em_sampler_kernel(SamplerParams p) {
   const long long c_local = (long long)blockIdx.x * (NW * 32) + w * 32 + (lane & 31);
   const bool valid = c_local < p.n_chains;
 
-  Engine<W, NL, K1S, NNET, NW, R, RES, NOISE, DIAG> eng{lds, {p.hidden, p.hidden2}, 0, w, lane};
+  Engine<W, NL, K1S, NNET, NW, R, RES, NOISE, DIAG, (TUNE & 1) != 0> eng{lds, {p.hidden, p.hidden2}, 0, w, lane};
+  if constexpr ((TUNE & 2) != 0) {
+    if (w >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  }
   {
     const size_t a1_stride = (size_t)L::T * K1S * 1024;
     const char* const a1[2] = {p.a1 + (p.a1_per_y ? yi * a1_stride : 0), p.a1_2};
@@ -601,7 +626,8 @@ static hipError_t launch_forward_t(const ForwardParams& p, hipStream_t st) {
   DMIP_SHAPES(X, MODE_CDIFFE, DMIP_NO_W512, 2, 23)
 
 // Development knob (not part of the ABI): DMIP_SAMPLER_VARIANT=10x runs the timing ablations
-// (DIAG = x) of the width-256 CDE sampler; see profiles/README.md.
+// (DIAG = x) and 20x the tuning variants (TUNE = x) of the width-256 CDE sampler; see
+// profiles/README.md.
 static int sampler_variant() {
   const char* e = getenv("DMIP_SAMPLER_VARIANT");
   return e ? atoi(e) : 0;
@@ -618,6 +644,17 @@ hipError_t launch_sampler(const SamplerParams& p, int mode, int width, int n_hid
   case d: hipLaunchKernelGGL((em_sampler_kernel<MODE_CDE, 256, 3, 3, 0, 8, 4, false, false, false, d>), grid, dim3(512), 0, st, p); break;
       DG(1) DG(2) DG(3) DG(4) DG(5) DG(6) DG(7)
 #undef DG
+      default: break;
+    }
+    return hipGetLastError();
+  }
+  if (mode == MODE_CDE && width == 256 && n_hidden == 3 && xdim == 3 && var >= 201 && var <= 203) {
+    dim3 grid((unsigned)((p.n_chains + 255) / 256), (unsigned)n_y);
+    switch (var - 200) {
+#define TG(t) \
+  case t: hipLaunchKernelGGL((em_sampler_kernel<MODE_CDE, 256, 3, 3, 0, 8, 4, false, false, false, 0, t>), grid, dim3(512), 0, st, p); break;
+      TG(1) TG(2) TG(3)
+#undef TG
       default: break;
     }
     return hipGetLastError();

@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--width", type=int, default=256)
+    ap.add_argument("--check-equal", action="store_true",
+                    help="also check that every variant reproduces variant 0's samples bit for bit")
     a = ap.parse_args()
     pkg = importlib.import_module("diffusion-modelling-for-inverse-problems_amd")
     dev = torch.device("cuda:0")
@@ -38,6 +40,14 @@ def main():
         os.environ["DMIP_SAMPLER_VARIANT"] = str(v)
         m.sample_device(y, 4096, 10, seed=0)
     torch.cuda.synchronize()
+    equal = {}
+    if a.check_equal:
+        outs = {}
+        for v in a.variants:
+            os.environ["DMIP_SAMPLER_VARIANT"] = str(v)
+            outs[v] = m.sample_device(y, 8192, 50, seed=3)
+        for v in a.variants:
+            equal[f"v{v}"] = bool(torch.equal(outs[v], outs[a.variants[0]]))
     for r in range(a.rounds):
         for n in a.chains:
             for v in a.variants:
@@ -55,6 +65,8 @@ def main():
         med = float(np.median(ts))
         out[k] = {"ms_median": med, "ms_min": float(np.min(ts)), "samples_per_s": n / med * 1e3,
                   "tflops": F * a.steps * n / (med * 1e-3) / 1e12}
+    if equal:
+        out["bit_equal_to_first_variant"] = equal
     print(json.dumps(out, indent=1))
 
 
