@@ -334,3 +334,200 @@ def ks_2samp_stat(a, b):
     ca = np.searchsorted(a, z, side="right") / a.size
     cb = np.searchsorted(b, z, side="right") / b.size
     return float(np.max(np.abs(ca - cb)))
+
+
+# ------------------------------------------------------------------------------------------
+# A13-A17  DSM / ScoreFPE / PINN losses and their parameter gradients -- losses.py:42-242
+# Restated with explicit forward-mode jets and a hand-written reverse pass (the formulation of the
+# fused HIP training kernel), in float64. Pinned against the reference's autograd values and
+# gradients (tests/golden/pinn_linear.npz, G5) by tests/test_oracle_golden.py.
+# ------------------------------------------------------------------------------------------
+
+def _vp_terms(t, beta_min=BETA_MIN, beta_max=BETA_MAX):
+    """alpha, std, beta, g and their t-derivatives (sdes.py:21-35), float64."""
+    d = beta_max - beta_min
+    alpha = np.exp(-0.25 * t * t * d - 0.5 * t * beta_min)
+    e = np.exp(-0.5 * t * t * d - t * beta_min)
+    var = 1.0 - e
+    std = np.sqrt(var)
+    beta = beta_min + d * t
+    g = np.sqrt(beta)
+    dalpha = alpha * (-0.5 * t * d - 0.5 * beta_min)
+    dstd = e * (t * d + beta_min) / (2.0 * std)
+    dg = d / (2.0 * g)
+    return alpha, std, beta, g, dalpha, dstd, dg
+
+
+def loss_grad(params, x, y, t, eps, kind="pinn", pde="FPE", pde_metric="L1", ic_metric="L2", lam=1.0,
+              lam2=1.0, ic_A=None, ic_b=None, ic_Sinv=None, beta_min=BETA_MIN, beta_max=BETA_MAX):
+    """Loss value, components and parameter gradients of the CDE training losses for one batch,
+    with the reference's semantics (models/diffusion.py:80-89 -> losses.py):
+      kind 'dsm'     DSMLoss(a/g, std, eps).mean()                        (losses.py:42-52)
+      kind 'dsm_pde' DSM_PDELoss: mean(DSM + lam PDE)                      (losses.py:126-164)
+      kind 'pinn'    PINNLoss: mean(DSM + IC) + mean(lam PDE)              (losses.py:168-242)
+      kind 'pinn2'   PINNLoss2: mean(IC + lam PDE)                         (losses.py:245-290)
+    PDE 'FPE' = ScoreFPELoss (exact divergence; ds/dt the total derivative through x_t(t) and g(t);
+    grad_x detached), 'cFPE' = ConditionalScoreFPELoss. IC = lam2 * metric(a(x, y, 0)/g(0) - ic(x, y))
+    with ic the linear problem's analytic posterior score (linear_problem.py:61-65).
+    Network: nets.py:17-35 with the double tanh on layer 1. Returns (loss, comps, grads) where
+    grads = [(dW, db), ...] per linear layer."""
+    P = [(np.asarray(W, np.float64), np.asarray(b, np.float64)) for W, b in params]
+    x = np.asarray(x, np.float64)
+    y = np.asarray(y, np.float64)
+    t = np.asarray(t, np.float64).reshape(-1, 1)
+    eps = np.asarray(eps, np.float64)
+    B, d = x.shape
+    L = len(P)
+    alpha, std, beta, g, dalpha, dstd, dg = _vp_terms(t, beta_min, beta_max)
+    x_t = eps * std + alpha * x
+    xdot = dalpha * x + dstd * eps
+
+    def forward(u, udot_list, u2_list=None, with_bias=True):
+        """Primal + first-order tangents (list of input directions) + optional second-order
+        (pairs of tangent indices). Returns per-layer caches and outputs."""
+        caches = []
+        h = u
+        hd = list(udot_list)
+        h2 = {} if u2_list is None else {k: np.zeros_like(u) for k in u2_list}
+        for li, (W, b) in enumerate(P):
+            z = h @ W.T + (b if with_bias else 0.0)
+            zd = [v @ W.T for v in hd]
+            z2 = {k: v @ W.T for k, v in h2.items()}
+            if li == L - 1:
+                caches.append(dict(h_in=h, hd_in=hd))
+                return z, zd, z2, caches
+            if li == 0:
+                p = np.tanh(z)
+                hn = np.tanh(p)
+                d1 = (1 - hn * hn) * (1 - p * p)
+                d2 = -2 * (1 - p * p) * (hn * d1 + p * (1 - hn * hn))
+            else:
+                p = None
+                hn = np.tanh(z)
+                d1 = 1 - hn * hn
+                d2 = -2 * hn * d1
+            hdn = [d1 * v for v in zd]
+            h2n = {(a, c): d1 * z2[(a, c)] + d2 * zd[a] * zd[c] for (a, c) in z2}
+            caches.append(dict(h_in=h, hd_in=hd, z=z, zd=zd, d1=d1, d2=d2))
+            h, hd, h2 = hn, hdn, h2n
+        raise AssertionError
+
+    inp = lambda xx, yy, tt: np.concatenate([xx, yy, np.broadcast_to(tt, (xx.shape[0], 1))], axis=1)
+    u_P = inp(x_t, y, t)
+    e = np.zeros((B, u_P.shape[1]))
+    v_dir = e.copy()
+    v_dir[:, :d] = xdot
+    v_dir[:, -1] = 1.0
+    dirs = [v_dir]
+    if pde == "FPE":
+        for a in range(d):
+            ea = e.copy()
+            ea[:, a] = 1.0
+            dirs.append(ea)
+        pairs = [(1 + a, 1 + c) for a in range(d) for c in range(a, d)]
+    else:
+        pairs = None
+    aP, aT, a2, cache_P = forward(u_P, dirs, pairs)
+    s = aP / g
+    a_V = aT[0]
+    ds_dt = a_V / g - aP * dg / (g * g)
+    comps = {}
+    # DSM (losses.py:50-52)
+    r = s * std + eps
+    dsm_rows = 0.5 * np.sum(r * r, axis=1)
+    dL_ds = np.zeros_like(s)
+    dL_dV = np.zeros_like(s)
+    loss = 0.0
+    has_dsm = kind in ("dsm", "dsm_pde", "pinn")
+    has_pde = kind in ("dsm_pde", "pinn", "pinn2")
+    has_ic = kind in ("pinn", "pinn2")
+    comps["DSM"] = dsm_rows.mean()
+    if has_dsm:
+        loss += dsm_rows.mean()
+        dL_ds += r * std / B
+    if has_pde:
+        if pde == "FPE":
+            J = np.stack([aT[1 + a] / g for a in range(d)], axis=2)  # J[b, i, a] = ds_i/dx_a
+            H = {k: v / g for k, v in a2.items()}
+            div = sum(J[:, i, i] for i in range(d)).reshape(-1, 1)
+            grad_x = np.zeros_like(s)
+            for j in range(d):
+                for i in range(d):
+                    key = (1 + min(i, j), 1 + max(i, j))
+                    grad_x[:, j] += H[key][:, i]
+                    grad_x[:, j] += 2 * s[:, i] * J[:, i, j] + x_t[:, i] * J[:, i, j]
+                grad_x[:, j] += s[:, j]
+            u = ds_dt - 0.5 * beta * grad_x
+            if pde_metric == "L1":
+                rows = np.mean(np.abs(u), axis=1)
+                du = np.sign(u) / d
+            else:
+                rows = np.mean(u * u, axis=1)
+                du = 2 * u / d
+            dds = du  # d rows / d ds_dt
+            comps["div"] = div
+        else:
+            u = std ** 3 * ds_dt - 0.5 * eps * beta * alpha ** 2
+            if pde_metric == "L2":
+                rows = np.sum(u * u, axis=1)
+                du = 2 * u
+            else:
+                rows = np.sum(np.abs(u), axis=1)
+                du = np.sign(u)
+            dds = du * std ** 3
+        comps["ds_dt"] = ds_dt
+        comps["PDE"] = lam * rows.mean()
+        comps["pde_rows"] = rows
+        loss += lam * rows.mean()
+        dL_dV += lam * dds / B / g
+        dL_ds += lam * dds / B * (-dg / g)  # through ds_dt's -a g'/g^2 term (times g below)
+    dL_daP = dL_ds / g
+    grads = [(np.zeros_like(W), np.zeros_like(b)) for W, b in P]
+
+    def backward(cache, abar, adbar, u_in, with_bias=True):
+        """Reverse through the primal and the first tangent stream (direction 0)."""
+        zbar, zdbar = abar, adbar
+        for li in range(L - 1, -1, -1):
+            W, b = P[li]
+            c = cache[li]
+            hin = c["h_in"] if li > 0 else u_in
+            hdin = c["hd_in"][0] if li > 0 else cache[0]["hd_in"][0]
+            gW = zbar.T @ hin + (zdbar.T @ hdin if zdbar is not None else 0.0)
+            gb = zbar.sum(0) if with_bias else 0.0
+            grads[li] = (grads[li][0] + gW, grads[li][1] + gb)
+            if li == 0:
+                break
+            hbar = zbar @ W
+            hdbar = zdbar @ W if zdbar is not None else None
+            cp = cache[li - 1]
+            zbar_new = cp["d1"] * hbar
+            zdbar_new = None
+            if hdbar is not None:
+                zdbar_new = cp["d1"] * hdbar
+                zbar_new = zbar_new + cp["d2"] * cp["zd"][0] * hdbar
+            zbar, zdbar = zbar_new, zdbar_new
+
+    backward(cache_P, dL_daP, dL_dV, u_P)
+    if has_ic:
+        u_C = inp(x, y, np.zeros_like(t))
+        aC, _, _, cache_C = forward(u_C, [e])  # dummy tangent (zero direction)
+        g0 = np.sqrt(beta_min)
+        s0 = aC / g0
+        A = np.asarray(ic_A, np.float64)
+        bb = np.asarray(ic_b, np.float64)
+        S = np.asarray(ic_Sinv, np.float64)
+        ic = -x + ((y - (x @ A.T + bb)) @ S.T) @ A
+        dlt = s0[:, :d] - ic
+        if ic_metric == "L2":
+            rows = lam2 * np.mean(dlt * dlt, axis=1)
+            dd = lam2 * 2 * dlt / d
+        else:
+            rows = lam2 * np.mean(np.abs(dlt), axis=1)
+            dd = lam2 * np.sign(dlt) / d
+        comps["IC"] = rows.mean()
+        loss += rows.mean()
+        abar = np.zeros_like(aC)
+        abar[:, :d] = dd / B / g0
+        backward(cache_C, abar, None, u_C)
+    comps["loss"] = loss
+    return loss, comps, grads

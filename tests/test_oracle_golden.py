@@ -119,3 +119,32 @@ def test_reference_samples_fixture_consistent(golden):
         for k in range(q.shape[1]):
             med = np.median(s["samples"][:, k])
             assert abs(med - q[500, k]) < 0.05 * (q[990, k] - q[10, k])
+
+
+LOSS_CFGS = {
+    "pinn": dict(kind="pinn", pde="FPE", pde_metric="L1", ic_metric="L2", lam=1e-3, lam2=0.1),
+    "pinn_l1l2": dict(kind="pinn", pde="FPE", pde_metric="L2", ic_metric="L1", lam=0.5, lam2=0.3),
+    "dsmpde": dict(kind="dsm_pde", pde="FPE", pde_metric="L1", lam=1e-2),
+    "pinn_cfpe": dict(kind="pinn", pde="cFPE", pde_metric="L2", ic_metric="L2", lam=1e-3, lam2=0.1),
+    "dsm": dict(kind="dsm"),
+}
+LIN_IC = dict(ic_A=[[1, 0.5], [0, 1]], ic_b=[0.3, 0.5], ic_Sinv=np.eye(2) / 0.3)
+
+
+@pytest.mark.parametrize("name", list(LOSS_CFGS))
+def test_loss_grad_jets_match_reference_autograd(golden, name):
+    """The jet + hand-written-backward restatement (the fused training kernel's formulation) against
+    the reference's autograd losses and parameter gradients (G5)."""
+    z = golden("pinn_linear.npz")
+    params = O.mlp_params_from_state(dict(golden("ckpt_lin.npz")))
+    loss, comps, grads = O.loss_grad(params, z["x"], z["y"], z["t"], z["eps"], **LOSS_CFGS[name], **LIN_IC)
+    if name != "dsm":
+        assert loss == pytest.approx(float(z[f"{name}_loss"]), rel=5e-5)
+        assert comps["PDE"] == pytest.approx(float(z[f"{name}_PDE_Loss"]), rel=5e-5)
+    for (gW, gb), k in zip(grads, ["0", "3", "5", "7"]):
+        rW, rb = z[f"{name}_grad_{k}_weight"], z[f"{name}_grad_{k}_bias"]
+        assert np.abs(gW - rW).max() <= 1e-4 * np.abs(rW).max()
+        assert np.abs(gb - rb).max() <= 1e-4 * np.abs(rb).max()
+    if name == "dsmpde":
+        np.testing.assert_allclose(comps["div"], z["fpe_div"], rtol=1e-4, atol=1e-4)
+        np.testing.assert_allclose(comps["pde_rows"].reshape(-1, 1), z["fpe_rows"], rtol=1e-3, atol=1e-4)
