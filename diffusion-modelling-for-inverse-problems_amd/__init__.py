@@ -13,13 +13,14 @@ from .factory import get_model_from_args
 from .losses import (ConditionalScoreFPELoss, DSM_PDELoss, DSMLoss, PINNLoss, PINNLoss2, PosteriorLoss,
                      ScoreFPELoss, batch_gradient, divergence)
 from .nets import MLP, MLP2, PosteriorScore
+from .problems import LinearForwardProblem
 from .sdes import PluginReverseSDE, VariancePreservingSDE, sample_vp_truncated_q
 
 __all__ = [
     "BaseClassDiffusionModel", "CDE", "CDiffE", "PosteriorDiffusionEstimator", "get_model_from_args",
     "ConditionalScoreFPELoss", "DSM_PDELoss", "DSMLoss", "PINNLoss", "PINNLoss2", "PosteriorLoss",
     "ScoreFPELoss", "batch_gradient", "divergence", "MLP", "MLP2", "PosteriorScore",
-    "PluginReverseSDE", "VariancePreservingSDE", "sample_vp_truncated_q",
+    "PluginReverseSDE", "VariancePreservingSDE", "sample_vp_truncated_q", "LinearForwardProblem",
 ]
 
 

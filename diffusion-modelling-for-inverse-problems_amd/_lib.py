@@ -20,18 +20,28 @@ DMIP_INPUT_X_Y_T, DMIP_INPUT_X_T = 0, 1
 DMIP_ACT_TANH_TWICE_FIRST, DMIP_ACT_TANH = 0, 1
 DMIP_PREC_BF16 = 0
 DMIP_SAMPLER_CDE, DMIP_SAMPLER_POSTERIOR, DMIP_SAMPLER_CDIFFE = 0, 1, 2
-ABI_VERSION = 2
+ABI_VERSION = 3
+DMIP_LOSS_DSM, DMIP_LOSS_DSM_PDE, DMIP_LOSS_PINN, DMIP_LOSS_PINN2 = 0, 1, 2, 3
+DMIP_PDE_NONE, DMIP_PDE_FPE, DMIP_PDE_CFPE = 0, 1, 2
+DMIP_METRIC_L1, DMIP_METRIC_L2 = 0, 1
 
 # every symbol include/dmip.h declares (checked by tests/test_capi.py)
 EXPORTED = (
     "dmip_mlp_create", "dmip_mlp_destroy", "dmip_mlp_forward", "dmip_em_sample", "dmip_rng_words",
     "dmip_rng_normals", "dmip_schedule", "dmip_last_error", "dmip_abi_version", "dmip_sampler_supported",
-    "dmip_em_sample_stamps", "dmip_em_sample_posterior", "dmip_em_sample_cdiffe",
+    "dmip_em_sample_stamps", "dmip_em_sample_posterior", "dmip_em_sample_cdiffe", "dmip_loss_grad",
+    "dmip_loss_grad_supported",
 )
 
 
 class DmipVpsde(ctypes.Structure):
     _fields_ = [("beta_min", ctypes.c_double), ("beta_max", ctypes.c_double), ("T", ctypes.c_double)]
+
+
+class DmipLossCfg(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int), ("pde", ctypes.c_int), ("pde_metric", ctypes.c_int),
+                ("ic_metric", ctypes.c_int), ("lam", ctypes.c_float), ("lam2", ctypes.c_float),
+                ("ic_A", ctypes.c_float * 4), ("ic_b", ctypes.c_float * 2), ("ic_Sinv", ctypes.c_float * 4)]
 
 
 _c_void_p = ctypes.c_void_p
@@ -40,7 +50,7 @@ _f32 = ctypes.c_float
 
 _lib = None
 _lock = threading.Lock()
-calls = {"em_sample": 0, "mlp_forward": 0, "em_sample_posterior": 0, "em_sample_cdiffe": 0}  # instrumentation: proves the HIP path ran
+calls = {"em_sample": 0, "mlp_forward": 0, "em_sample_posterior": 0, "em_sample_cdiffe": 0, "loss_grad": 0}  # instrumentation: proves the HIP path ran
 
 
 def _declare(lib):
@@ -61,6 +71,11 @@ def _declare(lib):
                                              _c_void_p]
     lib.dmip_em_sample_cdiffe.argtypes = [_c_void_p, ctypes.POINTER(DmipVpsde), _c_void_p, _i32, _i32, _i32,
                                           _i64, _i64, _i32, _f32, _f32, _u64, _i32, _c_void_p, _c_void_p]
+    lib.dmip_loss_grad.argtypes = [_i32, _i32, _i32, ctypes.POINTER(_i32), _i32, ctypes.POINTER(_c_void_p),
+                                   ctypes.POINTER(_c_void_p), ctypes.POINTER(DmipVpsde), ctypes.POINTER(DmipLossCfg),
+                                   _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _c_void_p, _c_void_p,
+                                   _c_void_p]
+    lib.dmip_loss_grad_supported.argtypes = [_i32, _i32, _i32, ctypes.POINTER(_i32), _i32]
     lib.dmip_em_sample_stamps.argtypes = [_c_void_p, ctypes.POINTER(DmipVpsde), _c_void_p, _i32, _i32, _i32,
                                           _i64, _i32, _u64, _c_void_p, _c_void_p, _c_void_p]
     lib.dmip_rng_words.argtypes = [_u64, _i64, _u64, _i64, _i32, _c_void_p, _c_void_p]
@@ -68,7 +83,8 @@ def _declare(lib):
     lib.dmip_schedule.argtypes = [_i32, ctypes.POINTER(DmipVpsde), _c_void_p, _c_void_p]
     for name in ("dmip_mlp_create", "dmip_mlp_destroy", "dmip_mlp_forward", "dmip_em_sample",
                  "dmip_rng_words", "dmip_rng_normals", "dmip_schedule", "dmip_sampler_supported",
-                 "dmip_em_sample_stamps", "dmip_em_sample_posterior", "dmip_em_sample_cdiffe"):
+                 "dmip_em_sample_stamps", "dmip_em_sample_posterior", "dmip_em_sample_cdiffe",
+                 "dmip_loss_grad", "dmip_loss_grad_supported"):
         getattr(lib, name).restype = _i32
 
 
@@ -181,3 +197,20 @@ def em_sample_cdiffe(handle, sde, y, n_chains, chain_offset, num_steps, mean, st
 
 def sampler_supported(width, n_hidden, xdim, ydim=0, mode=DMIP_SAMPLER_CDE):
     return bool(lib().dmip_sampler_supported(mode, width, n_hidden, xdim, ydim))
+
+
+def loss_grad_supported(in_dim, out_dim, widths, xdim):
+    w = (_i32 * len(widths))(*widths)
+    return bool(lib().dmip_loss_grad_supported(in_dim, out_dim, len(widths), w, xdim))
+
+
+def loss_grad(layers, in_dim, out_dim, xdim, sde, cfg, x, y, t, eps, grad_out, loss_out):
+    """layers: [(weight, bias), ...] device fp32 tensors (the torch parameters)."""
+    calls["loss_grad"] += 1
+    L = len(layers) - 1
+    widths = (_i32 * L)(*[int(layers[i][0].shape[0]) for i in range(L)])
+    wp = (_c_void_p * (L + 1))(*[w.data_ptr() for w, _ in layers])
+    bp = (_c_void_p * (L + 1))(*[b.data_ptr() for _, b in layers])
+    check(lib().dmip_loss_grad(in_dim, out_dim, L, widths, xdim, wp, bp, ctypes.byref(sde), ctypes.byref(cfg),
+                               ptr(x), ptr(y), ptr(t), ptr(eps), int(x.shape[0]), ptr(grad_out), ptr(loss_out),
+                               stream_of(x.device)))

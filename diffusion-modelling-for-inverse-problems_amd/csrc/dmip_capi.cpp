@@ -11,6 +11,7 @@
 //     c = 2 log2(e) (exp2 instead of exp).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -421,6 +422,82 @@ int dmip_em_sample_stamps(const dmip_mlp* net, const dmip_vpsde* sde, const floa
   const SampleArgs a{sde,  y_dev, n_y,  ydim,           xdim,    n_chains,  0,      num_steps,
                      0.0f, 1.0f,  seed, DMIP_PREC_BF16, nullptr, x_out_dev, stream, stamps_dev};
   return em_sample_impl(DMIP_SAMPLER_CDE, net, nullptr, a);
+}
+
+static bool train_shape_ok(int in_dim, int out_dim, int n_hidden, const int* widths, int xdim) {
+  if (!widths || (n_hidden != 2 && n_hidden != 3)) return false;
+  for (int i = 0; i < n_hidden; ++i)
+    if (widths[i] != dmip::kTrainWidth) return false;
+  return xdim == dmip::kTrainXdim && out_dim == dmip::kTrainXdim &&
+         in_dim == dmip::kTrainXdim + dmip::kTrainYdim + 1;
+}
+
+int dmip_loss_grad_supported(int in_dim, int out_dim, int n_hidden, const int* widths, int xdim) {
+  return train_shape_ok(in_dim, out_dim, n_hidden, widths, xdim) ? 1 : 0;
+}
+
+int dmip_loss_grad(int in_dim, int out_dim, int n_hidden, const int* widths, int xdim,
+                   const float* const* weights_dev, const float* const* biases_dev, const dmip_vpsde* sde,
+                   const dmip_loss_cfg* cfg, const float* x_dev, const float* y_dev, const float* t_dev,
+                   const float* eps_dev, int64_t batch, float* grad_out_dev, float* loss_out_dev, void* stream) {
+  if (!weights_dev || !biases_dev || !sde || !cfg || !x_dev || !y_dev || !t_dev || !eps_dev || !grad_out_dev ||
+      !loss_out_dev)
+    return fail(DMIP_ERR_INVALID, "null argument");
+  if (!train_shape_ok(in_dim, out_dim, n_hidden, widths, xdim))
+    return fail(DMIP_ERR_UNSUPPORTED, "no compiled training kernel for this network (compiled: in 5, out 2, xdim 2, "
+                                      "widths 64, 2 or 3 hidden layers)");
+  for (int i = 0; i <= n_hidden; ++i)
+    if (!weights_dev[i] || !biases_dev[i]) return fail(DMIP_ERR_INVALID, "null layer pointer");
+  if (batch < 1) return fail(DMIP_ERR_INVALID, "batch must be >= 1");
+  if (cfg->kind < DMIP_LOSS_DSM || cfg->kind > DMIP_LOSS_PINN2) return fail(DMIP_ERR_INVALID, "unknown loss kind");
+  const bool needs_pde = cfg->kind != DMIP_LOSS_DSM;
+  if (needs_pde && cfg->pde != DMIP_PDE_FPE && cfg->pde != DMIP_PDE_CFPE)
+    return fail(DMIP_ERR_INVALID, "pde must be DMIP_PDE_FPE or DMIP_PDE_CFPE for this loss");
+  for (int m : {cfg->pde_metric, cfg->ic_metric})
+    if (m != DMIP_METRIC_L1 && m != DMIP_METRIC_L2) return fail(DMIP_ERR_INVALID, "metric must be L1 or L2");
+  if (!(sde->beta_min > 0.0)) return fail(DMIP_ERR_INVALID, "beta_min must be > 0");
+  hipStream_t st = (hipStream_t)stream;
+  dmip::TrainParams p{};
+  for (int i = 0; i <= n_hidden; ++i) p.w[i] = weights_dev[i], p.b[i] = biases_dev[i];
+  p.x = x_dev;
+  p.y = y_dev;
+  p.t = t_dev;
+  p.eps = eps_dev;
+  p.n = batch;
+  p.inv_n = (float)(1.0 / (double)batch);
+  p.bmin = (float)sde->beta_min;
+  p.bdiff = (float)(sde->beta_max - sde->beta_min);
+  p.has_dsm = cfg->kind == DMIP_LOSS_DSM || cfg->kind == DMIP_LOSS_DSM_PDE || cfg->kind == DMIP_LOSS_PINN;
+  p.has_ic = cfg->kind == DMIP_LOSS_PINN || cfg->kind == DMIP_LOSS_PINN2;
+  p.pde = needs_pde ? cfg->pde : 0;
+  p.pde_l1 = cfg->pde_metric == DMIP_METRIC_L1;
+  p.ic_l1 = cfg->ic_metric == DMIP_METRIC_L1;
+  p.lam = cfg->lam;
+  p.lam2 = cfg->lam2;
+  for (int i = 0; i < 4; ++i) p.icA[i] = cfg->ic_A[i], p.icS[i] = cfg->ic_Sinv[i];
+  p.icb[0] = cfg->ic_b[0];
+  p.icb[1] = cfg->ic_b[1];
+  // one 2-wave workgroup per CU (LDS-bound), 16-sample tiles strided over the waves
+  int n_cu = 256;
+  {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess &&
+        prop.multiProcessorCount > 0)
+      n_cu = prop.multiProcessorCount;
+  }
+  const int64_t tiles = (batch + 15) / 16;
+  const int64_t per_wg = dmip::train_waves_per_wg();
+  int n_wg = (int)std::min<int64_t>((int64_t)n_cu, (tiles + per_wg - 1) / per_wg);
+  if (n_wg < 1) n_wg = 1;
+  const size_t part_bytes = (size_t)n_wg * per_wg * dmip::train_partial_stride(n_hidden) * sizeof(float);
+  float* partials = nullptr;
+  hipError_t e = hipMallocAsync((void**)&partials, part_bytes, st);
+  if (e != hipSuccess) return fail(DMIP_ERR_ALLOC, std::string("hipMallocAsync: ") + hipGetErrorString(e));
+  e = dmip::launch_loss_grad(p, n_hidden, grad_out_dev, loss_out_dev, partials, n_wg, st);
+  (void)hipFreeAsync(partials, st);
+  if (e != hipSuccess) return hip_fail(e, "loss_grad launch");
+  return DMIP_OK;
 }
 
 int dmip_rng_words(uint64_t seed, int64_t chain_offset, uint64_t stream_id, int64_t n_chains, int n_words,

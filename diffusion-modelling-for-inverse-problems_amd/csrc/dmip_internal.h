@@ -57,6 +57,30 @@ struct A1PrepParams {
   int width, in_dim, xdim, ydim, y_col0, t_col, k1s;
 };
 
+// Fused training step (dmip_train.hip): the linear problem's width-64 CDE (x 2, y 2).
+constexpr int kTrainWidth = 64, kTrainXdim = 2, kTrainYdim = 2;
+
+struct TrainParams {
+  const float* w[4];          // device fp32 weights, nn.Linear layout [out][in], layers 0..n_hidden
+  const float* b[4];
+  const float* x;             // [n][xdim] clean samples
+  const float* y;             // [n][ydim]
+  const float* t;             // [n] diffusion times (sample_t)
+  const float* eps;           // [n][xdim] forward-diffusion noise (base_sde.sample's randn)
+  long long n;
+  float inv_n, bmin, bdiff;
+  int has_dsm, has_ic, pde, pde_l1, ic_l1;  // pde: 0 none, 1 ScoreFPE, 2 cScoreFPE
+  float lam, lam2;
+  float icA[4], icb[2], icS[4];  // linear-problem IC target: -x + ((y - (A x + b)) S^T) A
+  float* partials;            // [n_waves][partial stride]
+};
+
+int train_nparam(int n_hidden);
+int train_partial_stride(int n_hidden);
+int train_waves_per_wg();
+hipError_t launch_loss_grad(const TrainParams& p, int n_hidden, float* grads, float* loss_out, float* partials,
+                            int n_wg, hipStream_t st);
+
 hipError_t launch_sampler(const SamplerParams& p, int mode, int width, int n_hidden, int xdim, int ydim, int n_y,
                           hipStream_t st, bool* supported);
 bool sampler_shape_supported(int mode, int width, int n_hidden, int xdim, int ydim);

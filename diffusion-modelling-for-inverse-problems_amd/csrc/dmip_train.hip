@@ -1,0 +1,742 @@
+// Fused score-matching training step: loss value and parameter gradients of the CDE training losses
+// (losses.py:42-242 as called by CDE.train_epoch, models/diffusion.py:74-89) for one batch, in one
+// persistent kernel plus a deterministic reduction.
+//
+// Formulation (restated and pinned in oracle/dmip_oracle.py:loss_grad):
+//  * forward pass with forward-mode jets through the MLP (nets.py:17-35, double tanh on layer 1):
+//    primal P at (x_t, y, t); tangent V along d/dt of (x_t(t), y, t) (the total derivative of
+//    batch_gradient, losses.py:20-26); tangents E0, E1 along x_t (the divergence, losses.py:14-18) and
+//    second-order E00, E01, E11 (grad_x of div s, losses.py:88-89); IC primal C at (x, y, 0);
+//  * per-sample DSM / ScoreFPE / cScoreFPE / IC terms and their adjoints;
+//  * reverse pass through the P, V and C streams (grad_x is detached in the reference, so the
+//    E-streams need no reverse), recomputing the forward activations layer by layer instead of
+//    storing them; weight gradients as sample-contracted MFMA products through an LDS transpose.
+//
+// Precision: the primal-type streams (P, V, C) are split-bf16 products (W_hi h_hi + W_hi h_lo +
+// W_lo h_hi, ~fp32): near a trained optimum the loss adjoints are small residuals (s std + eps, the
+// FPE and IC residuals) and plain bf16 weights perturb the gradient by up to ~10 % (measured in a
+// numpy bf16 simulation of the trained fixture); the jet streams E* (detached grad_x) and the reverse
+// products stay plain bf16 (<0.5 % on the same fixture).
+//
+// Layout: 16 samples per tile and wave; every stream is a 64 x 16 (units x samples) matrix held as
+// four 16x16 accumulator tiles (v_mfma_f32_16x16x32_bf16: unit = 16R + 4(lane>>4) + reg, sample =
+// lane & 15), which repack into the next layer's B operand with no lane movement (k-permuted weight
+// fragments, as in the sampler). Weight-gradient products contract over samples and use
+// v_mfma_f32_32x32x16_bf16 (K = the tile's 16 samples). Each wave accumulates its gradient partial
+// in its own LDS region (deterministic), written out once; loss_grad_reduce_kernel sums the
+// partials in a fixed order.
+#include "dmip_device.h"
+#include "dmip_internal.h"
+
+namespace dmip {
+namespace train {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+constexpr int W = kTrainWidth;  // hidden width
+constexpr int D = kTrainXdim;   // xdim
+constexpr int M = kTrainYdim;   // ydim
+constexpr int IN = D + M + 1;   // cat[x, y, t] (nets.py:33)
+constexpr int OUT = D;          // CDE drift
+constexpr int NWV = 2;          // waves per workgroup
+constexpr int NS = 16;          // samples per tile
+constexpr int NSTREAM = 8;      // P, V, C, E0, E1, E00, E01, E11
+static_assert(W == 64 && D == 2, "compiled for the linear problem's width-64 CDE");
+static_assert(3 * IN + 2 <= 32, "layer-1 split operand fits one k-step");
+
+template <int NL>
+struct TL {
+  static constexpr int p_w(int l) { return l == 0 ? 0 : W * IN + W + (l - 1) * (W * W + W); }
+  static constexpr int p_b(int l) { return l == NL ? p_w(NL) + OUT * W : p_w(l) + (l == 0 ? W * IN : W * W); }
+  static constexpr int NPARAM = p_w(NL) + OUT * W + OUT;
+  static constexpr int PART = NPARAM + 4;                // per-wave partial: grads + 3 loss sums (+pad)
+  // LDS (bytes)
+  static constexpr int WF = 0;                           // forward fragments, hidden W x W layers (bf16 hi)
+  static constexpr int WFL = WF + (NL - 1) * 8192;       // their bf16 residuals (lo), for the split products
+  static constexpr int WT = WFL + (NL - 1) * 8192;       // transposed fragments (reverse pass)
+  static constexpr int A1 = WT + (NL - 1) * 8192;        // layer-1 split fragments
+  static constexpr int AO = A1 + 4096;                   // output layer, rows duplicated per lane group
+  static constexpr int AOL = AO + 2048;                  // its lo residuals
+  static constexpr int AOT = AOL + 2048;                 // output layer transposed
+  static constexpr int BIAS = AOT + 4096;                // fp32 [NL + 1][64]: b_l of hidden l, b_out at NL
+  static constexpr int COL = BIAS + (NL + 1) * W * 4;    // fp32 [D][64]: layer-1 weight columns of x
+  static constexpr int WAVE = COL + D * W * 4;
+  static constexpr int GACC = 0;                         // per wave: fp32 gradient partial (param order)
+  static constexpr int SCR = ((NPARAM * 4 + 15) / 16) * 16;  // per wave: 6 transposed [64][16] bf16
+  static constexpr int WAVE_BYTES = SCR + 6 * W * NS * 2;
+  static constexpr int TOTAL = WAVE + NWV * WAVE_BYTES;
+  static_assert(TOTAL <= 160 * 1024, "LDS budget");
+};
+
+__device__ __forceinline__ int kp(int s, int g, int j) { return 32 * s + 16 * (j >> 2) + 4 * g + (j & 3); }
+
+__device__ __forceinline__ __bf16 bf_hi(float v) { return (__bf16)v; }
+__device__ __forceinline__ __bf16 bf_lo(float v) { return (__bf16)(v - (float)(__bf16)v); }
+
+// tanh with full relative accuracy near 0 (the 1 - 2/(1+e^2z) form cancels there)
+__device__ __forceinline__ float tanh_f(float z) {
+  const float e = __builtin_amdgcn_exp2f(2.8853900817779268f * z);
+  const float t = 1.0f - 2.0f * __builtin_amdgcn_rcpf(1.0f + e);
+  const float z2 = z * z;
+  const float small = z * (1.0f - z2 * (0.33333333f - 0.13333333f * z2));
+  return fabsf(z) < 0.03125f ? small : t;
+}
+
+__device__ __forceinline__ float sgn(float v) { return (float)((v > 0.0f) - (v < 0.0f)); }
+
+// B operand of layer 1 for one stream: slots [hi(u) | lo(u) | hi(u) | one | one | 0...]; lane group g
+// supplies slots 8g..8g+7 of its sample
+__device__ __forceinline__ bf16x8 b1_operand(const float (&u)[IN], float one, int g) {
+  __bf16 sl[32];
+#pragma unroll
+  for (int k = 0; k < 32; ++k) {
+    if (k < IN) sl[k] = bf_hi(u[k]);
+    else if (k < 2 * IN) sl[k] = bf_lo(u[k - IN]);
+    else if (k < 3 * IN) sl[k] = bf_hi(u[k - 2 * IN]);
+    else if (k < 3 * IN + 2) sl[k] = (__bf16)one;
+    else sl[k] = (__bf16)0.0f;
+  }
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = g == 0 ? sl[j] : (g == 1 ? sl[8 + j] : (g == 2 ? sl[16 + j] : sl[24 + j]));
+  return r;
+}
+
+__device__ __forceinline__ const bf16x8& frag(const char* base, int idx, int lane) {
+  return *(const bf16x8*)(base + (idx * 64 + lane) * 16);
+}
+
+// write one acc-form stream (64 units x 16 samples) transposed: scr[unit][sample] bf16
+__device__ __forceinline__ void put_t(__bf16* scr, const f32x4 (&z)[4], int g, int c16) {
+#pragma unroll
+  for (int R = 0; R < 4; ++R)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) scr[(16 * R + 4 * g + r) * NS + c16] = (__bf16)z[R][r];
+}
+
+__device__ __forceinline__ void pack_b(const f32x4 (&z)[4], bf16x8 (&b)[2]) {
+#pragma unroll
+  for (int R = 0; R < 4; ++R)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) b[R >> 1][4 * (R & 1) + r] = (__bf16)z[R][r];
+}
+
+// split-bf16 B operand of an acc-form stream: hi = bf16(v), lo = bf16(v - hi)
+__device__ __forceinline__ void pack_b2(const f32x4 (&z)[4], bf16x8 (&b)[2], bf16x8 (&bl)[2]) {
+#pragma unroll
+  for (int R = 0; R < 4; ++R)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      b[R >> 1][4 * (R & 1) + r] = bf_hi(z[R][r]);
+      bl[R >> 1][4 * (R & 1) + r] = bf_lo(z[R][r]);
+    }
+}
+
+// one 16-row tile of W (two k-steps) times a stream: plain bf16, or split (~fp32)
+__device__ __forceinline__ f32x4 mm(const bf16x8& a0, const bf16x8& a1, const bf16x8 (&h)[2], f32x4 acc) {
+  acc = mfma16(a0, h[0], acc);
+  return mfma16(a1, h[1], acc);
+}
+__device__ __forceinline__ f32x4 mm3(const bf16x8& a0, const bf16x8& a1, const bf16x8& l0, const bf16x8& l1,
+                                     const bf16x8 (&h)[2], const bf16x8 (&hl)[2], f32x4 acc) {
+  acc = mfma16(l0, h[0], acc);
+  acc = mfma16(l1, h[1], acc);
+  acc = mfma16(a0, hl[0], acc);
+  acc = mfma16(a1, hl[1], acc);
+  acc = mfma16(a0, h[0], acc);
+  return mfma16(a1, h[1], acc);
+}
+
+// the 32x32x16 operand of a sample-contracted product: lane (i, hh) reads row (row0 + i), samples 8hh..8hh+7
+__device__ __forceinline__ bf16x8 tread(const __bf16* scr, int row, bool ok, int hh) {
+  if (!ok) return bf16x8{};
+  return *(const bf16x8*)(scr + row * NS + 8 * hh);
+}
+
+template <int NL>
+__global__ void __launch_bounds__(NWV * 64, 1) loss_grad_kernel(TrainParams p) {
+  using L = TL<NL>;
+  __shared__ __attribute__((aligned(16))) char lds[L::TOTAL];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int c16 = lane & 15, g = lane >> 4;
+  const int i32 = lane & 31, hh = lane >> 5;
+
+  // ---- pack the weights (fp32 device params, nn.Linear layout) into LDS fragments
+  {
+    __bf16* wf = (__bf16*)(lds + L::WF);
+    __bf16* wfl = (__bf16*)(lds + L::WFL);
+    __bf16* wt = (__bf16*)(lds + L::WT);
+    for (int e = tid; e < (NL - 1) * 4096; e += NWV * 64) {
+      const int l = e / 4096, r0 = e % 4096;
+      const int R = r0 / 1024, s = (r0 / 512) & 1, ln = (r0 / 8) & 63, j = r0 & 7;
+      const int row = 16 * R + (ln & 15), k = kp(s, ln >> 4, j);
+      const float* Wl = p.w[l + 1];
+      wf[e] = bf_hi(Wl[row * W + k]);
+      wfl[e] = bf_lo(Wl[row * W + k]);
+      wt[e] = (__bf16)Wl[k * W + row];
+    }
+    __bf16* a1 = (__bf16*)(lds + L::A1);
+    for (int e = tid; e < 2048; e += NWV * 64) {
+      const int R = e / 512, ln = (e / 8) & 63, j = e & 7;
+      const int row = 16 * R + (ln & 15), k = 8 * (ln >> 4) + j;
+      const float* W0 = p.w[0] + row * IN;
+      __bf16 o = (__bf16)0.0f;
+      if (k < IN) o = bf_hi(W0[k]);
+      else if (k < 2 * IN) o = bf_hi(W0[k - IN]);
+      else if (k < 3 * IN) o = bf_lo(W0[k - 2 * IN]);
+      else if (k == 3 * IN) o = bf_hi(p.b[0][row]);
+      else if (k == 3 * IN + 1) o = bf_lo(p.b[0][row]);
+      a1[e] = o;
+    }
+    __bf16* ao = (__bf16*)(lds + L::AO);
+    __bf16* aol = (__bf16*)(lds + L::AOL);
+    for (int e = tid; e < 1024; e += NWV * 64) {
+      const int s = e / 512, ln = (e / 8) & 63, j = e & 7;
+      const int o = (ln & 15) & 3;
+      const float v = o < OUT ? p.w[NL][o * W + kp(s, ln >> 4, j)] : 0.0f;
+      ao[e] = bf_hi(v);
+      aol[e] = bf_lo(v);
+    }
+    __bf16* aot = (__bf16*)(lds + L::AOT);
+    for (int e = tid; e < 2048; e += NWV * 64) {
+      const int R = e / 512, ln = (e / 8) & 63, j = e & 7;
+      const int unit = 16 * R + (ln & 15), k = 8 * (ln >> 4) + j;
+      aot[e] = k < OUT ? (__bf16)p.w[NL][k * W + unit] : (__bf16)0.0f;
+    }
+    float* bias = (float*)(lds + L::BIAS);
+    for (int e = tid; e < (NL + 1) * W; e += NWV * 64) {
+      const int l = e / W, u = e % W;
+      float v = 0.0f;
+      if (l >= 1 && l < NL) v = p.b[l][u];
+      else if (l == NL && u < OUT) v = p.b[NL][u];
+      bias[e] = v;
+    }
+    float* col = (float*)(lds + L::COL);
+    for (int e = tid; e < D * W; e += NWV * 64) col[e] = p.w[0][(e % W) * IN + e / W];
+    float* gacc = (float*)(lds + L::WAVE + w * L::WAVE_BYTES + L::GACC);
+    for (int e = lane; e < L::NPARAM; e += 64) gacc[e] = 0.0f;
+  }
+  __syncthreads();
+
+  const char* wfr = lds + L::WF;
+  const char* wtr = lds + L::WT;
+  const char* a1r = lds + L::A1;
+  const char* aor = lds + L::AO;
+  const char* aotr = lds + L::AOT;
+  const float* bias = (const float*)(lds + L::BIAS);
+  const float* col = (const float*)(lds + L::COL);
+  char* wave_base = lds + L::WAVE + w * L::WAVE_BYTES;
+  float* gacc = (float*)(wave_base + L::GACC);
+  __bf16* scr = (__bf16*)(wave_base + L::SCR);
+  auto S_ = [&](int k) { return scr + k * W * NS; };
+
+  f32x4 bbar[NL > 1 ? NL - 1 : 1][4];  // per-lane bias-gradient partials of the hidden W x W layers
+#pragma unroll
+  for (int l = 0; l < NL - 1; ++l)
+#pragma unroll
+    for (int R = 0; R < 4; ++R) bbar[l][R] = f32x4{};
+  float bobar[OUT] = {};
+  float lsum[3] = {0.0f, 0.0f, 0.0f};  // DSM, IC, PDE row sums (lane group 0 only)
+
+  const long long n_tiles = (p.n + NS - 1) / NS;
+  for (long long tile = (long long)blockIdx.x * NWV + w; tile < n_tiles; tile += (long long)gridDim.x * NWV) {
+    const long long si = tile * NS + c16;
+    const bool valid = si < p.n;
+    // ---------------------------------------------------------------- per-sample inputs
+    float x[D], y[M], eps[D], t;
+    if (valid) {
+#pragma unroll
+      for (int k = 0; k < D; ++k) x[k] = p.x[si * D + k], eps[k] = p.eps[si * D + k];
+#pragma unroll
+      for (int k = 0; k < M; ++k) y[k] = p.y[si * M + k];
+      t = p.t[si];
+    } else {
+#pragma unroll
+      for (int k = 0; k < D; ++k) x[k] = 0.0f, eps[k] = 0.0f;
+#pragma unroll
+      for (int k = 0; k < M; ++k) y[k] = 0.0f;
+      t = 0.5f;
+    }
+    // VP-SDE terms at t (sdes.py:21-44) and their t-derivatives
+    const float ex = __expf(-0.5f * t * t * p.bdiff - t * p.bmin);
+    const float alpha = __expf(-0.25f * t * t * p.bdiff - 0.5f * t * p.bmin);
+    const float std_ = sqrtf(1.0f - ex);
+    const float beta = p.bmin + p.bdiff * t;
+    const float gg = sqrtf(beta);
+    const float dalpha = alpha * (-0.5f * t * p.bdiff - 0.5f * p.bmin);
+    const float dstd = ex * (t * p.bdiff + p.bmin) / (2.0f * std_);
+    const float dg = p.bdiff / (2.0f * gg);
+    float xt[D], xd[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      xt[k] = eps[k] * std_ + alpha * x[k];
+      xd[k] = dalpha * x[k] + dstd * eps[k];
+    }
+    float uP[IN], uV[IN], uC[IN];
+#pragma unroll
+    for (int k = 0; k < D; ++k) uP[k] = xt[k], uV[k] = xd[k], uC[k] = x[k];
+#pragma unroll
+    for (int k = 0; k < M; ++k) uP[D + k] = y[k], uV[D + k] = 0.0f, uC[D + k] = y[k];
+    uP[IN - 1] = t, uV[IN - 1] = 1.0f, uC[IN - 1] = 0.0f;
+    const bf16x8 BP = b1_operand(uP, 1.0f, g), BV = b1_operand(uV, 0.0f, g), BC = b1_operand(uC, 1.0f, g);
+
+    // ======================================================== pass F: forward with jets
+    float aS[NSTREAM][OUT];
+    {
+      bf16x8 H[NSTREAM][2], HL[3][2];  // HL: lo residuals of the split streams P, V, C
+#pragma unroll
+      for (int R = 0; R < 4; ++R) {
+        const bf16x8 a = frag(a1r, R, lane);
+        const f32x4 zP = mfma16(a, BP, f32x4{}), zV = mfma16(a, BV, f32x4{}), zC = mfma16(a, BC, f32x4{});
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int u = 16 * R + 4 * g + r;
+          const float pz = tanh_f(zP[r]), h = tanh_f(pz);
+          const float q = 1.0f - pz * pz, k1 = 1.0f - h * h;
+          const float d1 = k1 * q, d2 = -2.0f * q * (h * d1 + pz * k1);
+          const float w0 = col[u], w1 = col[W + u];
+          const float v[NSTREAM] = {h, d1 * zV[r], tanh_f(tanh_f(zC[r])), d1 * w0, d1 * w1,
+                                    d2 * w0 * w0, d2 * w0 * w1, d2 * w1 * w1};
+#pragma unroll
+          for (int S = 0; S < NSTREAM; ++S) H[S][R >> 1][4 * (R & 1) + r] = bf_hi(v[S]);
+#pragma unroll
+          for (int S = 0; S < 3; ++S) HL[S][R >> 1][4 * (R & 1) + r] = bf_lo(v[S]);
+        }
+      }
+      for (int l = 1; l < NL; ++l) {
+        bf16x8 Hn[NSTREAM][2], HLn[3][2];
+        const char* wl = wfr + (l - 1) * 8192;
+        const char* wll = lds + L::WFL + (l - 1) * 8192;
+#pragma unroll
+        for (int R = 0; R < 4; ++R) {
+          const bf16x8 a0 = frag(wl, 2 * R, lane), a1 = frag(wl, 2 * R + 1, lane);
+          const bf16x8 l0 = frag(wll, 2 * R, lane), l1 = frag(wll, 2 * R + 1, lane);
+          f32x4 bt;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) bt[r] = bias[l * W + 16 * R + 4 * g + r];
+          f32x4 Z[NSTREAM];
+#pragma unroll
+          for (int S = 0; S < NSTREAM; ++S) {
+            Z[S] = (S == 0 || S == 2) ? bt : f32x4{};
+            if (S < 3) Z[S] = mm3(a0, a1, l0, l1, H[S], HL[S], Z[S]);
+            else Z[S] = mm(a0, a1, H[S], Z[S]);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float h = tanh_f(Z[0][r]);
+            const float d1 = 1.0f - h * h, d2 = -2.0f * h * d1;
+            const float v[NSTREAM] = {h,
+                                      d1 * Z[1][r],
+                                      tanh_f(Z[2][r]),
+                                      d1 * Z[3][r],
+                                      d1 * Z[4][r],
+                                      d1 * Z[5][r] + d2 * Z[3][r] * Z[3][r],
+                                      d1 * Z[6][r] + d2 * Z[3][r] * Z[4][r],
+                                      d1 * Z[7][r] + d2 * Z[4][r] * Z[4][r]};
+#pragma unroll
+            for (int S = 0; S < NSTREAM; ++S) Hn[S][R >> 1][4 * (R & 1) + r] = bf_hi(v[S]);
+#pragma unroll
+            for (int S = 0; S < 3; ++S) HLn[S][R >> 1][4 * (R & 1) + r] = bf_lo(v[S]);
+          }
+        }
+#pragma unroll
+        for (int S = 0; S < NSTREAM; ++S) H[S][0] = Hn[S][0], H[S][1] = Hn[S][1];
+#pragma unroll
+        for (int S = 0; S < 3; ++S) HL[S][0] = HLn[S][0], HL[S][1] = HLn[S][1];
+      }
+      const bf16x8 o0 = frag(aor, 0, lane), o1 = frag(aor, 1, lane);
+      const bf16x8 ol0 = frag(lds + L::AOL, 0, lane), ol1 = frag(lds + L::AOL, 1, lane);
+      f32x4 bo{};
+#pragma unroll
+      for (int r = 0; r < OUT; ++r) bo[r] = bias[NL * W + r];
+#pragma unroll
+      for (int S = 0; S < NSTREAM; ++S) {
+        f32x4 acc = (S == 0 || S == 2) ? bo : f32x4{};
+        if (S < 3) acc = mm3(o0, o1, ol0, ol1, H[S], HL[S], acc);
+        else acc = mm(o0, o1, H[S], acc);
+#pragma unroll
+        for (int k = 0; k < OUT; ++k) aS[S][k] = acc[k];
+      }
+    }
+
+    // ======================================================== per-sample loss terms and adjoints
+    float abP[OUT], abV[OUT], abC[OUT];
+    {
+      float s[OUT], dLds[OUT];
+#pragma unroll
+      for (int k = 0; k < OUT; ++k) s[k] = aS[0][k] / gg, dLds[k] = 0.0f, abV[k] = 0.0f, abC[k] = 0.0f;
+      float dsm = 0.0f;
+#pragma unroll
+      for (int k = 0; k < OUT; ++k) {
+        const float rr = s[k] * std_ + eps[k];
+        dsm += 0.5f * rr * rr;
+        if (p.has_dsm) dLds[k] += rr * std_ * p.inv_n;
+      }
+      float pde = 0.0f;
+      if (p.pde != 0) {
+        float dsdt[OUT], u[OUT], dds[OUT];
+#pragma unroll
+        for (int k = 0; k < OUT; ++k) dsdt[k] = aS[1][k] / gg - aS[0][k] * dg / (gg * gg);
+        if (p.pde == 1) {  // ScoreFPELoss (losses.py:78-98)
+          float J[OUT][D];
+#pragma unroll
+          for (int i = 0; i < OUT; ++i)
+#pragma unroll
+            for (int a = 0; a < D; ++a) J[i][a] = aS[3 + a][i] / gg;
+          // second-order streams: 5 = (0,0), 6 = (0,1), 7 = (1,1)
+#pragma unroll
+          for (int j = 0; j < D; ++j) {
+            float gx = s[j];
+#pragma unroll
+            for (int i = 0; i < OUT; ++i) {
+              const int lo = i < j ? i : j, hi = i < j ? j : i;
+              const int sidx = lo == 0 ? (hi == 0 ? 5 : 6) : 7;
+              gx += aS[sidx][i] / gg + (2.0f * s[i] + xt[i]) * J[i][j];
+            }
+            u[j] = dsdt[j] - 0.5f * beta * gx;
+          }
+          float rows = 0.0f;
+#pragma unroll
+          for (int k = 0; k < OUT; ++k) {
+            rows += p.pde_l1 ? fabsf(u[k]) : u[k] * u[k];
+            dds[k] = p.pde_l1 ? sgn(u[k]) / OUT : 2.0f * u[k] / OUT;
+          }
+          pde = p.lam * rows / OUT;
+        } else {  // ConditionalScoreFPELoss (losses.py:100-124)
+          const float s3 = std_ * std_ * std_;
+          float rows = 0.0f;
+#pragma unroll
+          for (int k = 0; k < OUT; ++k) {
+            u[k] = s3 * dsdt[k] - 0.5f * eps[k] * beta * alpha * alpha;
+            rows += p.pde_l1 ? fabsf(u[k]) : u[k] * u[k];
+            dds[k] = (p.pde_l1 ? sgn(u[k]) : 2.0f * u[k]) * s3;
+          }
+          pde = p.lam * rows;
+        }
+#pragma unroll
+        for (int k = 0; k < OUT; ++k) {
+          const float c = p.lam * dds[k] * p.inv_n;
+          abV[k] = c / gg;
+          dLds[k] += c * (-dg / gg);
+        }
+      }
+      float ic = 0.0f;
+      if (p.has_ic) {  // initial condition (losses.py:213-219) with the linear problem's score
+        const float g0 = sqrtf(p.bmin);
+        float res[M];
+#pragma unroll
+        for (int i = 0; i < M; ++i) res[i] = y[i] - (p.icA[i * D + 0] * x[0] + p.icA[i * D + 1] * x[1] + p.icb[i]);
+        float rs[M];
+#pragma unroll
+        for (int jj = 0; jj < M; ++jj) rs[jj] = res[0] * p.icS[jj * M + 0] + res[1] * p.icS[jj * M + 1];
+        float rows = 0.0f;
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+          const float target = -x[k] + rs[0] * p.icA[0 * D + k] + rs[1] * p.icA[1 * D + k];
+          const float dl = aS[2][k] / g0 - target;
+          rows += p.ic_l1 ? fabsf(dl) : dl * dl;
+          const float dd = p.lam2 * (p.ic_l1 ? sgn(dl) : 2.0f * dl) / D;
+          abC[k] = dd * p.inv_n / g0;
+        }
+        ic = p.lam2 * rows / D;
+      }
+#pragma unroll
+      for (int k = 0; k < OUT; ++k) abP[k] = dLds[k] / gg;
+      if (!valid) {
+#pragma unroll
+        for (int k = 0; k < OUT; ++k) abP[k] = abV[k] = abC[k] = 0.0f;
+      } else if (g == 0) {
+        lsum[0] += dsm;
+        lsum[1] += ic;
+        lsum[2] += pde;
+      }
+    }
+
+    // ======================================================== pass B: reverse with recomputation
+    f32x4 hbar[3][4];  // adjoint of the current layer's output, streams P, V, C (acc form)
+    for (int li = NL; li >= 0; --li) {
+      // ---- recompute P, V, C forward: h_{li-1} (B form + transposed into scratch 3..5) and z_li
+      bf16x8 H[3][2], HL[3][2];
+      f32x4 Z[3][4];
+      {
+#pragma unroll
+        for (int R = 0; R < 4; ++R) {
+          const bf16x8 a = frag(a1r, R, lane);
+          Z[0][R] = mfma16(a, BP, f32x4{});
+          Z[1][R] = mfma16(a, BV, f32x4{});
+          Z[2][R] = mfma16(a, BC, f32x4{});
+        }
+        for (int l = 1; l <= li && l <= NL; ++l) {
+          // activation of layer l-1 -> H
+          f32x4 Hf[3][4];
+#pragma unroll
+          for (int R = 0; R < 4; ++R)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              float h, d1, hc;
+              if (l == 1) {
+                const float pz = tanh_f(Z[0][R][r]);
+                h = tanh_f(pz);
+                d1 = (1.0f - h * h) * (1.0f - pz * pz);
+                hc = tanh_f(tanh_f(Z[2][R][r]));
+              } else {
+                h = tanh_f(Z[0][R][r]);
+                d1 = 1.0f - h * h;
+                hc = tanh_f(Z[2][R][r]);
+              }
+              Hf[0][R][r] = h;
+              Hf[1][R][r] = d1 * Z[1][R][r];
+              Hf[2][R][r] = hc;
+            }
+#pragma unroll
+          for (int S = 0; S < 3; ++S) pack_b2(Hf[S], H[S], HL[S]);
+          if (l == li) {
+#pragma unroll
+            for (int S = 0; S < 3; ++S) put_t(S_(3 + S), Hf[S], g, c16);
+          }
+          if (l == NL) break;  // li == NL: the output layer's pre-activation is not needed
+          const char* wl = wfr + (l - 1) * 8192;
+          const char* wll = lds + L::WFL + (l - 1) * 8192;
+#pragma unroll
+          for (int R = 0; R < 4; ++R) {
+            const bf16x8 a0 = frag(wl, 2 * R, lane), a1 = frag(wl, 2 * R + 1, lane);
+            const bf16x8 l0 = frag(wll, 2 * R, lane), l1 = frag(wll, 2 * R + 1, lane);
+            f32x4 bt;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) bt[r] = bias[l * W + 16 * R + 4 * g + r];
+#pragma unroll
+            for (int S = 0; S < 3; ++S) Z[S][R] = mm3(a0, a1, l0, l1, H[S], HL[S], S == 1 ? f32x4{} : bt);
+          }
+        }
+      }
+
+      if (li == NL) {
+        // ---- output layer: zbar = abar (per sample); W_NL-bar += abar h^T; b-bar; h-bar = W^T abar
+        const float* ab[3] = {abP, abV, abC};
+        if (g == 0) {
+#pragma unroll
+          for (int S = 0; S < 3; ++S)
+#pragma unroll
+            for (int o = 0; o < OUT; ++o) S_(S)[o * NS + c16] = (__bf16)ab[S][o];
+#pragma unroll
+          for (int o = 0; o < OUT; ++o) bobar[o] += abP[o] + abC[o];
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's scratch writes landed
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int U = 0; U < 2; ++U) {
+          f32x16 acc{};
+#pragma unroll
+          for (int S = 0; S < 3; ++S) {
+            const bf16x8 A = tread(S_(S), i32, i32 < OUT, hh);
+            const bf16x8 Bm = tread(S_(3 + S), 32 * U + i32, true, hh);
+            acc = mfma32(A, Bm, acc);
+          }
+          if (hh == 0) {
+#pragma unroll
+            for (int o = 0; o < OUT; ++o) gacc[L::p_w(NL) + o * W + 32 * U + i32] += acc[o];
+          }
+        }
+#pragma unroll
+        for (int S = 0; S < 3; ++S) {
+          bf16x8 Bm{};
+#pragma unroll
+          for (int j = 0; j < OUT; ++j) Bm[j] = g == 0 ? (__bf16)ab[S][j] : (__bf16)0.0f;
+#pragma unroll
+          for (int R = 0; R < 4; ++R) hbar[S][R] = mfma16(frag(aotr, R, lane), Bm, f32x4{});
+        }
+        __builtin_amdgcn_wave_barrier();
+        continue;
+      }
+
+      // ---- tanh layer li (li == 0: the double tanh of layer 1): zbar from hbar
+      f32x4 zb[3][4];
+#pragma unroll
+      for (int R = 0; R < 4; ++R)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float d1, d2, d1c;
+          if (li == 0) {
+            const float pz = tanh_f(Z[0][R][r]), h = tanh_f(pz);
+            const float q = 1.0f - pz * pz, k1 = 1.0f - h * h;
+            d1 = k1 * q;
+            d2 = -2.0f * q * (h * d1 + pz * k1);
+            const float pc = tanh_f(Z[2][R][r]), hc = tanh_f(pc);
+            d1c = (1.0f - hc * hc) * (1.0f - pc * pc);
+          } else {
+            const float h = tanh_f(Z[0][R][r]);
+            d1 = 1.0f - h * h;
+            d2 = -2.0f * h * d1;
+            const float hc = tanh_f(Z[2][R][r]);
+            d1c = 1.0f - hc * hc;
+          }
+          zb[0][R][r] = d1 * hbar[0][R][r] + d2 * Z[1][R][r] * hbar[1][R][r];
+          zb[1][R][r] = d1 * hbar[1][R][r];
+          zb[2][R][r] = d1c * hbar[2][R][r];
+        }
+#pragma unroll
+      for (int S = 0; S < 3; ++S) put_t(S_(S), zb[S], g, c16);
+      if (li == 0) {
+        // layer-1 inputs transposed: rows 0..IN-1 = u, row IN = the bias column (1 for P and C)
+        if (g == 0) {
+          const float* us[3] = {uP, uV, uC};
+#pragma unroll
+          for (int S = 0; S < 3; ++S) {
+#pragma unroll
+            for (int k = 0; k < IN; ++k) S_(3 + S)[k * NS + c16] = (__bf16)us[S][k];
+            S_(3 + S)[IN * NS + c16] = (__bf16)(S == 1 ? 0.0f : 1.0f);
+          }
+        }
+      } else if (li >= 1) {
+#pragma unroll
+        for (int R = 0; R < 4; ++R) bbar[(li - 1) > 0 ? li - 1 : 0][R] += zb[0][R] + zb[2][R];
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
+      if (li == 0) {
+#pragma unroll
+        for (int T = 0; T < 2; ++T) {
+          f32x16 acc{};
+#pragma unroll
+          for (int S = 0; S < 3; ++S) {
+            const bf16x8 A = tread(S_(S), 32 * T + i32, true, hh);
+            const bf16x8 Bm = tread(S_(3 + S), i32, i32 <= IN, hh);
+            acc = mfma32(A, Bm, acc);
+          }
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = 32 * T + (r & 3) + 8 * (r >> 2) + 4 * hh;
+            if (i32 < IN) gacc[L::p_w(0) + row * IN + i32] += acc[r];
+            else if (i32 == IN) gacc[L::p_b(0) + row] += acc[r];
+          }
+        }
+      } else {
+        const int pw = L::p_w(li);
+#pragma unroll
+        for (int T = 0; T < 2; ++T)
+#pragma unroll
+          for (int U = 0; U < 2; ++U) {
+            f32x16 acc{};
+#pragma unroll
+            for (int S = 0; S < 3; ++S) {
+              const bf16x8 A = tread(S_(S), 32 * T + i32, true, hh);
+              const bf16x8 Bm = tread(S_(3 + S), 32 * U + i32, true, hh);
+              acc = mfma32(A, Bm, acc);
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int row = 32 * T + (r & 3) + 8 * (r >> 2) + 4 * hh;
+              gacc[pw + row * W + 32 * U + i32] += acc[r];
+            }
+          }
+        // h-bar of layer li-1 = W_li^T zbar
+        const char* wl = wtr + (li - 1) * 8192;
+#pragma unroll
+        for (int S = 0; S < 3; ++S) {
+          bf16x8 zbB[2];
+          pack_b(zb[S], zbB);
+#pragma unroll
+          for (int R = 0; R < 4; ++R) {
+            f32x4 acc = mfma16(frag(wl, 2 * R, lane), zbB[0], f32x4{});
+            hbar[S][R] = mfma16(frag(wl, 2 * R + 1, lane), zbB[1], acc);
+          }
+        }
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+
+  // ---- flush: bias partials (reduce the 16 sample lanes of each lane group) and loss sums
+#pragma unroll
+  for (int l = 0; l < NL - 1; ++l)
+#pragma unroll
+    for (int R = 0; R < 4; ++R)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = bbar[l][R][r];
+#pragma unroll
+        for (int m = 1; m < 16; m <<= 1) v += __shfl_xor(v, m, 64);
+        if (c16 == 0) gacc[L::p_b(l + 1) + 16 * R + 4 * g + r] += v;
+      }
+#pragma unroll
+  for (int o = 0; o < OUT; ++o) {
+    float v = g == 0 ? bobar[o] : 0.0f;
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) v += __shfl_xor(v, m, 64);
+    if (lane == 0) gacc[L::p_b(NL) + o] += v;
+  }
+  float* part = p.partials + ((size_t)blockIdx.x * NWV + w) * L::PART;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    float v = lsum[k];
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) v += __shfl_xor(v, m, 64);
+    if (lane == 0) part[L::NPARAM + k] = v;
+  }
+  if (lane == 0) part[L::NPARAM + 3] = 0.0f;
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+  for (int e = lane; e < L::NPARAM; e += 64) part[e] = gacc[e];
+}
+
+// grads[k] = sum over the partials in a fixed order (deterministic); loss_out = {loss, PDE, IC, DSM}
+__global__ void loss_grad_reduce_kernel(const float* partials, int n_parts, int stride, int nparam, float* grads,
+                                        float* loss_out, float inv_n, int has_dsm, int has_ic, int has_pde) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= nparam + 3) return;
+  double s = 0.0;
+  for (int i = 0; i < n_parts; ++i) s += (double)partials[(size_t)i * stride + k];
+  if (k < nparam) {
+    grads[k] = (float)s;
+    return;
+  }
+  // k - nparam: 0 DSM, 1 IC, 2 PDE sums
+  const float mean = (float)(s * inv_n);
+  const int c = k - nparam;
+  if (c == 0) loss_out[3] = mean;
+  if (c == 1) loss_out[2] = mean;
+  if (c == 2) loss_out[1] = mean;
+}
+
+__global__ void loss_total_kernel(float* loss_out, int has_dsm, int has_ic, int has_pde) {
+  loss_out[0] = (has_dsm ? loss_out[3] : 0.0f) + (has_ic ? loss_out[2] : 0.0f) + (has_pde ? loss_out[1] : 0.0f);
+}
+
+}  // namespace train
+
+int train_nparam(int n_hidden) {
+  return n_hidden == 3 ? train::TL<3>::NPARAM : (n_hidden == 2 ? train::TL<2>::NPARAM : -1);
+}
+
+hipError_t launch_loss_grad(const TrainParams& p, int n_hidden, float* grads, float* loss_out, float* partials,
+                            int n_wg, hipStream_t st) {
+  using namespace train;
+  const int part = n_hidden == 3 ? TL<3>::PART : TL<2>::PART;
+  const int nparam = train_nparam(n_hidden);
+  TrainParams q = p;
+  q.partials = partials;
+  if (n_hidden == 3)
+    hipLaunchKernelGGL(loss_grad_kernel<3>, dim3(n_wg), dim3(NWV * 64), 0, st, q);
+  else
+    hipLaunchKernelGGL(loss_grad_kernel<2>, dim3(n_wg), dim3(NWV * 64), 0, st, q);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(loss_grad_reduce_kernel, dim3((nparam + 3 + 255) / 256), dim3(256), 0, st, partials, n_wg * NWV,
+                     part, nparam, grads, loss_out, p.inv_n, p.has_dsm, p.has_ic, p.pde != 0);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(loss_total_kernel, dim3(1), dim3(1), 0, st, loss_out, p.has_dsm, p.has_ic, p.pde != 0);
+  return hipGetLastError();
+}
+
+int train_partial_stride(int n_hidden) { return n_hidden == 3 ? train::TL<3>::PART : train::TL<2>::PART; }
+int train_waves_per_wg() { return train::NWV; }
+
+}  // namespace dmip

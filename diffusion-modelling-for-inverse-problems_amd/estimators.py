@@ -27,6 +27,13 @@ from .nets import MLP, MLP2, PosteriorScore
 device = 'cuda' if torch.cuda.is_available() else 'cpu'
 
 
+class _FusedStep:
+    """A batch whose loss and parameter gradients came from the fused kernel (training.py)."""
+
+    def __init__(self, loss, info):
+        self.loss, self.info = loss, info
+
+
 def _draw_seed():
     return int(torch.randint(0, 2 ** 62, (1,)).item())
 
@@ -112,9 +119,13 @@ class BaseClassDiffusionModel:
         mean_loss = 0
         logger_info = {}
         for k, (x, y) in enumerate(epoch_data_loader()):
-            loss = self._accumulate(logger_info, k, batch_loss(x, y))
-            optimizer.zero_grad()
-            loss.backward()
+            out = batch_loss(x, y)
+            if isinstance(out, _FusedStep):  # gradients already written by the fused kernel
+                loss = self._accumulate(logger_info, k, (out.loss, out.info))
+            else:
+                loss = self._accumulate(logger_info, k, out)
+                optimizer.zero_grad()
+                loss.backward()
             optimizer.step()
             mean_loss = mean_loss * k / (k + 1) + loss / (k + 1)
         return mean_loss, logger_info
@@ -142,8 +153,16 @@ class CDE(BaseClassDiffusionModel):
         return out
 
     def train_epoch(self, optimizer, loss_fn, epoch_data_loader):
+        from .training import fused_config, fused_loss_grad
+        cfg = fused_config(self, loss_fn)
+
         def batch_loss(x, y):
             t = self.sample_t(x)
+            if cfg is not None:
+                # same draws as base_sde.sample (sdes.py:37-49): eps = randn_like(x)
+                eps = torch.randn_like(x)
+                optimizer.zero_grad()
+                return _FusedStep(*fused_loss_grad(self, loss_fn, cfg, x, y, t, eps))
             x_t, target, std, g = self.sde.base_sde.sample(t, x, return_noise=True)
             if loss_fn.name == 'DSMLoss':
                 return loss_fn(self.sde.a(x_t, y, t) / g, std, target).mean()

@@ -1,0 +1,91 @@
+"""Fused training step on the HIP device (libdmip dmip_loss_grad).
+
+`fused_loss_grad(model, loss_fn, x, y, t, eps)` computes the loss value, its components and the
+parameter gradients of DSMLoss / DSM_PDELoss / PINNLoss / PINNLoss2 (losses.py:42-290 with the
+ScoreFPE or conditional ScoreFPE residual) in one persistent kernel + one reduction, writing the
+gradients into the parameters' `.grad` (set, not accumulated). It is what CDE.train_epoch runs on a
+HIP device when `fused_config` accepts the network and loss; everything else (other networks, the
+Posterior loss, CPU tensors) takes the autograd path of losses.py.
+"""
+import os
+
+import torch
+
+from . import _lib
+from .losses import DSMLoss, DSM_PDELoss, PINNLoss, PINNLoss2, ScoreFPELoss
+from .problems import LinearForwardProblem
+
+
+def _metric(m):
+    return _lib.DMIP_METRIC_L1 if m == 'L1' else _lib.DMIP_METRIC_L2
+
+
+def fused_config(model, loss_fn):
+    """dmip_loss_cfg for (model, loss_fn), or None when the fused kernel does not cover them."""
+    if os.environ.get("DMIP_TRAIN_FUSED", "1") == "0":
+        return None
+    net = model.sde.a
+    if not hasattr(net, "linear_layers"):
+        return None
+    layers = net.linear_layers()
+    p0 = layers[0][0]
+    if not p0.is_cuda or p0.dtype != torch.float32:
+        return None
+    widths = [int(w.shape[0]) for w, _ in layers[:-1]]
+    if not _lib.loss_grad_supported(net.input_dim, net.output_dim, widths, model.xdim):
+        return None
+    if net.output_dim != model.xdim:  # CDE only (CDiffE trains on the joint z)
+        return None
+    cfg = _lib.DmipLossCfg()
+    if type(loss_fn) is DSMLoss:
+        cfg.kind, cfg.pde = _lib.DMIP_LOSS_DSM, _lib.DMIP_PDE_NONE
+        return cfg
+    kinds = {DSM_PDELoss: _lib.DMIP_LOSS_DSM_PDE, PINNLoss: _lib.DMIP_LOSS_PINN, PINNLoss2: _lib.DMIP_LOSS_PINN2}
+    if type(loss_fn) not in kinds:
+        return None
+    cfg.kind = kinds[type(loss_fn)]
+    cfg.pde = _lib.DMIP_PDE_FPE if isinstance(loss_fn.pde_loss, ScoreFPELoss) else _lib.DMIP_PDE_CFPE
+    cfg.pde_metric = _metric(loss_fn.pde_loss.metric)
+    cfg.lam = float(loss_fn.lam)
+    if cfg.kind in (_lib.DMIP_LOSS_PINN, _lib.DMIP_LOSS_PINN2):
+        prob = getattr(loss_fn.initial_condition, "__self__", None)
+        if not isinstance(prob, LinearForwardProblem) or \
+                getattr(loss_fn.initial_condition, "__func__", None) is not LinearForwardProblem.score_posterior:
+            return None  # the kernel's IC target is the linear problem's analytic posterior score
+        cfg.ic_metric = _metric(loss_fn.ic_metric)
+        cfg.lam2 = float(loss_fn.lam2)
+        cfg.ic_A[:] = [float(v) for v in prob.A.reshape(-1)]
+        cfg.ic_b[:] = [float(v) for v in prob.b.reshape(-1)]
+        cfg.ic_Sinv[:] = [float(v) for v in prob.Sigma_inv.reshape(-1)]
+    return cfg
+
+
+def fused_loss_grad(model, loss_fn, cfg, x, y, t, eps):
+    """One fused loss + gradient evaluation. Returns (loss, info) like the reference loss objects:
+    a 0-d tensor and {component name: 0-d tensor}."""
+    net = model.sde.a
+    layers = [(w.detach(), b.detach()) for w, b in net.linear_layers()]
+    dev = layers[0][0].device
+    f32 = dict(device=dev, dtype=torch.float32)
+    x = x.detach().to(**f32).contiguous()
+    y = y.detach().to(**f32).contiguous()
+    t = t.detach().to(**f32).reshape(-1).contiguous()
+    eps = eps.detach().to(**f32).contiguous()
+    params = list(net.parameters())
+    flat = torch.empty(sum(p.numel() for p in params), **f32)
+    out = torch.empty(4, **f32)
+    base = model.sde.base_sde
+    _lib.loss_grad(layers, net.input_dim, net.output_dim, model.xdim, _lib.vpsde(base.beta_min, base.beta_max, 1.0),
+                   cfg, x, y, t, eps, flat, out)
+    off = 0
+    for p in params:
+        p.grad = flat[off:off + p.numel()].view_as(p)
+        off += p.numel()
+    loss, pde, ic, dsm = out[0], out[1], out[2], out[3]
+    if cfg.kind == _lib.DMIP_LOSS_DSM:
+        return loss, {}
+    if cfg.kind == _lib.DMIP_LOSS_DSM_PDE:
+        return loss, {'PDE-Loss': pde, 'DSM-Loss': dsm}
+    if cfg.kind == _lib.DMIP_LOSS_PINN:
+        return loss, {'PDE-Loss': pde, 'Initial Condition': ic, 'DSM-Loss': dsm}
+    return loss, {'PDE-Loss': pde, 'Initial Condition': ic, 'DSM_eval': dsm}

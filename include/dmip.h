@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define DMIP_ABI_VERSION 2
+#define DMIP_ABI_VERSION 3
 
 typedef enum {
   DMIP_OK = 0,
@@ -111,6 +111,43 @@ int dmip_em_sample_posterior(const dmip_mlp* prior, const dmip_mlp* likelihood, 
 int dmip_em_sample_cdiffe(const dmip_mlp* net, const dmip_vpsde* sde, const float* y_dev, int n_y, int ydim, int xdim,
                           int64_t n_chains, int64_t chain_offset, int num_steps, float mean, float stdv, uint64_t seed,
                           int precision, float* x_out_dev, void* stream);
+
+/* ---- training: fused loss value + parameter gradients ----------------------------------------- */
+typedef enum { DMIP_LOSS_DSM = 0, DMIP_LOSS_DSM_PDE = 1, DMIP_LOSS_PINN = 2, DMIP_LOSS_PINN2 = 3 } dmip_loss_kind;
+typedef enum { DMIP_PDE_NONE = 0, DMIP_PDE_FPE = 1, DMIP_PDE_CFPE = 2 } dmip_pde_kind;
+typedef enum { DMIP_METRIC_L1 = 0, DMIP_METRIC_L2 = 1 } dmip_metric;
+
+/* Loss configuration, mirroring the reference loss objects (losses.py:126-290):
+ *   kind        DSMLoss (.mean() as CDE.train_epoch takes it), DSM_PDELoss, PINNLoss, PINNLoss2
+ *   pde         ScoreFPELoss (exact divergence) or ConditionalScoreFPELoss; NONE for DSM
+ *   pde_metric / ic_metric   L1 / L2;  lam, lam2 the PDE / initial-condition weights
+ *   ic_A, ic_b, ic_Sinv      initial-condition target of PINNLoss(2): the linear problem's analytic
+ *               posterior score -x + ((y - (A x + b)) Sinv^T) A (linear_problem.py:61-65), row-major 2x2 */
+typedef struct {
+  int kind, pde, pde_metric, ic_metric;
+  float lam, lam2;
+  float ic_A[4], ic_b[2], ic_Sinv[4];
+} dmip_loss_cfg;
+
+/* One training step's loss and gradients for the CDE score network, fused (forward jets, per-sample
+ * loss terms, hand-written reverse pass, deterministic batch reduction).
+ * Replaces: the loss_fn(...) call + loss.backward() inside CDE.train_epoch (models/diffusion.py:80-89)
+ * for DSMLoss / DSM_PDELoss / PINNLoss / PINNLoss2 (losses.py:42-290), with the forward diffusion
+ * x_t = eps std(t) + mean_weight(t) x done in the kernel (sdes.py:37-49).
+ *   weights_dev / biases_dev   device fp32 parameters of the n_hidden + 1 linear layers (the torch
+ *               parameters themselves, nn.Linear layout); read, not modified
+ *   x_dev [batch][xdim], y_dev [batch][ydim], t_dev [batch] (sample_t), eps_dev [batch][xdim]
+ *   grad_out_dev  [n_params] fp32, written (not accumulated) in the reference parameter order
+ *               (0.weight, 0.bias, 3.weight, 3.bias, ...)
+ *   loss_out_dev  [4] fp32: the loss, and the PDE / initial-condition / DSM component means
+ * Compiled for the linear problem's network: in_dim 5, out_dim 2, xdim 2, widths 64, n_hidden 2 or 3. */
+int dmip_loss_grad(int in_dim, int out_dim, int n_hidden, const int* widths, int xdim,
+                   const float* const* weights_dev, const float* const* biases_dev, const dmip_vpsde* sde,
+                   const dmip_loss_cfg* cfg, const float* x_dev, const float* y_dev, const float* t_dev,
+                   const float* eps_dev, int64_t batch, float* grad_out_dev, float* loss_out_dev, void* stream);
+
+/* Non-zero when dmip_loss_grad has a kernel for this network shape. */
+int dmip_loss_grad_supported(int in_dim, int out_dim, int n_hidden, const int* widths, int xdim);
 
 /* Test hooks for the parity suite (integer RNG stream, normals, schedule). */
 int dmip_rng_words(uint64_t seed, int64_t chain_offset, uint64_t stream_id, int64_t n_chains, int n_words,
