@@ -490,7 +490,7 @@ int dmip_loss_grad(int in_dim, int out_dim, int n_hidden, const int* widths, int
   const int64_t per_wg = dmip::train_waves_per_wg();
   int n_wg = (int)std::min<int64_t>((int64_t)n_cu, (tiles + per_wg - 1) / per_wg);
   if (n_wg < 1) n_wg = 1;
-  const size_t part_bytes = (size_t)n_wg * per_wg * dmip::train_partial_stride(n_hidden) * sizeof(float);
+  const size_t part_bytes = (size_t)n_wg * dmip::train_partial_stride(n_hidden) * sizeof(float);
   float* partials = nullptr;
   hipError_t e = hipMallocAsync((void**)&partials, part_bytes, st);
   if (e != hipSuccess) return fail(DMIP_ERR_ALLOC, std::string("hipMallocAsync: ") + hipGetErrorString(e));

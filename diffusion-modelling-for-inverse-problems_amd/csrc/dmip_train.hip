@@ -23,8 +23,8 @@
 // lane & 15), which repack into the next layer's B operand with no lane movement (k-permuted weight
 // fragments, as in the sampler). Weight-gradient products contract over samples and use
 // v_mfma_f32_32x32x16_bf16 (K = the tile's 16 samples). Each wave accumulates its gradient partial
-// in its own LDS region (deterministic), written out once; loss_grad_reduce_kernel sums the
-// partials in a fixed order.
+// in its own LDS region (deterministic); the two waves' regions are summed in wave order into one
+// partial per workgroup, and loss_grad_reduce_kernel sums the partials in a fixed order.
 #include "dmip_device.h"
 #include "dmip_internal.h"
 
@@ -66,7 +66,7 @@ struct TL {
   static constexpr int COL = BIAS + (NL + 1) * W * 4;    // fp32 [D][64]: layer-1 weight columns of x
   static constexpr int WAVE = COL + D * W * 4;
   static constexpr int GACC = 0;                         // per wave: fp32 gradient partial (param order)
-  static constexpr int SCR = ((NPARAM * 4 + 15) / 16) * 16;  // per wave: 6 transposed [64][16] bf16
+  static constexpr int SCR = ((PART * 4 + 15) / 16) * 16;    // per wave: 6 transposed [64][16] bf16
   static constexpr int WAVE_BYTES = SCR + 6 * W * NS * 2;
   static constexpr int TOTAL = WAVE + NWV * WAVE_BYTES;
   static_assert(TOTAL <= 160 * 1024, "LDS budget");
@@ -220,7 +220,7 @@ __global__ void __launch_bounds__(NWV * 64, 1) loss_grad_kernel(TrainParams p) {
     float* col = (float*)(lds + L::COL);
     for (int e = tid; e < D * W; e += NWV * 64) col[e] = p.w[0][(e % W) * IN + e / W];
     float* gacc = (float*)(lds + L::WAVE + w * L::WAVE_BYTES + L::GACC);
-    for (int e = lane; e < L::NPARAM; e += 64) gacc[e] = 0.0f;
+    for (int e = lane; e < L::PART; e += 64) gacc[e] = 0.0f;
   }
   __syncthreads();
 
@@ -672,37 +672,49 @@ __global__ void __launch_bounds__(NWV * 64, 1) loss_grad_kernel(TrainParams p) {
     for (int m = 1; m < 64; m <<= 1) v += __shfl_xor(v, m, 64);
     if (lane == 0) gacc[L::p_b(NL) + o] += v;
   }
-  float* part = p.partials + ((size_t)blockIdx.x * NWV + w) * L::PART;
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     float v = lsum[k];
 #pragma unroll
     for (int m = 1; m < 64; m <<= 1) v += __shfl_xor(v, m, 64);
-    if (lane == 0) part[L::NPARAM + k] = v;
+    if (lane == 0) gacc[L::NPARAM + k] = v;
   }
-  if (lane == 0) part[L::NPARAM + 3] = 0.0f;
-  __builtin_amdgcn_s_waitcnt(0xc07f);
-  __builtin_amdgcn_wave_barrier();
-  for (int e = lane; e < L::NPARAM; e += 64) part[e] = gacc[e];
+  // one partial per workgroup: wave 0's region + wave 1's region, in that order (deterministic)
+  __syncthreads();
+  float* part = p.partials + (size_t)blockIdx.x * L::PART;
+  const float* g0 = (const float*)(lds + L::WAVE + L::GACC);
+  for (int e = tid; e < L::PART; e += NWV * 64) {
+    float v = g0[e];
+#pragma unroll
+    for (int ww = 1; ww < NWV; ++ww) v += ((const float*)(lds + L::WAVE + ww * L::WAVE_BYTES + L::GACC))[e];
+    part[e] = v;
+  }
 }
 
-// grads[k] = sum over the partials in a fixed order (deterministic); loss_out = {loss, PDE, IC, DSM}
-__global__ void loss_grad_reduce_kernel(const float* partials, int n_parts, int stride, int nparam, float* grads,
-                                        float* loss_out, float inv_n, int has_dsm, int has_ic, int has_pde) {
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= nparam + 3) return;
+// grads[k] = sum over the per-workgroup partials in a fixed order (deterministic); slots nparam..+2
+// are the DSM / IC / PDE row sums -> loss_out = {loss, PDE, IC, DSM} means. 64 slots per block, the
+// partials split over 4 thread groups, combined in LDS in group order.
+__global__ void __launch_bounds__(256) loss_grad_reduce_kernel(const float* partials, int n_parts, int stride,
+                                                               int nparam, float* grads, float* loss_out, float inv_n) {
+  __shared__ double red[4][64];
+  const int pi = threadIdx.x & 63, pg = threadIdx.x >> 6;
+  const int k = blockIdx.x * 64 + pi;
   double s = 0.0;
-  for (int i = 0; i < n_parts; ++i) s += (double)partials[(size_t)i * stride + k];
+  if (k < nparam + 3) {
+#pragma unroll 8
+    for (int i = pg; i < n_parts; i += 4) s += (double)partials[(size_t)i * stride + k];
+  }
+  red[pg][pi] = s;
+  __syncthreads();
+  if (pg != 0 || k >= nparam + 3) return;
+  s = red[0][pi] + red[1][pi] + red[2][pi] + red[3][pi];
   if (k < nparam) {
     grads[k] = (float)s;
     return;
   }
-  // k - nparam: 0 DSM, 1 IC, 2 PDE sums
   const float mean = (float)(s * inv_n);
-  const int c = k - nparam;
-  if (c == 0) loss_out[3] = mean;
-  if (c == 1) loss_out[2] = mean;
-  if (c == 2) loss_out[1] = mean;
+  const int c = k - nparam;  // 0 DSM, 1 IC, 2 PDE
+  loss_out[3 - c] = mean;
 }
 
 __global__ void loss_total_kernel(float* loss_out, int has_dsm, int has_ic, int has_pde) {
@@ -728,8 +740,8 @@ hipError_t launch_loss_grad(const TrainParams& p, int n_hidden, float* grads, fl
     hipLaunchKernelGGL(loss_grad_kernel<2>, dim3(n_wg), dim3(NWV * 64), 0, st, q);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(loss_grad_reduce_kernel, dim3((nparam + 3 + 255) / 256), dim3(256), 0, st, partials, n_wg * NWV,
-                     part, nparam, grads, loss_out, p.inv_n, p.has_dsm, p.has_ic, p.pde != 0);
+  hipLaunchKernelGGL(loss_grad_reduce_kernel, dim3((nparam + 3 + 63) / 64), dim3(256), 0, st, partials, n_wg, part,
+                     nparam, grads, loss_out, p.inv_n);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(loss_total_kernel, dim3(1), dim3(1), 0, st, loss_out, p.has_dsm, p.has_ic, p.pde != 0);
