@@ -30,7 +30,7 @@ EXPORTED = (
     "dmip_mlp_create", "dmip_mlp_destroy", "dmip_mlp_forward", "dmip_em_sample", "dmip_rng_words",
     "dmip_rng_normals", "dmip_schedule", "dmip_last_error", "dmip_abi_version", "dmip_sampler_supported",
     "dmip_em_sample_stamps", "dmip_em_sample_posterior", "dmip_em_sample_cdiffe", "dmip_loss_grad",
-    "dmip_loss_grad_supported",
+    "dmip_loss_grad_supported", "dmip_histogram",
 )
 
 
@@ -70,10 +70,13 @@ def _declare(lib):
                                              _i32, _i32, _i64, _i64, _i32, _f32, _f32, _u64, _i32, _c_void_p,
                                              _c_void_p]
     lib.dmip_em_sample_cdiffe.argtypes = [_c_void_p, ctypes.POINTER(DmipVpsde), _c_void_p, _i32, _i32, _i32,
-                                          _i64, _i64, _i32, _f32, _f32, _u64, _i32, _c_void_p, _c_void_p]
+                                          _i64, _i64, _i32, _f32, _f32, _u64, _i32, _i32, _f32, _c_void_p,
+                                          _c_void_p]
     lib.dmip_loss_grad.argtypes = [_i32, _i32, _i32, ctypes.POINTER(_i32), _i32, ctypes.POINTER(_c_void_p),
                                    ctypes.POINTER(_c_void_p), ctypes.POINTER(DmipVpsde), ctypes.POINTER(DmipLossCfg),
                                    _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _c_void_p, _c_void_p,
+                                   _c_void_p]
+    lib.dmip_histogram.argtypes = [_c_void_p, _i64, _i32, _i32, ctypes.c_double, ctypes.c_double, _i32, _c_void_p,
                                    _c_void_p]
     lib.dmip_loss_grad_supported.argtypes = [_i32, _i32, _i32, ctypes.POINTER(_i32), _i32]
     lib.dmip_em_sample_stamps.argtypes = [_c_void_p, ctypes.POINTER(DmipVpsde), _c_void_p, _i32, _i32, _i32,
@@ -84,7 +87,7 @@ def _declare(lib):
     for name in ("dmip_mlp_create", "dmip_mlp_destroy", "dmip_mlp_forward", "dmip_em_sample",
                  "dmip_rng_words", "dmip_rng_normals", "dmip_schedule", "dmip_sampler_supported",
                  "dmip_em_sample_stamps", "dmip_em_sample_posterior", "dmip_em_sample_cdiffe",
-                 "dmip_loss_grad", "dmip_loss_grad_supported"):
+                 "dmip_loss_grad", "dmip_loss_grad_supported", "dmip_histogram"):
         getattr(lib, name).restype = _i32
 
 
@@ -186,13 +189,14 @@ def em_sample_posterior(prior, likelihood, sde, y, n_chains, chain_offset, num_s
                                          DMIP_PREC_BF16, ptr(out), stream_of(y.device)))
 
 
-def em_sample_cdiffe(handle, sde, y, n_chains, chain_offset, num_steps, mean, std, seed, out):
+def em_sample_cdiffe(handle, sde, y, n_chains, chain_offset, num_steps, mean, std, seed, out, corrector_steps=0,
+                     snr=0.16):
     calls["em_sample_cdiffe"] += 1
     n_y, ydim = y.shape
     check(lib().dmip_em_sample_cdiffe(handle.h, ctypes.byref(sde), ptr(y), n_y, ydim, handle.xdim,
                                       int(n_chains), int(chain_offset), int(num_steps), float(mean), float(std),
-                                      ctypes.c_uint64(int(seed) & 0xFFFFFFFFFFFFFFFF), DMIP_PREC_BF16, ptr(out),
-                                      stream_of(y.device)))
+                                      ctypes.c_uint64(int(seed) & 0xFFFFFFFFFFFFFFFF), DMIP_PREC_BF16,
+                                      int(corrector_steps), float(snr), ptr(out), stream_of(y.device)))
 
 
 def sampler_supported(width, n_hidden, xdim, ydim=0, mode=DMIP_SAMPLER_CDE):
@@ -213,4 +217,12 @@ def loss_grad(layers, in_dim, out_dim, xdim, sde, cfg, x, y, t, eps, grad_out, l
     bp = (_c_void_p * (L + 1))(*[b.data_ptr() for _, b in layers])
     check(lib().dmip_loss_grad(in_dim, out_dim, L, widths, xdim, wp, bp, ctypes.byref(sde), ctypes.byref(cfg),
                                ptr(x), ptr(y), ptr(t), ptr(eps), int(x.shape[0]), ptr(grad_out), ptr(loss_out),
+                               stream_of(x.device)))
+
+
+def histogram(x, nbins, lo, hi, counts):
+    """x: (n_hist, n, d) fp32 device tensor; counts: (n_hist, nbins**d) int32 device tensor (accumulated)."""
+    calls["histogram"] = calls.get("histogram", 0) + 1
+    n_hist, n, d = x.shape
+    check(lib().dmip_histogram(ptr(x), int(n), int(d), int(nbins), float(lo), float(hi), int(n_hist), ptr(counts),
                                stream_of(x.device)))

@@ -293,6 +293,8 @@ struct SampleArgs {
   float* x_out_dev;
   void* stream;
   uint64_t* stamps;
+  int n_corr = 0;
+  float snr = 0.16f;
 };
 
 // net0: the CDE / CDiffE network or the Posterior likelihood; net1: the Posterior prior (else null)
@@ -367,6 +369,8 @@ static int em_sample_impl(int mode, const dmip_mlp* net0, const dmip_mlp* net1, 
     p.bias_out2 = net1->bias_out_samp;
   }
   p.y_obs = a.y_dev;
+  p.n_corr = a.n_corr;
+  p.snr = a.snr;
   p.noise = a.noise_dev;
   p.x_out = a.x_out_dev;
   p.n_chains = a.n_chains;
@@ -409,9 +413,13 @@ int dmip_em_sample_posterior(const dmip_mlp* prior, const dmip_mlp* likelihood, 
 
 int dmip_em_sample_cdiffe(const dmip_mlp* net, const dmip_vpsde* sde, const float* y_dev, int n_y, int ydim, int xdim,
                           int64_t n_chains, int64_t chain_offset, int num_steps, float mean, float stdv, uint64_t seed,
-                          int precision, float* x_out_dev, void* stream) {
-  const SampleArgs a{sde,  y_dev, n_y,       ydim,      xdim,    n_chains, chain_offset, num_steps,
-                     mean, stdv,  seed,      precision, nullptr, x_out_dev, stream,      nullptr};
+                          int precision, int corrector_steps, float snr, float* x_out_dev, void* stream) {
+  if (corrector_steps < 0) return fail(DMIP_ERR_INVALID, "corrector_steps must be >= 0");
+  if (corrector_steps > 0 && !(snr > 0.0f)) return fail(DMIP_ERR_INVALID, "snr must be > 0");
+  SampleArgs a{sde,  y_dev, n_y,       ydim,      xdim,    n_chains, chain_offset, num_steps,
+               mean, stdv,  seed,      precision, nullptr, x_out_dev, stream,      nullptr};
+  a.n_corr = corrector_steps;
+  a.snr = snr;
   return em_sample_impl(DMIP_SAMPLER_CDIFFE, net, nullptr, a);
 }
 
@@ -498,6 +506,17 @@ int dmip_loss_grad(int in_dim, int out_dim, int n_hidden, const int* widths, int
   (void)hipFreeAsync(partials, st);
   if (e != hipSuccess) return hip_fail(e, "loss_grad launch");
   return DMIP_OK;
+}
+
+int dmip_histogram(const float* x_dev, int64_t n, int d, int nbins, double lo, double hi, int n_hist,
+                   uint32_t* counts_dev, void* stream) {
+  if (!x_dev || !counts_dev) return fail(DMIP_ERR_INVALID, "null argument");
+  if (d < 1 || d > 3 || nbins < 1 || nbins > 4096 || n < 0 || n_hist < 1 || n_hist > 65535 || !(hi > lo))
+    return fail(DMIP_ERR_INVALID, "bad histogram shape or range");
+  if (n == 0) return DMIP_OK;
+  hipError_t e = dmip::launch_histogram(x_dev, n, d, nbins, lo, hi, n_hist, (unsigned int*)counts_dev,
+                                        (hipStream_t)stream);
+  return e == hipSuccess ? DMIP_OK : hip_fail(e, "histogram launch");
 }
 
 int dmip_rng_words(uint64_t seed, int64_t chain_offset, uint64_t stream_id, int64_t n_chains, int n_words,

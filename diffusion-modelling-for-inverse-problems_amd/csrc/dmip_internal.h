@@ -23,6 +23,8 @@ struct SamplerParams {
   const float* bias_hidden2;
   const float* bias_out2;
   const float* y_obs;         // CDiffE: observations [n_y][ydim] (re-diffused every step)
+  int n_corr;                 // CDiffE: Langevin corrector steps per time step (0 = plain EM)
+  float snr;                  // CDiffE: corrector signal-to-noise ratio
   const float* noise;         // injected normals [S+1][n_y][n_chains][D] (slot 0 -> x0) or null
   float* x_out;               // [n_y][n_chains][D]
   long long n_chains;         // chains per y
@@ -80,6 +82,9 @@ int train_partial_stride(int n_hidden);
 int train_waves_per_wg();
 hipError_t launch_loss_grad(const TrainParams& p, int n_hidden, float* grads, float* loss_out, float* partials,
                             int n_wg, hipStream_t st);
+
+hipError_t launch_histogram(const float* x, long long n, int d, int nbins, double lo, double hi, int n_hist,
+                            unsigned int* counts, hipStream_t st);
 
 hipError_t launch_sampler(const SamplerParams& p, int mode, int width, int n_hidden, int xdim, int ydim, int n_y,
                           hipStream_t st, bool* supported);

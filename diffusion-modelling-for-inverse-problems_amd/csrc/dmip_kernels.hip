@@ -277,6 +277,23 @@ __device__ __forceinline__ void build_b1(const float (&v)[NV], int h, bf16x8 (&B
   }
 }
 
+// rewrite the x slots (inputs 0..D-1) of a build_b1 operand after x changed
+template <int NV, int D, int K1S>
+__device__ __forceinline__ void patch_b1_x(const float (&x)[D], int h, bf16x8 (&B1)[K1S]) {
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    const __bf16 hi = (__bf16)x[k];
+    const __bf16 lo = (__bf16)(x[k] - (float)hi);
+    const int slots[3] = {k, NV + k, 2 * NV + k};
+    const __bf16 vals[3] = {hi, lo, hi};
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int sl = slots[q];
+      if (h == ((sl >> 3) & 1)) B1[sl >> 4][sl & 7] = vals[q];
+    }
+  }
+}
+
 // ------------------------------------------------------------------------- sampler kernel
 __device__ __forceinline__ unsigned long long stamp() {
   unsigned long long t;
@@ -383,6 +400,31 @@ em_sampler_kernel(SamplerParams p) {
     bf16x8 B1[K1S];
     build_b1<NV, K1S>(v, h, B1);
     if constexpr (MODE != MODE_CDE) __builtin_amdgcn_sched_barrier(0);
+    if constexpr (MODE == MODE_CDIFFE) {
+      // Langevin corrector steps at this time, before the predictor (Song et al. 2021 PC sampling,
+      // per-chain step size): s = a/g, eps = 2 alpha (snr |z| / |s|)^2, x <- x + eps s + sqrt(2 eps) z,
+      // alpha = exp(-beta delta) (the discrete VP alpha 1 - beta delta of score_sde, kept positive
+      // for coarse step counts). y_t is held fixed; only x's slots of the layer-1 operand change.
+      for (int c = 0; c < p.n_corr; ++c) {
+        const f32x16 oc = eng.eval(B1);
+        float z[D], sc[D];
+        rng_normals<D>(rng, z);
+        float zn = 0.0f, sn = 0.0f;
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+          sc[k] = oc[k] / cf.g;
+          zn += z[k] * z[k];
+          sn += sc[k] * sc[k];
+        }
+        const float alpha = __expf(-cf.beta * p.delta);
+        const float r = p.snr * p.snr * zn / fmaxf(sn, 1e-30f);
+        const float es = 2.0f * alpha * r;
+        const float ns = __fsqrt_rn(2.0f * es);
+#pragma unroll
+        for (int k = 0; k < D; ++k) x[k] = x[k] + es * sc[k] + ns * z[k];
+        patch_b1_x<NV, D, K1S>(x, h, B1);
+      }
+    }
     if constexpr (STAMP) t1 = stamp();
     f32x16 out = eng.eval(B1);
     if constexpr (STAMP) t2 = stamp();

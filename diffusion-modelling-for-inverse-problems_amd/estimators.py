@@ -215,8 +215,17 @@ class CDiffE(BaseClassDiffusionModel):
         score_net = MLP(xdim + ydim + 1, xdim + ydim, hidden_layers, nn.Tanh()).to(device)
         self.sde = sdes.PluginReverseSDE(sdes.VariancePreservingSDE(), score_net, T=1, debias=True)
 
+    def forward(self, y, num_samples=2000, num_steps=200, mean=0, std=1, corrector_steps=0, snr=0.16):
+        """As BaseClassDiffusionModel.forward; `corrector_steps` > 0 adds Langevin corrector steps
+        before every predictor step (predictor-corrector sampling, BASELINE config 3; see
+        dmip_em_sample_cdiffe in include/dmip.h for the definition)."""
+        from . import parallel
+        x = parallel.sample_sharded(self, y, num_samples, num_steps, mean, std,
+                                    corrector_steps=corrector_steps, snr=snr)
+        return x.cpu().numpy()
+
     def sample_device(self, y, num_samples, num_steps=200, mean=0, std=1, seed=None, chain_offset=0,
-                      noise=None):
+                      noise=None, corrector_steps=0, snr=0.16):
         if noise is not None:
             raise ValueError("noise injection is only implemented for the fused CDE sampler")
         net = self.sde.a
@@ -224,8 +233,11 @@ class CDiffE(BaseClassDiffusionModel):
         seed = _draw_seed() if seed is None else seed
         handle = net.dmip_handle(dev, self.xdim)
         if _lib.sampler_supported(handle.width, handle.n_hidden, self.xdim, self.ydim, _lib.DMIP_SAMPLER_CDIFFE):
-            _lib.em_sample_cdiffe(handle, sde, ys, num_samples, chain_offset, num_steps, mean, std, seed, out)
+            _lib.em_sample_cdiffe(handle, sde, ys, num_samples, chain_offset, num_steps, mean, std, seed, out,
+                                  corrector_steps, snr)
             return out
+        if corrector_steps:
+            raise ValueError("the predictor-corrector sampler needs a compiled fused CDiffE kernel for this shape")
         base = self.sde.base_sde
         xd = self.xdim
 

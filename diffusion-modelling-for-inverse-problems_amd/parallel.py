@@ -56,13 +56,14 @@ def gather_shards(local, n, device):
     return torch.cat(parts, dim=1).to(device)
 
 
-def sample_sharded(model, y, num_samples, num_steps, mean, std, seed=None):
-    """model(y, ...) over all ranks; returns the full (num_samples, xdim) device tensor."""
+def sample_sharded(model, y, num_samples, num_steps, mean, std, seed=None, **sampler_kwargs):
+    """model(y, ...) over all ranks; returns the full (num_samples, xdim) device tensor.
+    `sampler_kwargs` go to model.sample_device (e.g. CDiffE's corrector_steps / snr)."""
     from .estimators import _draw_seed
     rank, ws = world()
     dev = model._exec_device(y)
     seed = common_seed(_draw_seed() if seed is None else seed, dev)
     lo, hi = shard_range(num_samples, rank, ws)
-    local = model.sample_device(y, hi - lo, num_steps, mean, std, seed=seed, chain_offset=lo)
+    local = model.sample_device(y, hi - lo, num_steps, mean, std, seed=seed, chain_offset=lo, **sampler_kwargs)
     full = gather_shards(local, num_samples, dev)
     return full[0] if torch.as_tensor(y).ndim == 1 else full

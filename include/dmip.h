@@ -107,10 +107,15 @@ int dmip_em_sample_posterior(const dmip_mlp* prior, const dmip_mlp* likelihood, 
  * step re-diffuses the observation, y_t = eps std(T-t) + mean_weight(T-t) y (sdes.py:37-44), evaluates
  * the joint score a(x, y_t, T-t) (out_dim = xdim + ydim) and takes the EM step on the x part.
  *   net   MLP handle (DMIP_INPUT_X_Y_T, in_dim = xdim + ydim + 1, out_dim = xdim + ydim)
+ *   corrector_steps, snr   predictor-corrector sampling (BASELINE config 3; no reference code): before
+ *         each predictor step, corrector_steps Langevin steps at the same time and y_t (Song et al.
+ *         2021, per-chain step size): s = a/g on the x rows, eps = 2 alpha (snr |z| / |s|)^2,
+ *         x <- x + eps s + sqrt(2 eps) z, alpha = exp(-beta(T-t) delta) (score_sde's discrete VP
+ *         alpha 1 - beta delta to first order, positive at any step count). 0 = plain EM.
  * Other arguments as dmip_em_sample (no injection). */
 int dmip_em_sample_cdiffe(const dmip_mlp* net, const dmip_vpsde* sde, const float* y_dev, int n_y, int ydim, int xdim,
                           int64_t n_chains, int64_t chain_offset, int num_steps, float mean, float stdv, uint64_t seed,
-                          int precision, float* x_out_dev, void* stream);
+                          int precision, int corrector_steps, float snr, float* x_out_dev, void* stream);
 
 /* ---- training: fused loss value + parameter gradients ----------------------------------------- */
 typedef enum { DMIP_LOSS_DSM = 0, DMIP_LOSS_DSM_PDE = 1, DMIP_LOSS_PINN = 2, DMIP_LOSS_PINN2 = 3 } dmip_loss_kind;
@@ -148,6 +153,16 @@ int dmip_loss_grad(int in_dim, int out_dim, int n_hidden, const int* widths, int
 
 /* Non-zero when dmip_loss_grad has a kernel for this network shape. */
 int dmip_loss_grad_supported(int in_dim, int out_dim, int n_hidden, const int* widths, int xdim);
+
+/* ---- evaluation ------------------------------------------------------------------------------ */
+/* counts[h][b0][b1]...[b_{d-1}] += number of points of x[h] in that bin, binned exactly like
+ * numpy.histogramdd(x[h], bins=(nbins,)*d, range=[(lo, hi)]*d) (float64 edges, right edge closed,
+ * outside points dropped). Replaces: the np.histogramdd calls of the evaluate drivers
+ * (main_diffusion_scatterometry.py:71-74).
+ *   x_dev      [n_hist][n][d] fp32;  d in 1..3
+ *   counts_dev [n_hist][nbins^d] uint32, accumulated (zero it first) */
+int dmip_histogram(const float* x_dev, int64_t n, int d, int nbins, double lo, double hi, int n_hist,
+                   uint32_t* counts_dev, void* stream);
 
 /* Test hooks for the parity suite (integer RNG stream, normals, schedule). */
 int dmip_rng_words(uint64_t seed, int64_t chain_offset, uint64_t stream_id, int64_t n_chains, int n_words,

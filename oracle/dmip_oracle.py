@@ -285,7 +285,7 @@ def posterior_sample(prior_params, lik_params, y, num_samples, num_steps, seed, 
 
 
 def cdiffe_sample(params, y, num_samples, num_steps, seed, mean=0.0, std=1.0, chain_offset=0, stream=0,
-                  T=1.0, beta_min=BETA_MIN, beta_max=BETA_MAX):
+                  T=1.0, beta_min=BETA_MIN, beta_max=BETA_MAX, corrector_steps=0, snr=0.16):
     """Product-RNG CDiffE sampler, repaired semantics of models/diffusion.py:158-180 (the reference
     loop raises TypeError at :174): per step y_t = eps std(T-t) + mean_weight(T-t) y
     (sdes.py:37-44, eps = ydim fresh normals), a = net(x, y_t, T-t)[:, :xdim], then the EM update of
@@ -302,6 +302,18 @@ def cdiffe_sample(params, y, num_samples, num_steps, seed, mean=0.0, std=1.0, ch
         sd = np.sqrt(vp_var(tau[i], beta_min, beta_max)).astype(F32)
         eps = rng_normals(st, ydim)
         y_t = ((eps * sd).astype(F32) + (mw * y).astype(F32)).astype(F32)
+        beta = vp_beta(tau[i], beta_min, beta_max)
+        g = np.sqrt(beta).astype(F32)
+        for _ in range(corrector_steps):
+            # Langevin corrector (the build's definition, include/dmip.h dmip_em_sample_cdiffe; no
+            # reference code): per-chain step 2 alpha (snr |z| / |s|)^2, alpha = exp(-beta delta)
+            sc = (cde_a(params, x, y_t, tau[i])[:, :xdim] / g).astype(F32)
+            z = rng_normals(st, xdim)
+            zn = np.sum(z * z, axis=1, keepdims=True)
+            sn = np.maximum(np.sum(sc * sc, axis=1, keepdims=True), F32(1e-30))
+            alpha = np.exp(-beta * F32(delta)).astype(F32)
+            es = (F32(2.0) * alpha * (F32(snr) * F32(snr) * zn / sn)).astype(F32)
+            x = (x + es * sc + np.sqrt(F32(2.0) * es) * z).astype(F32)
         a = cde_a(params, x, y_t, tau[i])[:, :xdim]
         xi = rng_normals(st, xdim)
         x = em_step(x, a, tau[i], delta, beta_min, beta_max, xi)

@@ -74,7 +74,8 @@ def test_sampler_rejects_null_handle(lib, dmip):
     rc = lib.dmip_em_sample_posterior(None, None, ctypes.byref(sde), None, 1, 2, 2, 10, 0, 10, 0.0, 1.0, 1, 0,
                                       None, None)
     assert rc == L.DMIP_ERR_INVALID
-    rc = lib.dmip_em_sample_cdiffe(None, ctypes.byref(sde), None, 1, 2, 2, 10, 0, 10, 0.0, 1.0, 1, 0, None, None)
+    rc = lib.dmip_em_sample_cdiffe(None, ctypes.byref(sde), None, 1, 2, 2, 10, 0, 10, 0.0, 1.0, 1, 0, 0, 0.16, None,
+                                   None)
     assert rc == L.DMIP_ERR_INVALID
     rc = lib.dmip_schedule(0, ctypes.byref(sde), None, None)
     assert rc == L.DMIP_ERR_INVALID
