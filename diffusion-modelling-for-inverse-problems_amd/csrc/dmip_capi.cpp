@@ -6,9 +6,10 @@
 //     v_mfma_f32_32x32x16_bf16: lane l = i + 32h holds A[row i][k = 8h + j], j = 0..7.
 //   * Hidden layer k-order: the B operand is the previous layer's accumulator registers, so
 //     element j of lane half h in k-step s is hidden unit kperm(s, h, j) (see below).
-//   * r-form activations: kernels carry r = 1/(1+exp(2z)) = (1 - tanh z)/2, so the next layer
-//     uses weights -2W and bias b + sum_k W; pre-activations of tanh layers are scaled by
-//     c = 2 log2(e) (exp2 instead of exp).
+//   * r-form activations: kernels carry r = 1/(1+exp(2z)) = (1 - tanh z)/2 after a single tanh,
+//     so the next layer uses weights -2W and bias b + sum_k W; after layer 1's double tanh they
+//     carry the value itself (t-form: weights W, bias b). Pre-activations of tanh layers are
+//     scaled by c = 2 log2(e) (exp2 instead of exp).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -128,22 +129,25 @@ int dmip_mlp_create(int in_dim, int out_dim, int n_hidden, const int* widths, in
   net->xdim = xdim;
   const int T = W / 32, KS = W / 16, L = n_hidden;
 
-  // ---- hidden W x W layers: A = bf16(-2c W), init = c b - 0.5 sum_k A
+  // ---- hidden W x W layers. Input in r-form (after a single tanh): A = bf16(-2c W),
+  // init = c b - 0.5 sum_k A. Input in t-form (the first W x W layer: layer 1's double tanh is
+  // emitted as the value itself, dmip_device.h act_t_twice): A = bf16(c W), init = c b.
   std::vector<uint16_t> hid((size_t)(L - 1) * T * KS * 512);
   std::vector<float> bh((size_t)(L - 1) * T * 32);
   for (int li = 0; li < L - 1; ++li) {
     const float* Wl = weights[li + 1];
     const float* bl = biases[li + 1];
+    const bool t_form = li == 0;
     std::vector<uint16_t> A((size_t)W * W);
     std::vector<float> init(W);
     for (int r = 0; r < W; ++r) {
       double acc = 0.0;
       for (int k = 0; k < W; ++k) {
-        const uint16_t a = f2bf((float)(-2.0 * kC * (double)Wl[(size_t)r * W + k]));
+        const uint16_t a = f2bf((float)((t_form ? 1.0 : -2.0) * kC * (double)Wl[(size_t)r * W + k]));
         A[(size_t)r * W + k] = a;
         acc += (double)bf2f(a);
       }
-      init[r] = (float)(kC * (double)bl[r] - 0.5 * acc);
+      init[r] = (float)(kC * (double)bl[r] - (t_form ? 0.0 : 0.5 * acc));
     }
     for (int rt = 0; rt < T; ++rt)
       for (int s = 0; s < KS; ++s)
@@ -157,19 +161,21 @@ int dmip_mlp_create(int in_dim, int out_dim, int n_hidden, const int* widths, in
         for (int r = 0; r < 16; ++r) bh[((size_t)(li * T + rt) * 2 + h) * 16 + r] = init[rt * 32 + acc_row(r, h)];
   }
 
-  // ---- output layer: A = bf16(-2 W), init = b - 0.5 sum_k A (no tanh scale: raw drift a)
+  // ---- output layer: A = bf16(-2 W), init = b - 0.5 sum_k A (no tanh scale: raw drift a);
+  // t-form input (L == 1: directly after layer 1's double tanh): A = bf16(W), init = b
   const float* Wo = weights[L];
   const float* bo = biases[L];
+  const bool out_t_form = L == 1;
   std::vector<uint16_t> Ao((size_t)out_dim * W);
   std::vector<float> init_o(out_dim);
   for (int d = 0; d < out_dim; ++d) {
     double acc = 0.0;
     for (int k = 0; k < W; ++k) {
-      const uint16_t a = f2bf((float)(-2.0 * (double)Wo[(size_t)d * W + k]));
+      const uint16_t a = f2bf((float)((out_t_form ? 1.0 : -2.0) * (double)Wo[(size_t)d * W + k]));
       Ao[(size_t)d * W + k] = a;
       acc += (double)bf2f(a);
     }
-    init_o[d] = (float)((double)bo[d] - 0.5 * acc);
+    init_o[d] = (float)((double)bo[d] - (out_t_form ? 0.0 : 0.5 * acc));
   }
   std::vector<uint16_t> ao_s((size_t)KS * 512, 0), ao_f((size_t)KS * 512, 0);
   std::vector<float> bo_s(32, 0.0f), bo_f(32, 0.0f);

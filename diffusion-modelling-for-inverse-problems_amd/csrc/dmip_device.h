@@ -144,25 +144,27 @@ __device__ __forceinline__ float em_update(float x, float a, float xi, const Ste
 __device__ __forceinline__ float act_r(float zs) {
   return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(zs));
 }
-// tanh(tanh(z)) of the reference's first layer (nets.py:21-26 double Tanh) in r-form:
-// q = r(z), tanh(z) = 1 - 2q, r1 = r(c (1 - 2q)) = 1 / (1 + 2^c 2^(-2cq)). The scale -2c is folded
-// into the first reciprocal (q' = 1 / fma(e, k, k) = -2c q with k = -1/(2c)) and 2^c into the second
-// denominator (fma(2^q', 2^c, 1)), so the two stages cost exp, fma, rcp, exp, fma, rcp.
-// (An odd polynomial for the bounded outer tanh costs as much VALU issue as exp + rcp on gfx950.)
-__device__ __forceinline__ float act_r_twice(float zs) {
-  constexpr float k = -1.0f / (2.0f * kTanhScale);
-  constexpr float two_c = 7.389056098930650f;  // 2^c = e^2
-  const float e = __builtin_amdgcn_exp2f(zs);
-  const float qs = __builtin_amdgcn_rcpf(__builtin_fmaf(e, k, k));
-  return __builtin_amdgcn_rcpf(__builtin_fmaf(__builtin_amdgcn_exp2f(qs), two_c, 1.0f));
+// tanh(tanh(z)) of the reference's first layer (nets.py:21-26 double Tanh), returned in t-form
+// (the value itself; the host packs the next layer for a t-form input). With e = exp(-2|z|) in
+// (0, 1], tanh|z| = (1 - e)/(1 + e) and tanh(tanh|z|) = (1 - e) q(e), q a degree-4 fit (max abs
+// error 1.7e-5 in f32 Horner, exact 0 at z = 0; bf16 rounding of the result is ~100x larger).
+// One transcendental + 5 FMAs + copysign: 32 issue cycles per unit against 40 for the two
+// exp + rcp stages (exp, fma, rcp, exp, fma, rcp) it replaces.
+__device__ __forceinline__ float act_t_twice(float zs) {
+  const float e = __builtin_amdgcn_exp2f(-__builtin_fabsf(zs));
+  float q = __builtin_fmaf(-0.17045435309410095f, e, 0.5245547890663147f);
+  q = __builtin_fmaf(q, e, -0.5390751957893372f);
+  q = __builtin_fmaf(q, e, -0.07747964560985565f);
+  q = __builtin_fmaf(q, e, 0.761600136756897f);
+  return __builtin_copysignf(__builtin_fmaf(-e, q, q), zs);
 }
 
 template <bool TWICE, bool CAST_ONLY = false>
 __device__ __forceinline__ void act_pack(const f32x16& acc, bf16x8& lo, bf16x8& hi) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const float a = CAST_ONLY ? acc[j] : (TWICE ? act_r_twice(acc[j]) : act_r(acc[j]));
-    const float b = CAST_ONLY ? acc[8 + j] : (TWICE ? act_r_twice(acc[8 + j]) : act_r(acc[8 + j]));
+    const float a = CAST_ONLY ? acc[j] : (TWICE ? act_t_twice(acc[j]) : act_r(acc[j]));
+    const float b = CAST_ONLY ? acc[8 + j] : (TWICE ? act_t_twice(acc[8 + j]) : act_r(acc[8 + j]));
     lo[j] = (__bf16)a;
     hi[j] = (__bf16)b;
   }
