@@ -4,7 +4,7 @@ CSRC := $(PKG)/csrc
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-parameter
-OBJS := $(CSRC)/dmip_kernels.o $(CSRC)/dmip_train.o $(CSRC)/dmip_eval.o $(CSRC)/dmip_capi.o
+OBJS := $(CSRC)/dmip_kernels.o $(CSRC)/dmip_train.o $(CSRC)/dmip_eval.o $(CSRC)/dmip_surrogate.o $(CSRC)/dmip_capi.o
 HDRS := $(CSRC)/dmip_device.h $(CSRC)/dmip_internal.h include/dmip.h
 
 all: $(PKG)/libdmip.so
@@ -16,6 +16,9 @@ $(CSRC)/dmip_train.o: $(CSRC)/dmip_train.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(CSRC)/dmip_eval.o: $(CSRC)/dmip_eval.hip $(HDRS)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(CSRC)/dmip_surrogate.o: $(CSRC)/dmip_surrogate.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(CSRC)/dmip_capi.o: $(CSRC)/dmip_capi.cpp $(HDRS)

@@ -13,7 +13,8 @@ from .factory import get_model_from_args
 from .losses import (ConditionalScoreFPELoss, DSM_PDELoss, DSMLoss, PINNLoss, PINNLoss2, PosteriorLoss,
                      ScoreFPELoss, batch_gradient, divergence)
 from .nets import MLP, MLP2, PosteriorScore
-from .problems import LinearForwardProblem
+from .problems import (LinearForwardProblem, ScatterometryEnergy, anneal_to_energy, energy_grad,
+                       generate_gt_samples, get_log_posterior, load_forward_model, mh_sample)
 from .sdes import PluginReverseSDE, VariancePreservingSDE, sample_vp_truncated_q
 
 __all__ = [
@@ -21,6 +22,8 @@ __all__ = [
     "ConditionalScoreFPELoss", "DSM_PDELoss", "DSMLoss", "PINNLoss", "PINNLoss2", "PosteriorLoss",
     "ScoreFPELoss", "batch_gradient", "divergence", "MLP", "MLP2", "PosteriorScore",
     "PluginReverseSDE", "VariancePreservingSDE", "sample_vp_truncated_q", "LinearForwardProblem",
+    "ScatterometryEnergy", "anneal_to_energy", "energy_grad", "generate_gt_samples", "get_log_posterior",
+    "load_forward_model", "mh_sample",
 ]
 
 

@@ -20,7 +20,7 @@ DMIP_INPUT_X_Y_T, DMIP_INPUT_X_T = 0, 1
 DMIP_ACT_TANH_TWICE_FIRST, DMIP_ACT_TANH = 0, 1
 DMIP_PREC_BF16 = 0
 DMIP_SAMPLER_CDE, DMIP_SAMPLER_POSTERIOR, DMIP_SAMPLER_CDIFFE = 0, 1, 2
-ABI_VERSION = 3
+ABI_VERSION = 4
 DMIP_LOSS_DSM, DMIP_LOSS_DSM_PDE, DMIP_LOSS_PINN, DMIP_LOSS_PINN2 = 0, 1, 2, 3
 DMIP_PDE_NONE, DMIP_PDE_FPE, DMIP_PDE_CFPE = 0, 1, 2
 DMIP_METRIC_L1, DMIP_METRIC_L2 = 0, 1
@@ -30,7 +30,8 @@ EXPORTED = (
     "dmip_mlp_create", "dmip_mlp_destroy", "dmip_mlp_forward", "dmip_em_sample", "dmip_rng_words",
     "dmip_rng_normals", "dmip_schedule", "dmip_last_error", "dmip_abi_version", "dmip_sampler_supported",
     "dmip_em_sample_stamps", "dmip_em_sample_posterior", "dmip_em_sample_cdiffe", "dmip_loss_grad",
-    "dmip_loss_grad_supported", "dmip_histogram",
+    "dmip_loss_grad_supported", "dmip_histogram", "dmip_surrogate_create", "dmip_surrogate_destroy",
+    "dmip_surrogate_forward", "dmip_log_posterior", "dmip_mh_sample",
 )
 
 
@@ -42,6 +43,10 @@ class DmipLossCfg(ctypes.Structure):
     _fields_ = [("kind", ctypes.c_int), ("pde", ctypes.c_int), ("pde_metric", ctypes.c_int),
                 ("ic_metric", ctypes.c_int), ("lam", ctypes.c_float), ("lam2", ctypes.c_float),
                 ("ic_A", ctypes.c_float * 4), ("ic_b", ctypes.c_float * 2), ("ic_Sinv", ctypes.c_float * 4)]
+
+
+class DmipScatNoise(ctypes.Structure):
+    _fields_ = [("a", ctypes.c_float), ("b", ctypes.c_float), ("lambd_bd", ctypes.c_float)]
 
 
 _c_void_p = ctypes.c_void_p
@@ -84,10 +89,19 @@ def _declare(lib):
     lib.dmip_rng_words.argtypes = [_u64, _i64, _u64, _i64, _i32, _c_void_p, _c_void_p]
     lib.dmip_rng_normals.argtypes = [_u64, _i64, _u64, _i64, _i32, _c_void_p, _c_void_p]
     lib.dmip_schedule.argtypes = [_i32, ctypes.POINTER(DmipVpsde), _c_void_p, _c_void_p]
+    lib.dmip_surrogate_create.argtypes = [_i32, _i32, _i32, ctypes.POINTER(_i32), ctypes.POINTER(_c_void_p),
+                                          ctypes.POINTER(_c_void_p), ctypes.POINTER(_c_void_p)]
+    lib.dmip_surrogate_destroy.argtypes = [_c_void_p]
+    lib.dmip_surrogate_forward.argtypes = [_c_void_p, _c_void_p, _i64, _c_void_p, _c_void_p]
+    lib.dmip_log_posterior.argtypes = [_c_void_p, ctypes.POINTER(DmipScatNoise), _c_void_p, _c_void_p, _i64, _i64,
+                                       _c_void_p, _c_void_p, _c_void_p]
+    lib.dmip_mh_sample.argtypes = [_c_void_p, ctypes.POINTER(DmipScatNoise), _c_void_p, _i32, _i64, _i64, _i32, _f32,
+                                   _u64, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p]
     for name in ("dmip_mlp_create", "dmip_mlp_destroy", "dmip_mlp_forward", "dmip_em_sample",
                  "dmip_rng_words", "dmip_rng_normals", "dmip_schedule", "dmip_sampler_supported",
                  "dmip_em_sample_stamps", "dmip_em_sample_posterior", "dmip_em_sample_cdiffe",
-                 "dmip_loss_grad", "dmip_loss_grad_supported", "dmip_histogram"):
+                 "dmip_loss_grad", "dmip_loss_grad_supported", "dmip_histogram", "dmip_surrogate_create",
+                 "dmip_surrogate_destroy", "dmip_surrogate_forward", "dmip_log_posterior", "dmip_mh_sample"):
         getattr(lib, name).restype = _i32
 
 
@@ -226,3 +240,55 @@ def histogram(x, nbins, lo, hi, counts):
     n_hist, n, d = x.shape
     check(lib().dmip_histogram(ptr(x), int(n), int(d), int(nbins), float(lo), float(hi), int(n_hist), ptr(counts),
                                stream_of(x.device)))
+
+
+# ------------------------------------------------------------------------- scatterometry surrogate
+class SurrogateHandle:
+    """Owns a dmip_surrogate* (packed f32 MFMA images of the frozen forward model)."""
+
+    def __init__(self, layers, device):
+        widths = (_i32 * 3)(*[int(layers[i][0].shape[0]) for i in range(3)])
+        with torch.cuda.device(device):
+            ws = [w.detach().float().contiguous().cpu() for w, _ in layers]
+            bs = [b.detach().float().contiguous().cpu() for _, b in layers]
+            wp = (_c_void_p * 4)(*[w.data_ptr() for w in ws])
+            bp = (_c_void_p * 4)(*[b.data_ptr() for b in bs])
+            out = _c_void_p()
+            check(lib().dmip_surrogate_create(int(layers[0][0].shape[1]), int(layers[-1][0].shape[0]), 3, widths,
+                                              wp, bp, ctypes.byref(out)))
+        self.h = out
+        self.device = device
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h and _lib is not None:
+            try:
+                torch.cuda.synchronize(self.device)
+            except Exception:
+                pass
+            _lib.dmip_surrogate_destroy(h)
+            self.h = None
+
+
+def scat_noise(a, b, lambd_bd):
+    return DmipScatNoise(float(a), float(b), float(lambd_bd))
+
+
+def surrogate_forward(handle, x, out):
+    calls["surrogate_forward"] = calls.get("surrogate_forward", 0) + 1
+    check(lib().dmip_surrogate_forward(handle.h, ptr(x), int(x.shape[0]), ptr(out), stream_of(x.device)))
+
+
+def log_posterior(handle, noise, x, y, y_stride, e_out, grad_out=None):
+    calls["log_posterior"] = calls.get("log_posterior", 0) + 1
+    check(lib().dmip_log_posterior(handle.h, ctypes.byref(noise), ptr(x), ptr(y), int(y_stride), int(x.shape[0]),
+                                   ptr(e_out), ptr(grad_out), stream_of(x.device)))
+
+
+def mh_sample(handle, noise, y, n_chains, chain_offset, num_steps, noise_std, seed, x_out, x_init=None,
+              inj_noise=None, inj_unif=None, e_out=None):
+    calls["mh_sample"] = calls.get("mh_sample", 0) + 1
+    check(lib().dmip_mh_sample(handle.h, ctypes.byref(noise), ptr(y), int(y.shape[0]), int(n_chains),
+                               int(chain_offset), int(num_steps), float(noise_std),
+                               ctypes.c_uint64(int(seed) & 0xFFFFFFFFFFFFFFFF), ptr(x_init), ptr(inj_noise),
+                               ptr(inj_unif), ptr(x_out), ptr(e_out), stream_of(y.device)))

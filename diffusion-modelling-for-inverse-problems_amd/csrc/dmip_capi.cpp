@@ -525,6 +525,204 @@ int dmip_histogram(const float* x_dev, int64_t n, int d, int nbins, double lo, d
   return e == hipSuccess ? DMIP_OK : hip_fail(e, "histogram launch");
 }
 
+}  // extern "C"
+
+// ------------------------------------------------------------------- scatterometry surrogate
+// f32 A-fragment images for v_mfma_f32_16x16x4_f32 (dmip_surrogate.hip): k-step (q, r) of output
+// tile o, lane l = i + 16 g, holds M[16 o + i][16 q + 4 g + r]; stored [o][q][lane][r] (one float4
+// per lane per q). M(row, col) returns 0 outside the matrix.
+struct dmip_surrogate {
+  float* l1 = nullptr;
+  float* bias = nullptr;
+  char* img[7] = {};  // w2, w3, w4, w3t, w2t, w4t, w1t
+  ~dmip_surrogate() {
+    if (l1) (void)hipFree(l1);
+    if (bias) (void)hipFree(bias);
+    for (char* p : img)
+      if (p) (void)hipFree(p);
+  }
+};
+
+namespace {
+
+template <typename F>
+std::vector<char> pack_f32_tiles(int n_tiles, int n_q, F M) {
+  std::vector<float> v((size_t)n_tiles * n_q * 64 * 4);
+  for (int o = 0; o < n_tiles; ++o)
+    for (int q = 0; q < n_q; ++q)
+      for (int l = 0; l < 64; ++l)
+        for (int r = 0; r < 4; ++r)
+          v[(((size_t)o * n_q + q) * 64 + l) * 4 + r] = M(16 * o + (l & 15), 16 * q + 4 * (l >> 4) + r);
+  std::vector<char> b(v.size() * 4);
+  std::memcpy(b.data(), v.data(), b.size());
+  return b;
+}
+
+int surrogate_check(const dmip_surrogate* s, int64_t n) {
+  if (!s) return fail(DMIP_ERR_INVALID, "null surrogate handle");
+  if (n < 0) return fail(DMIP_ERR_INVALID, "n < 0");
+  return DMIP_OK;
+}
+
+int surrogate_n_wg(int64_t rows) {
+  int n_cu = 256;
+  int dev = 0;
+  hipDeviceProp_t prop;
+  if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess &&
+      prop.multiProcessorCount > 0)
+    n_cu = prop.multiProcessorCount;
+  const int64_t per = dmip::surrogate_rows_per_wg();
+  return (int)std::max<int64_t>(1, std::min<int64_t>(n_cu, (rows + per - 1) / per));
+}
+
+void surrogate_params(const dmip_surrogate* s, dmip::SurrogateParams& p) {
+  p.l1 = s->l1;
+  p.bias = s->bias;
+  p.w2 = s->img[0];
+  p.w3 = s->img[1];
+  p.w4 = s->img[2];
+  p.w3t = s->img[3];
+  p.w2t = s->img[4];
+  p.w4t = s->img[5];
+  p.w1t = s->img[6];
+}
+
+int noise_check(const dmip_scat_noise* nz, dmip::SurrogateParams& p) {
+  if (!nz) return fail(DMIP_ERR_INVALID, "null noise model");
+  if (!(nz->b > 0.0f) || !(nz->a >= 0.0f) || !(nz->lambd_bd >= 0.0f))
+    return fail(DMIP_ERR_INVALID, "noise model needs b > 0, a >= 0, lambd_bd >= 0");
+  p.a = nz->a;
+  p.b2 = (float)((double)nz->b * (double)nz->b);  // python b**2, rounded once to f32 (torch scalar add)
+  p.lam = nz->lambd_bd;
+  return DMIP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dmip_surrogate_create(int in_dim, int out_dim, int n_hidden, const int* widths, const float* const* weights,
+                          const float* const* biases, dmip_surrogate** out) {
+  using dmip::kSurW;
+  if (!out || !widths || !weights || !biases) return fail(DMIP_ERR_INVALID, "null argument");
+  *out = nullptr;
+  if (in_dim != dmip::kSurXdim || out_dim != dmip::kSurYdim || n_hidden != 3)
+    return fail(DMIP_ERR_UNSUPPORTED, "surrogate compiled for in 3, out 23, 3 hidden layers");
+  for (int i = 0; i < 3; ++i)
+    if (widths[i] != kSurW) return fail(DMIP_ERR_UNSUPPORTED, "surrogate compiled for hidden widths [256]*3");
+  for (int i = 0; i < 4; ++i)
+    if (!weights[i] || !biases[i]) return fail(DMIP_ERR_INVALID, "null layer pointer");
+  const float *W1 = weights[0], *W2 = weights[1], *W3 = weights[2], *W4 = weights[3];
+  const int XD = dmip::kSurXdim, YD = dmip::kSurYdim;
+  auto sq = [](const float* Wm) {
+    return [Wm](int r, int c) { return Wm[(size_t)r * kSurW + c]; };
+  };
+  auto tr = [](const float* Wm) {
+    return [Wm](int r, int c) { return Wm[(size_t)c * kSurW + r]; };
+  };
+  std::vector<char> imgs[7] = {
+      pack_f32_tiles(16, 16, sq(W2)),
+      pack_f32_tiles(16, 16, sq(W3)),
+      pack_f32_tiles(2, 16, [&](int r, int c) { return r < YD ? W4[(size_t)r * kSurW + c] : 0.0f; }),
+      pack_f32_tiles(16, 16, tr(W3)),
+      pack_f32_tiles(16, 16, tr(W2)),
+      pack_f32_tiles(16, 2, [&](int r, int c) { return c < YD ? W4[(size_t)c * kSurW + r] : 0.0f; }),
+      pack_f32_tiles(1, 16, [&](int r, int c) { return r < XD ? W1[(size_t)c * XD + r] : 0.0f; }),
+  };
+  std::vector<float> l1((size_t)16 * 64), bias((size_t)3 * kSurW + 32, 0.0f);
+  for (int o = 0; o < 16; ++o)
+    for (int l = 0; l < 64; ++l) {
+      const int row = 16 * o + (l & 15), g = l >> 4;
+      l1[(size_t)o * 64 + l] = g < XD ? W1[(size_t)row * XD + g] : biases[0][row];
+    }
+  for (int li = 0; li < 3; ++li)
+    for (int k = 0; k < kSurW; ++k) bias[(size_t)li * kSurW + k] = biases[li][k];
+  for (int k = 0; k < YD; ++k) bias[(size_t)3 * kSurW + k] = biases[3][k];
+
+  dmip_surrogate* s = new (std::nothrow) dmip_surrogate;
+  if (!s) return fail(DMIP_ERR_ALLOC, "host allocation");
+  int rc = DMIP_OK;
+  if ((rc = upload(&s->l1, l1)) || (rc = upload(&s->bias, bias))) {
+    delete s;
+    return rc;
+  }
+  for (int i = 0; i < 7; ++i)
+    if ((rc = upload(&s->img[i], imgs[i]))) {
+      delete s;
+      return rc;
+    }
+  *out = s;
+  return DMIP_OK;
+}
+
+int dmip_surrogate_destroy(dmip_surrogate* s) {
+  delete s;
+  return DMIP_OK;
+}
+
+int dmip_surrogate_forward(const dmip_surrogate* s, const float* x_dev, int64_t n, float* f_out_dev, void* stream) {
+  if (int rc = surrogate_check(s, n)) return rc;
+  if (n == 0) return DMIP_OK;
+  if (!x_dev || !f_out_dev) return fail(DMIP_ERR_INVALID, "null argument");
+  dmip::SurrogateParams p{};
+  surrogate_params(s, p);
+  p.x = x_dev;
+  p.n = n;
+  p.f_out = f_out_dev;
+  hipError_t e = dmip::launch_surrogate_eval(p, 0, surrogate_n_wg(n), (hipStream_t)stream);
+  return e == hipSuccess ? DMIP_OK : hip_fail(e, "surrogate_forward launch");
+}
+
+int dmip_log_posterior(const dmip_surrogate* s, const dmip_scat_noise* noise, const float* x_dev, const float* y_dev,
+                       int64_t y_stride, int64_t n, float* e_out_dev, float* grad_out_dev, void* stream) {
+  if (int rc = surrogate_check(s, n)) return rc;
+  dmip::SurrogateParams p{};
+  if (int rc = noise_check(noise, p)) return rc;
+  if (y_stride != 0 && y_stride != dmip::kSurYdim) return fail(DMIP_ERR_INVALID, "y_stride must be 0 or 23");
+  if (n == 0) return DMIP_OK;
+  if (!x_dev || !y_dev || !e_out_dev) return fail(DMIP_ERR_INVALID, "null argument");
+  surrogate_params(s, p);
+  p.x = x_dev;
+  p.y = y_dev;
+  p.y_stride = y_stride;
+  p.n = n;
+  p.e_out = e_out_dev;
+  p.g_out = grad_out_dev;
+  hipError_t e = dmip::launch_surrogate_eval(p, grad_out_dev ? 2 : 1, surrogate_n_wg(n), (hipStream_t)stream);
+  return e == hipSuccess ? DMIP_OK : hip_fail(e, "log_posterior launch");
+}
+
+int dmip_mh_sample(const dmip_surrogate* s, const dmip_scat_noise* noise, const float* y_dev, int n_y,
+                   int64_t n_chains, int64_t chain_offset, int num_steps, float noise_std, uint64_t seed,
+                   const float* x_init_dev, const float* noise_dev, const float* unif_dev, float* x_out_dev,
+                   float* e_out_dev, void* stream) {
+  if (int rc = surrogate_check(s, n_chains)) return rc;
+  dmip::SurrogateParams p{};
+  if (int rc = noise_check(noise, p)) return rc;
+  if (!y_dev || !x_out_dev) return fail(DMIP_ERR_INVALID, "null argument");
+  if (n_y < 1 || n_y > 65535) return fail(DMIP_ERR_INVALID, "n_y must be in [1, 65535]");
+  if (chain_offset < 0) return fail(DMIP_ERR_INVALID, "negative chain offset");
+  if (num_steps < 0) return fail(DMIP_ERR_INVALID, "num_steps must be >= 0");
+  if (!(noise_std >= 0.0f)) return fail(DMIP_ERR_INVALID, "noise_std must be >= 0");
+  if ((noise_dev == nullptr) != (unif_dev == nullptr))
+    return fail(DMIP_ERR_INVALID, "inject both the proposal normals and the uniforms, or neither");
+  if (n_chains == 0) return DMIP_OK;
+  surrogate_params(s, p);
+  p.y = y_dev;
+  p.n_chains = n_chains;
+  p.chain_offset = chain_offset;
+  p.num_steps = num_steps;
+  p.noise_std = noise_std;
+  p.seed = seed;
+  p.x_init = x_init_dev;
+  p.noise = noise_dev;
+  p.unif = unif_dev;
+  p.x_out = x_out_dev;
+  p.e_out = e_out_dev;
+  hipError_t e = dmip::launch_mh(p, n_y, (hipStream_t)stream);
+  return e == hipSuccess ? DMIP_OK : hip_fail(e, "mh_sample launch");
+}
+
 int dmip_rng_words(uint64_t seed, int64_t chain_offset, uint64_t stream_id, int64_t n_chains, int n_words,
                    uint32_t* out_dev, void* stream) {
   if (!out_dev || n_chains < 0 || n_words < 0) return fail(DMIP_ERR_INVALID, "bad argument");

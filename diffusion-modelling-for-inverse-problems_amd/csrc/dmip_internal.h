@@ -83,6 +83,44 @@ int train_waves_per_wg();
 hipError_t launch_loss_grad(const TrainParams& p, int n_hidden, float* grads, float* loss_out, float* partials,
                             int n_wg, hipStream_t st);
 
+// Scatterometry surrogate (dmip_surrogate.hip): 3 -> 256 -> 256 -> 256 -> 23 ReLU, exact f32 MFMA.
+constexpr int kSurW = 256, kSurXdim = 3, kSurYdim = 23;
+
+struct SurrogateParams {
+  // packed f32 weight images (dmip_capi.cpp pack_surrogate)
+  const float* l1;     // [16 tiles][64 lanes]: W1 | b1 as k = 0..3
+  const char* w2;      // [16 tiles][16 q][64][4] forward 256 x 256 images
+  const char* w3;
+  const char* w4;      // [2 tiles][16 q][64][4] output layer, rows >= 23 zero
+  const char* w3t;     // transposed images for the reverse pass
+  const char* w2t;
+  const char* w4t;     // [16 tiles][2 q][64][4]
+  const char* w1t;     // [16 q][64][4] (rows >= 3 zero)
+  const float* bias;   // b1 | b2 | b3 [256] | b4 [32]
+  // evaluation
+  const float* x;      // [n][3]
+  const float* y;      // [n][23] (y_stride = 23) or one row (0)
+  long long y_stride;
+  long long n;
+  float* f_out;        // [n][23]
+  float* e_out;        // [n]  (MH: [n_y][n_chains] E(x_S) - E(x_0), optional)
+  float* g_out;        // [n][3]
+  float a, b2, lam;    // noise model a, b^2 and the boundary weight lambda
+  // Metropolis-Hastings
+  long long n_chains, chain_offset;
+  int num_steps;
+  float noise_std;
+  unsigned long long seed;
+  const float* x_init; // [n_y][n_chains][3] or null (uniform on [-1, 1]^3 from the RNG)
+  const float* noise;  // injected proposals [S][n_y][n_chains][3] or null
+  const float* unif;   // injected uniforms  [S][n_y][n_chains]
+  float* x_out;        // [n_y][n_chains][3]
+};
+
+hipError_t launch_surrogate_eval(const SurrogateParams& p, int mode, int n_wg, hipStream_t st);
+int surrogate_rows_per_wg();
+hipError_t launch_mh(const SurrogateParams& p, int n_y, hipStream_t st);
+
 hipError_t launch_histogram(const float* x, long long n, int d, int nbins, double lo, double hi, int n_hist,
                             unsigned int* counts, hipStream_t st);
 

@@ -1,0 +1,429 @@
+// The scatterometry forward model on gfx950: the frozen surrogate 3 -> 256 -> 256 -> 256 -> 23 ReLU
+// (utils_scatterometry.py:8-25), the negative log posterior built on it (get_log_posterior,
+// utils_scatterometry.py:30-38), its input gradient (energy_grad, models/SNF.py:234-237), and the
+// random-walk Metropolis-Hastings ground-truth sampler that anneals to it (anneal_to_energy,
+// models/SNF.py:250-275, driven by generate_scatterometry_ground_truth.py:26-39).
+//
+// Arithmetic: exact f32 on the matrix cores (v_mfma_f32_16x16x4_f32: a k-ordered fmaf chain, no
+// reduced-precision operands). The MH acceptance exp(E_cur - E_prop) and the heteroscedastic
+// likelihood (prefactor (a f)^2 + b^2 with b = 0.01) turn bf16-level errors of f into O(0.1)
+// energy errors for small outputs, so this path keeps the reference's f32.
+//
+// Layout (one wave = 16 chains; 8 waves = 128 chains per workgroup):
+//   * a layer's output tile is 16 units x 16 chains: lane (g = l>>4, j = l&15) holds units 4g + r
+//     (r = 0..3) of chain j. That tile IS the B operand of 4 k-steps of the next layer (k-step r
+//     takes register r: B[k = g][j]), so activations stay in registers between layers, in f32.
+//   * weights are packed on the host so the A fragment of k-step (q, r) of output tile o is
+//     lane (i, g): W[16o + i][16q + 4g + r] -- a float4 per lane per q (one ds_read_b128 for
+//     4 MFMAs).
+//   * the 256 x 256 layers (forward W2, W3; backward W3^T, W2^T) and the output layer W4 stream
+//     from L2 through a 4-slot LDS ring in 16 KiB chunks (one output tile each) by LDS-DMA;
+//     layer 1, W4^T, W1^T and the biases are LDS-resident.
+//   * the gradient is a reverse pass (vector-Jacobian product) with the ReLU masks of the forward
+//     pass kept as bits (2 VGPRs per layer).
+#include "dmip_device.h"
+#include "dmip_internal.h"
+
+namespace dmip {
+namespace sg {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int W = kSurW;           // 256
+constexpr int ST = W / 16;         // 16 output tiles per 256-wide layer
+constexpr int KG = W / 16;         // 16 k-groups (of 4 k-steps) over 256 inputs
+constexpr int XD = kSurXdim, YD = kSurYdim;
+constexpr int NW = 8;              // waves per workgroup (two per SIMD)
+constexpr int R = 4;               // ring slots
+constexpr int CHUNK = KG * 64 * 16;      // 16 KiB
+constexpr int PPW = CHUNK / 1024 / NW;   // LDS-DMA pieces per wave per chunk
+constexpr int NCF = 2 * ST + 2;          // forward chunks per evaluation: W2, W3 tiles, W4 tiles
+constexpr int NCB = 2 * ST;              // backward chunks: W3^T, W2^T tiles
+
+// LDS layout
+constexpr int L1_OFF = 0, L1_BYTES = ST * 64 * 4;
+constexpr int BIAS_OFF = L1_OFF + L1_BYTES;  // b1 | b2 | b3 [256] | b4 [32]
+constexpr int BIAS_FLOATS = 3 * W + 32;
+constexpr int Y_OFF = BIAS_OFF + BIAS_FLOATS * 4;  // the workgroup's observation y [32]
+constexpr int W4T_OFF = Y_OFF + 32 * 4;
+constexpr int W4T_BYTES = ST * 2 * 64 * 16;
+constexpr int W1T_OFF = W4T_OFF + W4T_BYTES;
+constexpr int W1T_BYTES = KG * 64 * 16;
+template <bool GRAD>
+struct LayoutS {
+  static constexpr int RING_OFF = GRAD ? W1T_OFF + W1T_BYTES : W4T_OFF;
+  static constexpr int TOTAL = RING_OFF + R * CHUNK;
+  static constexpr int NCT = GRAD ? NCF + NCB : NCF;
+};
+static_assert(LayoutS<true>::TOTAL <= 160 * 1024, "LDS budget");
+static_assert(W4T_OFF % 16 == 0 && L1_BYTES % 16 == 0, "LDS-DMA alignment");
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float shfl_xor(float v, int m) { return __shfl_xor(v, m, 64); }
+
+template <bool GRAD>
+struct Engine {
+  using LS = LayoutS<GRAD>;
+  char* lds;
+  const char* src[5];  // streamed images in chunk order: W2, W3, W4, W3^T, W2^T
+  long long gc;
+  int w, lane, g;
+
+  __device__ __forceinline__ const char* chunk_src(int c) const {
+    if (c < ST) return src[0] + (size_t)c * CHUNK;
+    if (c < 2 * ST) return src[1] + (size_t)(c - ST) * CHUNK;
+    if (c < NCF) return src[2] + (size_t)(c - 2 * ST) * CHUNK;
+    if (c < NCF + ST) return src[3] + (size_t)(c - NCF) * CHUNK;
+    return src[4] + (size_t)(c - NCF - ST) * CHUNK;
+  }
+
+  __device__ __forceinline__ void ring_issue(long long gi) {
+    const char* base = chunk_src((int)(gi % LS::NCT));
+    char* dst = lds + LS::RING_OFF + (int)(gi % R) * CHUNK;
+#pragma unroll
+    for (int q = 0; q < PPW; ++q) {
+      const int piece = w * PPW + q;
+      const char* gp = base + piece * 1024;
+      asm volatile("" : "+s"(gp));  // keep the per-chunk address out of the loop-invariant hoist
+      glds16(gp, dst + piece * 1024, lane);
+    }
+  }
+
+  // the next chunk of the stream: landed (own pieces counted, others' by the barrier), and the
+  // slot it replaces is refilled R-1 chunks ahead. Other VMEM ops only make the wait stricter.
+  __device__ __forceinline__ const char* chunk_sync() {
+    wait_vmcnt<(R - 2) * PPW>();
+    lds_barrier();
+    ring_issue(gc + R - 1);
+    const char* slot = lds + LS::RING_OFF + (int)(gc % R) * CHUNK;
+    ++gc;
+    return slot;
+  }
+
+  __device__ __forceinline__ void prologue(const SurrogateParams& p) {
+    const int tid = threadIdx.x;
+    stage_lds(lds + L1_OFF, (const char*)p.l1, L1_BYTES);
+    if constexpr (GRAD) {
+      stage_lds(lds + W4T_OFF, p.w4t, W4T_BYTES);
+      stage_lds(lds + W1T_OFF, p.w1t, W1T_BYTES);
+    }
+    float* bl = (float*)(lds + BIAS_OFF);
+    for (int i = tid; i < BIAS_FLOATS; i += NW * 64) bl[i] = p.bias[i];
+    wait_vmcnt<0>();
+    __syncthreads();
+    for (int q = 0; q < R - 1; ++q) ring_issue(q);
+  }
+
+  __device__ __forceinline__ void stage_lds(char* dst, const char* src, int bytes) {
+    for (int blk = w; blk < bytes / 1024; blk += NW) glds16(src + blk * 1024, dst + blk * 1024, lane);
+  }
+
+  __device__ __forceinline__ void epilogue() { wait_vmcnt<0>(); }
+
+  __device__ __forceinline__ f32x4 bias4(int layer, int tile) const {
+    return *(const f32x4*)((const float*)(lds + BIAS_OFF) + layer * W + 16 * tile + 4 * g);
+  }
+
+  // layer 1 (3 -> 256, bias as the 4th k): exact f32, then ReLU (+ mask bits)
+  __device__ __forceinline__ void layer1(const float (&x)[XD], float (&H)[ST][4], uint32_t (&m)[2]) {
+    const float bsel = g == 0 ? x[0] : (g == 1 ? x[1] : (g == 2 ? x[2] : 1.0f));
+    m[0] = m[1] = 0u;
+#pragma unroll
+    for (int o = 0; o < ST; ++o) {
+      const float a = ((const float*)(lds + L1_OFF))[o * 64 + lane];
+      const f32x4 z = mfma4(a, bsel, f32x4{0.0f, 0.0f, 0.0f, 0.0f});
+      relu_tile(z, o, H, m);
+    }
+  }
+
+  __device__ __forceinline__ static void relu_tile(const f32x4& z, int o, float (&H)[ST][4], uint32_t (&m)[2]) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const bool pos = z[r] > 0.0f;
+      H[o][r] = pos ? z[r] : 0.0f;
+      if constexpr (GRAD) m[o >> 3] |= (pos ? 1u : 0u) << ((o & 7) * 4 + r);
+    }
+  }
+
+  // acc(tile) = sum over the 64 k-steps of a streamed 256-k chunk; two accumulation chains
+  // (even / odd k-groups) so the 40-cycle MFMA dependency does not pace one wave
+  __device__ __forceinline__ static f32x4 tile_product(const char* ch, int lane, const float (&H)[ST][4],
+                                                        f32x4 acc0) {
+    f32x4 acc1 = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int q = 0; q < KG; ++q) {
+      const f32x4 a = *(const f32x4*)(ch + (q * 64 + lane) * 16);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (q & 1) acc1 = mfma4(a[r], H[q][r], acc1);
+        else acc0 = mfma4(a[r], H[q][r], acc0);
+      }
+    }
+    return acc0 + acc1;
+  }
+
+  // a 256 -> 256 ReLU layer from the ring (layer index li = 1, 2 for the biases)
+  __device__ __forceinline__ void hidden(int li, const float (&Hin)[ST][4], float (&Hout)[ST][4], uint32_t (&m)[2]) {
+    m[0] = m[1] = 0u;
+#pragma unroll
+    for (int o = 0; o < ST; ++o) {
+      const char* ch = chunk_sync();
+      const f32x4 z = tile_product(ch, lane, Hin, bias4(li, o));
+      relu_tile(z, o, Hout, m);
+    }
+  }
+
+  // output layer (256 -> 23, two 16-row tiles): f rows 16t + 4g + r
+  __device__ __forceinline__ void output(const float (&Hin)[ST][4], f32x4 (&f)[2]) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const char* ch = chunk_sync();
+      f[t] = tile_product(ch, lane, Hin, bias4(3, t));
+    }
+  }
+
+  // full forward; masks only in GRAD mode
+  __device__ __forceinline__ void forward(const float (&x)[XD], f32x4 (&f)[2], uint32_t (&m)[3][2]) {
+    float Ha[ST][4], Hb[ST][4];
+    layer1(x, Ha, m[0]);
+    hidden(1, Ha, Hb, m[1]);
+    hidden(2, Hb, Ha, m[2]);
+    output(Ha, f);
+  }
+
+  // reverse pass: v = dE/df (rows as f) -> dE/dx (every lane of the chain gets it)
+  __device__ __forceinline__ void backward(const f32x4 (&v)[2], const uint32_t (&m)[3][2], float (&gx)[XD]) {
+    float Ga[ST][4], Gb[ST][4];
+    // W4^T (LDS-resident, k = 32 padded output rows): unit tiles of layer 3, masked by m3
+#pragma unroll
+    for (int o = 0; o < ST; ++o) {
+      f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const f32x4 a = *(const f32x4*)(lds + W4T_OFF + ((o * 2 + q) * 64 + lane) * 16);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc = mfma4(a[r], v[q][r], acc);
+      }
+      mask_tile(acc, o, m[2], Ga);
+    }
+    // W3^T then W2^T from the ring
+#pragma unroll
+    for (int o = 0; o < ST; ++o) {
+      const char* ch = chunk_sync();
+      mask_tile(tile_product(ch, lane, Ga, f32x4{0.0f, 0.0f, 0.0f, 0.0f}), o, m[1], Gb);
+    }
+#pragma unroll
+    for (int o = 0; o < ST; ++o) {
+      const char* ch = chunk_sync();
+      mask_tile(tile_product(ch, lane, Gb, f32x4{0.0f, 0.0f, 0.0f, 0.0f}), o, m[0], Ga);
+    }
+    // W1^T (LDS-resident): rows 0..2 = dE/dx at lane group 0
+    asm volatile("" ::: "memory");
+    const f32x4 gxa = tile_product(lds + W1T_OFF, lane, Ga, f32x4{0.0f, 0.0f, 0.0f, 0.0f});
+    const int src = lane & 15;
+#pragma unroll
+    for (int d = 0; d < XD; ++d) gx[d] = __shfl(gxa[d], src, 64);
+  }
+
+  __device__ __forceinline__ static void mask_tile(const f32x4& z, int o, const uint32_t (&m)[2], float (&G)[ST][4]) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) G[o][r] = ((m[o >> 3] >> ((o & 7) * 4 + r)) & 1u) ? z[r] : 0.0f;
+  }
+};
+
+// Negative log posterior of the scatterometry problem (utils_scatterometry.py:30-38):
+//   E = 0.5 sum_k log((a f_k)^2 + b^2) + 0.5 sum_k (y_k - f_k)^2 / ((a f_k)^2 + b^2)
+//       + lambda sum_d relu(x_d - 1) + relu(-1 - x_d)
+// The 23 output rows are spread over the 4 lane groups of a chain: partial sums, then two xor
+// shuffles. v = dE/df_k for the reverse pass (rows >= 23 zero).
+__device__ __forceinline__ float energy(const f32x4 (&f)[2], const float* y, const float (&x)[XD], float a,
+                                        float b2, float lam, int g, f32x4 (&v)[2], bool want_v) {
+  float slog = 0.0f, ssq = 0.0f;
+  const float a2 = a * a;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 16 * t + 4 * g + r;
+      float vk = 0.0f;
+      if (row < YD) {
+        const float fk = f[t][r];
+        const float af = a * fk;
+        const float pref = af * af + b2;
+        const float res = y[row] - fk;
+        slog += logf(pref);
+        const float q = res * res / pref;
+        ssq += q;
+        if (want_v) {
+          // d/df [0.5 log pref + 0.5 res^2 / pref] = a^2 f / pref - res / pref - a^2 f res^2 / pref^2
+          vk = (a2 * fk * (1.0f - q) - res) / pref;
+        }
+      }
+      v[t][r] = vk;
+    }
+  }
+  slog += shfl_xor(slog, 16);
+  slog += shfl_xor(slog, 32);
+  ssq += shfl_xor(ssq, 16);
+  ssq += shfl_xor(ssq, 32);
+  float bd = 0.0f;
+#pragma unroll
+  for (int d = 0; d < XD; ++d) bd += fmaxf(x[d] - 1.0f, 0.0f) + fmaxf(-1.0f - x[d], 0.0f);
+  return 0.5f * slog + 0.5f * ssq + lam * bd;
+}
+
+__device__ __forceinline__ float boundary_grad(float xd, float lam) {
+  return (xd > 1.0f ? lam : 0.0f) - (xd < -1.0f ? lam : 0.0f);
+}
+
+// ------------------------------------------------------------------------- evaluation kernel
+// MODE 0: f = F(x); 1: E(x, y); 2: E and dE/dx. Rows strided over the grid, 16 per wave.
+template <int MODE>
+__global__ void __launch_bounds__(NW * 64, 1) surrogate_eval_kernel(SurrogateParams p) {
+  constexpr bool GRAD = MODE == 2;
+  using LS = LayoutS<GRAD>;
+  __shared__ __attribute__((aligned(16))) char lds[LS::TOTAL];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4;
+  Engine<GRAD> eng{lds, {p.w2, p.w3, p.w4, p.w3t, p.w2t}, 0, w, lane, g};
+  eng.prologue(p);
+  const long long n_tiles = (p.n + 15) / 16;
+  const long long per_round = (long long)gridDim.x * NW;
+  const long long rounds = (n_tiles + per_round - 1) / per_round;
+  for (long long rd = 0; rd < rounds; ++rd) {
+    const long long row = ((rd * gridDim.x + blockIdx.x) * NW + w) * 16 + (lane & 15);
+    const bool valid = row < p.n;
+    const long long rr = valid ? row : 0;
+    float x[XD];
+#pragma unroll
+    for (int d = 0; d < XD; ++d) x[d] = p.x[rr * XD + d];
+    f32x4 f[2];
+    uint32_t m[3][2];
+    eng.forward(x, f, m);
+    if constexpr (MODE == 0) {
+      if (valid) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int k = 16 * t + 4 * g + r;
+            if (k < YD) p.f_out[row * YD + k] = f[t][r];
+          }
+      }
+    } else {
+      const float* y = p.y + (p.y_stride ? rr * p.y_stride : 0);
+      f32x4 v[2];
+      const float e = energy(f, y, x, p.a, p.b2, p.lam, g, v, GRAD);
+      if (valid && g == 0) p.e_out[row] = e;
+      if constexpr (GRAD) {
+        float gx[XD];
+        eng.backward(v, m, gx);
+        if (valid && g == 0) {
+#pragma unroll
+          for (int d = 0; d < XD; ++d) p.g_out[row * XD + d] = gx[d] + boundary_grad(x[d], p.lam);
+        }
+      }
+    }
+  }
+  eng.epilogue();
+}
+
+// ------------------------------------------------------------------- Metropolis-Hastings kernel
+// anneal_to_energy (models/SNF.py:250-275) without Langevin proposals: per step
+//   x_prop = x + noise_std * xi;  accept iff u < exp(-E(x_prop) + E(x))
+// with E the negative log posterior above for this workgroup's y. The chain state (x, E(x), RNG)
+// stays in registers for all steps (every lane of a chain carries an identical copy); E(x) is
+// carried instead of being recomputed (the reference's energy(x_curr) is the same value).
+// Outputs x and E(x_final) - E(x_0) (the reference's second return value).
+// INJECT: xi [S][n_y][n][3] and u [S][n_y][n] replace the RNG (replaying captured draws).
+template <bool INJECT>
+__global__ void __launch_bounds__(NW * 64, 1) mh_kernel(SurrogateParams p) {
+  using LS = LayoutS<false>;
+  __shared__ __attribute__((aligned(16))) char lds[LS::TOTAL];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4;
+  const int yi = blockIdx.y;
+  const long long c_local = (long long)blockIdx.x * (NW * 16) + w * 16 + (lane & 15);
+  const bool valid = c_local < p.n_chains;
+  const long long cc = valid ? c_local : 0;
+  Engine<false> eng{lds, {p.w2, p.w3, p.w4, p.w3t, p.w2t}, 0, w, lane, g};
+  float* ylds = (float*)(lds + Y_OFF);
+  for (int i = threadIdx.x; i < 32; i += NW * 64) ylds[i] = i < YD ? p.y[(size_t)yi * YD + i] : 0.0f;
+  eng.prologue(p);
+
+  Rng rng = rng_init(p.seed, (uint64_t)(p.chain_offset + c_local), (uint64_t)yi);
+  float x[XD];
+  if (p.x_init) {
+#pragma unroll
+    for (int d = 0; d < XD; ++d) x[d] = p.x_init[((size_t)yi * p.n_chains + cc) * XD + d];
+  } else {
+    // torch.rand(n, 3) * 2 - 1 (generate_scatterometry_ground_truth.py:27)
+#pragma unroll
+    for (int d = 0; d < XD; ++d) x[d] = (float)(rng_next(rng) >> 8) * 0x1p-24f * 2.0f - 1.0f;
+  }
+  f32x4 f[2], v[2];
+  uint32_t m[3][2];
+  eng.forward(x, f, m);
+  const float e0 = energy(f, ylds, x, p.a, p.b2, p.lam, g, v, false);
+  float e_cur = e0;
+  const size_t plane = (size_t)gridDim.y * p.n_chains;
+  for (int s = 0; s < p.num_steps; ++s) {
+    float xi[XD], u;
+    if constexpr (INJECT) {
+      const float* src = p.noise + ((size_t)s * plane + (size_t)yi * p.n_chains + cc) * XD;
+#pragma unroll
+      for (int d = 0; d < XD; ++d) xi[d] = src[d];
+      u = p.unif[(size_t)s * plane + (size_t)yi * p.n_chains + cc];
+    } else {
+      rng_normals<XD>(rng, xi);
+      u = (float)(rng_next(rng) >> 8) * 0x1p-24f;
+    }
+    float xp[XD];
+#pragma unroll
+    for (int d = 0; d < XD; ++d) xp[d] = x[d] + p.noise_std * xi[d];
+    eng.forward(xp, f, m);
+    const float e_prop = energy(f, ylds, xp, p.a, p.b2, p.lam, g, v, false);
+    const bool acc = u < expf(-e_prop + e_cur);
+#pragma unroll
+    for (int d = 0; d < XD; ++d) x[d] = acc ? xp[d] : x[d];
+    e_cur = acc ? e_prop : e_cur;
+  }
+  eng.epilogue();
+  if (valid && g == 0) {
+    float* dst = p.x_out + ((size_t)yi * p.n_chains + c_local) * XD;
+#pragma unroll
+    for (int d = 0; d < XD; ++d) dst[d] = x[d];
+    if (p.e_out) p.e_out[(size_t)yi * p.n_chains + c_local] = e_cur - e0;
+  }
+}
+
+}  // namespace sg
+
+hipError_t launch_surrogate_eval(const SurrogateParams& p, int mode, int n_wg, hipStream_t st) {
+  const dim3 grid((unsigned)n_wg), block(sg::NW * 64);
+  switch (mode) {
+    case 0: hipLaunchKernelGGL(sg::surrogate_eval_kernel<0>, grid, block, 0, st, p); break;
+    case 1: hipLaunchKernelGGL(sg::surrogate_eval_kernel<1>, grid, block, 0, st, p); break;
+    default: hipLaunchKernelGGL(sg::surrogate_eval_kernel<2>, grid, block, 0, st, p); break;
+  }
+  return hipGetLastError();
+}
+
+int surrogate_rows_per_wg() { return sg::NW * 16; }
+
+hipError_t launch_mh(const SurrogateParams& p, int n_y, hipStream_t st) {
+  const long long per_wg = sg::NW * 16;
+  const dim3 grid((unsigned)((p.n_chains + per_wg - 1) / per_wg), (unsigned)n_y), block(sg::NW * 64);
+  if (p.noise)
+    hipLaunchKernelGGL(sg::mh_kernel<true>, grid, block, 0, st, p);
+  else
+    hipLaunchKernelGGL(sg::mh_kernel<false>, grid, block, 0, st, p);
+  return hipGetLastError();
+}
+
+}  // namespace dmip

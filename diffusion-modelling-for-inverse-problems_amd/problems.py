@@ -2,8 +2,11 @@
 "Scatterometry problem", "Datasets"), with the reference's function names so the drivers keep
 working: linear_problem.py:5-65, utils_scatterometry.py:8-52, datasets.py:8-54, models/SNF.py:234-237.
 
-These are host-side data producers (a few small torch ops per call); the hot path consumes their
-outputs (y observations, training pairs) on the device.
+The data producers are host-side torch ops; the hot path consumes their outputs (y observations,
+training pairs) on the device. The scatterometry posterior itself (get_log_posterior, energy_grad)
+and the Metropolis-Hastings ground-truth sampler (anneal_to_energy) run on the device as fused
+exact-f32 MFMA kernels (libdmip dmip_log_posterior / dmip_mh_sample, csrc/dmip_surrogate.hip)
+whenever the samples are on a HIP device and the forward model is the reference's surrogate shape.
 """
 import os
 
@@ -85,9 +88,77 @@ def load_forward_model(src_dir):
     return fm, dict(SCAT_PARAMS)
 
 
+_SUR_SHAPES = [(256, 3), (256, 256), (256, 256), (23, 256)]
+
+
+def _surrogate_layers(forward_model):
+    """[(weight, bias)] if forward_model is the reference surrogate (Linear/ReLU x3/Linear,
+    3 -> 256 -> 256 -> 256 -> 23, utils_scatterometry.py:9-12), else None."""
+    if not isinstance(forward_model, nn.Sequential) or len(forward_model) != 7:
+        return None
+    mods = list(forward_model)
+    if not all(isinstance(mods[i], nn.ReLU) for i in (1, 3, 5)):
+        return None
+    lin = [mods[i] for i in (0, 2, 4, 6)]
+    if not all(isinstance(m, nn.Linear) and m.bias is not None for m in lin):
+        return None
+    if [tuple(m.weight.shape) for m in lin] != _SUR_SHAPES:
+        return None
+    return [(m.weight, m.bias) for m in lin]
+
+
+def surrogate_handle(forward_model, device):
+    """Packed device images of the frozen surrogate (dmip_surrogate_create), cached on the module
+    per parameter snapshot; None if the module is not the compiled surrogate shape."""
+    from . import _lib
+    layers = _surrogate_layers(forward_model)
+    if layers is None:
+        return None
+    key = (str(device),) + tuple((p.data_ptr(), p._version) for p in forward_model.parameters())
+    cached = getattr(forward_model, "_dmip_surrogate", None)
+    if cached is None or cached[0] != key:
+        cached = (key, _lib.SurrogateHandle(layers, device))
+        forward_model._dmip_surrogate = cached
+    return cached[1]
+
+
+class _FusedLogPosterior(torch.autograd.Function):
+    """get_log_posterior on the device: E and (when samples need a gradient) dE/dx from one launch of
+    the fused kernel; backward scales the stored gradient (first order, as energy_grad uses it)."""
+
+    @staticmethod
+    def forward(ctx, samples, handle, noise, ys, y_stride):
+        from . import _lib
+        x = samples.detach().to(torch.float32).contiguous()
+        e = torch.empty(x.shape[0], device=x.device, dtype=torch.float32)
+        g = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+        _lib.log_posterior(handle, noise, x, ys, y_stride, e, g)
+        ctx.save_for_backward(g if g is not None else e)
+        ctx.has_grad = g is not None
+        return e
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, ge):
+        (g,) = ctx.saved_tensors
+        return (ge[:, None] * g if ctx.has_grad else None), None, None, None, None
+
+
 def get_log_posterior(samples, forward_model, a, b, ys, lambd_bd):
     """Negative log posterior: heteroscedastic Gaussian likelihood + boundary-penalty prior
-    (utils_scatterometry.py:30-38)."""
+    (utils_scatterometry.py:30-38). On a HIP device with the reference surrogate: the fused exact-f32
+    kernel (differentiable w.r.t. samples, first order); otherwise the reference's torch ops."""
+    if isinstance(samples, torch.Tensor) and samples.is_cuda:
+        h = surrogate_handle(forward_model, samples.device)
+        if h is not None and samples.ndim == 2 and samples.shape[1] == 3:
+            from . import _lib
+            y = torch.as_tensor(ys).to(device=samples.device, dtype=torch.float32)
+            if y.ndim == 1 or y.shape[0] == 1:
+                y, stride = y.reshape(1, -1).contiguous(), 0
+            else:
+                y = y.expand(samples.shape[0], -1).contiguous()
+                stride = y.shape[1]
+            return _FusedLogPosterior.apply(samples, h, _lib.scat_noise(a, b, lambd_bd), y, stride)
     f = forward_model(samples)
     pref = (a * f) ** 2 + b ** 2
     p = .5 * torch.sum(torch.log(pref), dim=1)
@@ -114,6 +185,90 @@ def energy_grad(x, energy):
     x = x.requires_grad_(True)
     e = energy(x)
     return torch.autograd.grad(e.sum(), x, create_graph=True)[0], e
+
+
+# ------------------------------------------------------- Metropolis-Hastings ground truth (F3)
+class ScatterometryEnergy:
+    """energy(x) = get_log_posterior(x, forward_model, a, b, y, lambd_bd) for one observation y -- the
+    `mcmc_energy` of generate_scatterometry_ground_truth.py:61 as an object anneal_to_energy can fuse."""
+
+    def __init__(self, forward_model, a, b, y, lambd_bd):
+        self.forward_model, self.a, self.b, self.lambd_bd = forward_model, a, b, lambd_bd
+        self.y = torch.as_tensor(y, dtype=torch.float32).reshape(-1)
+
+    def __call__(self, x):
+        return get_log_posterior(x, self.forward_model, self.a, self.b, self.y.to(x.device)[None, :], self.lambd_bd)
+
+
+def mh_sample(forward_model, params, ys, n_chains, num_steps, noise_std, seed=None, chain_offset=0, x_init=None,
+              noise=None, unif=None, return_ediff=False):
+    """Fused random-walk MH (dmip_mh_sample) for every row of ys (n_y, 23): device tensor
+    (n_y, n_chains, 3). x_init (n_y, n_chains, 3) or None for x0 ~ U[-1, 1]^3 from the chain RNG;
+    noise (S, n_y, n_chains, 3) / unif (S, n_y, n_chains) replay captured draws."""
+    from . import _lib
+    ys = torch.as_tensor(ys)
+    if not torch.cuda.is_available():
+        raise RuntimeError("dmip: MH sampling needs a HIP device (fused kernel; there is no CPU path)")
+    dev = ys.device if ys.is_cuda else torch.device("cuda", torch.cuda.current_device())
+    ys = ys.to(device=dev, dtype=torch.float32).reshape(-1, 23).contiguous()
+    h = surrogate_handle(forward_model, dev)
+    if h is None:
+        raise ValueError("mh_sample: forward_model is not the scatterometry surrogate shape (3 -> 256^3 -> 23)")
+    if seed is None:
+        seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+    out = torch.empty(ys.shape[0], int(n_chains), 3, device=dev, dtype=torch.float32)
+    ed = torch.empty(ys.shape[0], int(n_chains), device=dev, dtype=torch.float32) if return_ediff else None
+    prep = lambda t: None if t is None else t.to(device=dev, dtype=torch.float32).contiguous()
+    _lib.mh_sample(h, _lib.scat_noise(params['a'], params['b'], params['lambd_bd']), ys, n_chains, chain_offset,
+                   num_steps, noise_std, seed, out, prep(x_init), prep(noise), prep(unif), ed)
+    return (out, ed) if return_ediff else out
+
+
+def anneal_to_energy(x_curr, energy, metr_steps_per_block, noise_std=0.1, langevin_prop=False, lang_steps=None,
+                     stepsize=None):
+    """models/SNF.py:250-275 (random-walk proposals). Returns (x, E(x) - E(x0)). With a
+    ScatterometryEnergy and device samples: one fused launch for all steps; any other energy
+    callable: the reference's loop (its energy evaluations still go to the device kernel when the
+    callable is get_log_posterior on device samples)."""
+    if langevin_prop:
+        raise NotImplementedError("Langevin proposals belong to the SNF baseline (out of scope, SURVEY.md §2)")
+    if isinstance(energy, ScatterometryEnergy) and x_curr.is_cuda:
+        x0 = x_curr.detach().to(torch.float32).reshape(1, -1, 3).contiguous()
+        x, ed = mh_sample(energy.forward_model, {'a': energy.a, 'b': energy.b, 'lambd_bd': energy.lambd_bd},
+                          energy.y.to(x_curr.device)[None, :], x0.shape[1], metr_steps_per_block, noise_std,
+                          x_init=x0, return_ediff=True)
+        return x[0], ed[0]
+    e0 = energy(x_curr)
+    e_curr = e0
+    for _ in range(metr_steps_per_block):
+        x_prop = x_curr + noise_std * torch.randn_like(x_curr)
+        e_prop = energy(x_prop)
+        e_curr = energy(x_curr)
+        acc = (torch.rand_like(e_prop) < torch.exp(-e_prop + e_curr)).float().view(len(x_prop), 1)
+        x_curr = (1. - acc) * x_curr + acc * x_prop
+        e_curr = (1. - acc.view(-1)) * e_curr + acc.view(-1) * e_prop
+    return x_curr, e_curr.view(-1) - e0.view(-1)
+
+
+def generate_gt_samples(forward_model, params, ys, out_dir=None, n_samples_x=30000, n_repeats=10, metr_steps=1000,
+                        noise_std=0.5, seed=None):
+    """generate_scatterometry_ground_truth.py:26-63 on the device: for every y and repeat j,
+    n_samples_x MH chains from U[-1, 1]^3 for metr_steps steps (NOISE_STD_MCMC, METR_STEPS of
+    config_scatterometry.yml), all in one launch; optionally written as out_dir/<i>/<j>.npy.
+    Returns a device tensor (n_y, n_repeats, n_samples_x, 3)."""
+    ys = torch.as_tensor(ys, dtype=torch.float32).reshape(-1, 23)
+    rows = ys.repeat_interleave(n_repeats, dim=0)
+    x = mh_sample(forward_model, params, rows, n_samples_x, metr_steps, noise_std, seed=seed)
+    x = x.reshape(ys.shape[0], n_repeats, n_samples_x, 3)
+    if out_dir:
+        xh = x.cpu().numpy()
+        for i in range(ys.shape[0]):
+            d = os.path.join(out_dir, str(i))
+            os.makedirs(d, exist_ok=True)
+            for j in range(n_repeats):
+                with open(os.path.join(d, '%d.npy' % j), 'wb') as fh:
+                    np.save(fh, xh[i, j])
+    return x
 
 
 # ---------------------------------------------------------------------------------- datasets

@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define DMIP_ABI_VERSION 3
+#define DMIP_ABI_VERSION 4
 
 typedef enum {
   DMIP_OK = 0,
@@ -163,6 +163,51 @@ int dmip_loss_grad_supported(int in_dim, int out_dim, int n_hidden, const int* w
  *   counts_dev [n_hist][nbins^d] uint32, accumulated (zero it first) */
 int dmip_histogram(const float* x_dev, int64_t n, int d, int nbins, double lo, double hi, int n_hist,
                    uint32_t* counts_dev, void* stream);
+
+/* ---- scatterometry forward model --------------------------------------- */
+typedef struct dmip_surrogate dmip_surrogate;
+
+/* Noise model and prior of the scatterometry problem (utils_scatterometry.py:18-21): y = f(x) +
+ * b eps1 + a f(x) eps2, boundary-penalty prior with weight lambd_bd. */
+typedef struct {
+  float a, b, lambd_bd;
+} dmip_scat_noise;
+
+/* Create a handle for the frozen scatterometry surrogate nn.Sequential(Linear(3,256), ReLU,
+ * Linear(256,256), ReLU, Linear(256,256), ReLU, Linear(256,23)) from fp32 host weights (state_dict
+ * keys 0, 2, 4, 6; nn.Linear layout). Replaces: load_forward_model (utils_scatterometry.py:8-25).
+ * Compiled for exactly that shape (in 3, widths [256]*3, out 23); arithmetic is exact f32 (f32
+ * MFMA, fmaf-chain accumulation). */
+int dmip_surrogate_create(int in_dim, int out_dim, int n_hidden, const int* widths, const float* const* weights,
+                          const float* const* biases, dmip_surrogate** out);
+int dmip_surrogate_destroy(dmip_surrogate* s);
+
+/* f_out[n][23] = forward_model(x[n][3]) (the surrogate's forward, e.g. datasets.py:11-13). */
+int dmip_surrogate_forward(const dmip_surrogate* s, const float* x_dev, int64_t n, float* f_out_dev, void* stream);
+
+/* e_out[n] = get_log_posterior(x, forward_model, a, b, y, lambd_bd) (utils_scatterometry.py:30-38,
+ * the NEGATIVE log posterior up to a constant) and, if grad_out_dev is not NULL, grad_out[n][3] =
+ * d e / d x as energy_grad computes it by autograd (models/SNF.py:234-237; the posterior score is
+ * its negative, main_diffusion_scatterometry.py:65-66).
+ *   y_dev [n][23] (y_stride = 23) or one observation broadcast to all rows (y_stride = 0) */
+int dmip_log_posterior(const dmip_surrogate* s, const dmip_scat_noise* noise, const float* x_dev, const float* y_dev,
+                       int64_t y_stride, int64_t n, float* e_out_dev, float* grad_out_dev, void* stream);
+
+/* Random-walk Metropolis-Hastings ground-truth sampler, fused (all steps in one launch, chain state
+ * in registers). Replaces: anneal_to_energy(x0, energy, METR_STEPS, noise_std) (models/SNF.py:250-275)
+ * with energy = get_log_posterior(., y) as generate_scatterometry_ground_truth.py:26-28,59-62 drives it:
+ * x_prop = x + noise_std xi, accept iff u < exp(E(x) - E(x_prop)).
+ *   y_dev       [n_y][23]; chains of y index k go to x_out[k]
+ *   x_init_dev  [n_y][n_chains][3] start points, or NULL for x0 ~ U[-1, 1]^3 from the chain RNG
+ *               (torch.rand(n, 3) * 2 - 1, generate_scatterometry_ground_truth.py:27)
+ *   noise_dev / unif_dev   NULL, or injected proposal normals [S][n_y][n_chains][3] and acceptance
+ *               uniforms [S][n_y][n_chains] (replaying captured draws; both or neither)
+ *   x_out_dev   [n_y][n_chains][3];  e_out_dev (optional) [n_y][n_chains] = E(x_S) - E(x_0)
+ * The RNG stream of chain c of y index k is a function of (seed, chain_offset + c, k). */
+int dmip_mh_sample(const dmip_surrogate* s, const dmip_scat_noise* noise, const float* y_dev, int n_y,
+                   int64_t n_chains, int64_t chain_offset, int num_steps, float noise_std, uint64_t seed,
+                   const float* x_init_dev, const float* noise_dev, const float* unif_dev, float* x_out_dev,
+                   float* e_out_dev, void* stream);
 
 /* Test hooks for the parity suite (integer RNG stream, normals, schedule). */
 int dmip_rng_words(uint64_t seed, int64_t chain_offset, uint64_t stream_id, int64_t n_chains, int n_words,

@@ -543,3 +543,89 @@ def loss_grad(params, x, y, t, eps, kind="pinn", pde="FPE", pde_metric="L1", ic_
         backward(cache_C, abar, None, u_C)
     comps["loss"] = loss
     return loss, comps, grads
+
+
+# ------------------------------------------------------------------------------------------
+# F2  scatterometry surrogate, negative log posterior and its input gradient
+#     utils_scatterometry.py:8-25 (model), :30-38 (get_log_posterior), models/SNF.py:234-237
+#     (energy_grad by autograd; restated here as the explicit vector-Jacobian product)
+# ------------------------------------------------------------------------------------------
+
+def surrogate_params_from_npz(z, prefix=""):
+    """[(W, b)] of nn.Sequential(Linear, ReLU, Linear, ReLU, Linear, ReLU, Linear): keys 0, 2, 4, 6."""
+    return [(np.asarray(z[f"{prefix}{i}_weight"]), np.asarray(z[f"{prefix}{i}_bias"])) for i in (0, 2, 4, 6)]
+
+
+def surrogate_forward(params, x, keep=False):
+    """forward_model(x) in float64 (Linear -> ReLU x3 -> Linear)."""
+    h = np.asarray(x, np.float64)
+    pre = []
+    for i, (W, b) in enumerate(params):
+        z = h @ np.asarray(W, np.float64).T + np.asarray(b, np.float64)
+        if i < len(params) - 1:
+            pre.append(z)
+            h = np.maximum(z, 0.0)
+        else:
+            h = z
+    return (h, pre) if keep else h
+
+
+def scat_log_posterior(params, x, y, a=0.2, b=0.01, lambd_bd=1000.0, grad=False):
+    """Negative log posterior get_log_posterior (utils_scatterometry.py:30-38):
+    E = 0.5 sum log((a f)^2 + b^2) + 0.5 sum (y - f)^2 / ((a f)^2 + b^2) + lambd_bd sum relu(x-1) + relu(-1-x).
+    grad=True also returns dE/dx (energy_grad, models/SNF.py:234-237): the reverse pass through the
+    surrogate with v = dE/df = a^2 f / pref - (y - f) / pref - a^2 f (y - f)^2 / pref^2, plus the
+    boundary term lambd_bd ([x > 1] - [x < -1]) (torch's relu gradient is 0 at 0)."""
+    x = np.asarray(x, np.float64)
+    y = np.broadcast_to(np.asarray(y, np.float64), (x.shape[0], np.shape(y)[-1]))
+    f, pre = surrogate_forward(params, x, keep=True)
+    pref = (a * f) ** 2 + b ** 2
+    res = y - f
+    e = 0.5 * np.log(pref).sum(1) + 0.5 * (res ** 2 / pref).sum(1) + lambd_bd * (
+        np.maximum(x - 1, 0) + np.maximum(-1 - x, 0)).sum(1)
+    if not grad:
+        return e
+    v = a * a * f / pref - res / pref - a * a * f * res ** 2 / pref ** 2
+    for i in range(len(params) - 1, -1, -1):
+        W = np.asarray(params[i][0], np.float64)
+        v = v @ W
+        if i > 0:
+            v = v * (pre[i - 1] > 0)
+    g = v + lambd_bd * ((x > 1).astype(np.float64) - (x < -1).astype(np.float64))
+    return e, g
+
+
+# ------------------------------------------------------------------------------------------
+# F3  random-walk Metropolis-Hastings ground truth -- models/SNF.py:250-275 (anneal_to_energy,
+#     langevin_prop=False) as generate_scatterometry_ground_truth.py:26-28 drives it
+# ------------------------------------------------------------------------------------------
+
+def mh_sample(params, y, num_steps, noise_std, a=0.2, b=0.01, lambd_bd=1000.0, x0=None, noise=None, unif=None,
+              seed=None, n_chains=None, chain_offset=0, stream=0):
+    """x_prop = x + noise_std * xi; accept iff u < exp(-E(x_prop) + E(x)). Returns (x, E(x) - E(x0)).
+    Draws: injected (x0 (n,3), noise (S,n,3), unif (S,n)) -- the reference's captured torch draws --
+    or the product RNG keyed (seed, chain_offset + c, stream): x0 from three words
+    ((w >> 8) 2^-24 * 2 - 1, float32) unless given, then per step rng_normals(3) (4 words) and one
+    word for u = (w >> 8) 2^-24."""
+    s = None
+    if noise is None:
+        s = rng_init(seed, np.arange(chain_offset, chain_offset + n_chains), stream)
+    if x0 is None:
+        inv = F32(2.0 ** -24)
+        x0 = np.stack([((rng_next(s) >> np.uint32(8)).astype(F32) * inv * F32(2.0) - F32(1.0)).astype(F32)
+                       for _ in range(3)], 1)
+    x = np.asarray(x0, F32).copy()
+    e_cur = scat_log_posterior(params, x, y, a, b, lambd_bd)
+    e0 = e_cur.copy()
+    for i in range(num_steps):
+        if noise is None:
+            xi = rng_normals(s, 3)
+            u = ((rng_next(s) >> np.uint32(8)).astype(F32) * F32(2.0 ** -24)).astype(F32)
+        else:
+            xi, u = np.asarray(noise[i], F32), np.asarray(unif[i], F32)
+        xp = (x + (F32(noise_std) * xi).astype(F32)).astype(F32)
+        e_prop = scat_log_posterior(params, xp, y, a, b, lambd_bd)
+        acc = u < np.exp(-e_prop + e_cur)
+        x = np.where(acc[:, None], xp, x)
+        e_cur = np.where(acc, e_prop, e_cur)
+    return x, e_cur - e0

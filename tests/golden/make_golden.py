@@ -18,6 +18,9 @@ Fixtures (SURVEY.md §8c "Golden fixtures"):
   G5 pinn_linear.npz       PINNLoss / DSM_PDELoss / DSMLoss components and parameter grads
   G6 data_*.npz            y_test / x_test of both problems
   G7 surrogate.npz         scatterometry surrogate weights (fp32)
+  G8 surrogate_io.npz      surrogate forward, get_log_posterior and its autograd input gradient
+                           (energy_grad) on 256 seeded rows; anneal_to_energy (random-walk MH) with
+                           its captured draws (64 chains x 50 steps) and a 4000-chain x 1000-step run
 
 Usage:  python tests/golden/make_golden.py [--what all|schedule|mlp|data|train|traj|samples|pinn]
 """
@@ -50,12 +53,22 @@ def import_reference():
 
     u.sample_v = u.log_normal = u.sample_vp_truncated_q = _missing
     sys.modules.setdefault("include.sdeflow_light.lib.utils", u)
+    # FrEIA (the SNF/INN baselines' flow library) is not installed; models/SNF.py imports five of its
+    # names at module level but anneal_to_energy / energy_grad (models/SNF.py:234-275) use torch only
+    fr = types.ModuleType("FrEIA")
+    frf = types.ModuleType("FrEIA.framework")
+    for nm in ("InputNode", "OutputNode", "Node", "ReversibleGraphNet", "ConditionNode"):
+        setattr(frf, nm, object)
+    frm = types.ModuleType("FrEIA.modules")
+    frm.GLOWCouplingBlock = object
+    for nm, mod in (("FrEIA", fr), ("FrEIA.framework", frf), ("FrEIA.modules", frm)):
+        sys.modules.setdefault(nm, mod)
     import torch  # noqa: F401
     import nets, sdes, losses, linear_problem, utils_scatterometry, datasets  # noqa: E401
-    from models import diffusion
+    from models import diffusion, SNF
     return types.SimpleNamespace(nets=nets, sdes=sdes, losses=losses, diffusion=diffusion,
                                  linear_problem=linear_problem, scat=utils_scatterometry,
-                                 datasets=datasets)
+                                 datasets=datasets, snf=SNF)
 
 
 def state_to_npz_dict(sd, prefix=""):
@@ -298,6 +311,62 @@ def gen_pinn(R):
     np.savez(os.path.join(OUT, "pinn_linear.npz"), **out)
 
 
+# ----------------------------------------------------------------------------------------- G8
+def gen_surrogate(R):
+    import torch
+    torch.set_num_threads(os.cpu_count())
+    fm, prm = R.scat.load_forward_model(os.path.join(REF, "trained_models/scatterometry"))
+    a, b, lam = prm["a"], prm["b"], prm["lambd_bd"]
+    z = np.load(os.path.join(OUT, "data_scat.npz"))
+    ys = torch.from_numpy(z["y_test"])
+    g = torch.Generator().manual_seed(8)
+    n = 256
+    # mostly inside the prior box, some outside (boundary penalty and its gradient)
+    x = (torch.rand(n, 3, generator=g) * 2.2 - 1.1)
+    y = ys[torch.arange(n) % ys.shape[0]]
+    out = {"x": x.numpy(), "y": y.numpy(), "a": a, "b": b, "lambd_bd": lam}
+    with torch.no_grad():
+        out["f"] = fm(x).numpy()
+    # energy_grad (models/SNF.py:234-237) on get_log_posterior (utils_scatterometry.py:30-38)
+    energy = lambda v: R.scat.get_log_posterior(v, fm, a, b, y, lam)
+    grad, e = R.snf.energy_grad(x.clone(), energy)
+    out["energy"] = e.detach().numpy()
+    out["grad"] = grad.detach().numpy()
+    # anneal_to_energy with captured draws: generate_gt_samples draws x0 = rand*2-1, then every MH
+    # step draws randn_like(x) (the proposal) and rand_like(e_diff) (the acceptance uniform)
+    y0 = ys[0]
+    for tag, (nc, S, ns) in {"mh": (64, 50, 0.5)}.items():
+        inflated = y0[None, :].repeat(nc, 1)
+        en = lambda v: R.scat.get_log_posterior(v, fm, a, b, inflated, lam)
+        torch.manual_seed(31)
+        x0 = torch.rand(nc, 3) * 2 - 1
+        xi, u = [], []
+        for _ in range(S):
+            xi.append(torch.randn(nc, 3))
+            u.append(torch.rand(nc))
+        torch.manual_seed(31)
+        x0b = torch.rand(nc, 3) * 2 - 1
+        assert torch.equal(x0, x0b)
+        xs, ediff = R.snf.anneal_to_energy(x0b, en, S, noise_std=ns)
+        out.update({f"{tag}_y": y0.numpy(), f"{tag}_x0": x0.numpy(), f"{tag}_xi": torch.stack(xi).numpy(),
+                    f"{tag}_u": torch.stack(u).numpy(), f"{tag}_x": xs.detach().numpy(),
+                    f"{tag}_ediff": ediff.detach().numpy(), f"{tag}_noise_std": ns})
+    # a ground-truth-style run (generate_scatterometry_ground_truth.py:27 with METR_STEPS = 1000,
+    # NOISE_STD_MCMC = 0.5 of config_scatterometry.yml) for distributional parity
+    nc, S = 4000, 1000
+    inflated = y0[None, :].repeat(nc, 1)
+    en = lambda v: R.scat.get_log_posterior(v, fm, a, b, inflated, lam)
+    torch.manual_seed(2025)
+    t0 = time.time()
+    with torch.no_grad():
+        xs, _ = R.snf.anneal_to_energy(torch.rand(nc, 3) * 2 - 1, en, S, noise_std=0.5)
+    out["gt_samples"] = xs.numpy()
+    out["gt_steps"] = S
+    out["gt_seconds"] = time.time() - t0
+    print("MH", nc, "x", S, "in", out["gt_seconds"], "s")
+    np.savez(os.path.join(OUT, "surrogate_io.npz"), **out)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--what", default="all")
@@ -322,6 +391,8 @@ def main():
         gen_pinn(R)
     if w in ("all", "samples"):
         gen_samples(R)
+    if w in ("all", "surrogate"):
+        gen_surrogate(R)
 
 
 if __name__ == "__main__":

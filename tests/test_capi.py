@@ -32,7 +32,7 @@ def test_exports_every_declared_symbol(lib, dmip):
 
 
 def test_abi_version(lib, dmip):
-    assert lib.dmip_abi_version() == dmip._lib.ABI_VERSION == 3
+    assert lib.dmip_abi_version() == dmip._lib.ABI_VERSION == 4
 
 
 def test_supported_shapes(lib, dmip):
@@ -103,3 +103,19 @@ def test_fused_config_acceptance(dmip):
     # CPU parameters -> autograd path
     m.sde.a.to("cpu")
     assert tr.fused_config(m, dmip.DSMLoss()) is None
+
+
+def test_surrogate_entry_points_reject_bad_arguments(lib, dmip):
+    L = dmip._lib
+    out = ctypes.c_void_p()
+    null = (ctypes.c_void_p * 4)()
+    w = (ctypes.c_int * 3)(256, 256, 256)
+    assert lib.dmip_surrogate_create(3, 23, 3, w, null, null, ctypes.byref(out)) == L.DMIP_ERR_INVALID
+    w128 = (ctypes.c_int * 3)(128, 128, 128)
+    assert lib.dmip_surrogate_create(3, 23, 3, w128, null, null, ctypes.byref(out)) == L.DMIP_ERR_UNSUPPORTED
+    assert lib.dmip_surrogate_create(2, 23, 3, w, null, null, ctypes.byref(out)) == L.DMIP_ERR_UNSUPPORTED
+    nz = L.scat_noise(0.2, 0.01, 1000)
+    assert lib.dmip_surrogate_forward(None, None, 4, None, None) == L.DMIP_ERR_INVALID
+    assert lib.dmip_log_posterior(None, ctypes.byref(nz), None, None, 0, 4, None, None, None) == L.DMIP_ERR_INVALID
+    assert lib.dmip_mh_sample(None, ctypes.byref(nz), None, 1, 10, 0, 5, 0.5, 1, None, None, None, None, None,
+                              None) == L.DMIP_ERR_INVALID

@@ -148,3 +148,30 @@ def test_loss_grad_jets_match_reference_autograd(golden, name):
     if name == "dsmpde":
         np.testing.assert_allclose(comps["div"], z["fpe_div"], rtol=1e-4, atol=1e-4)
         np.testing.assert_allclose(comps["pde_rows"].reshape(-1, 1), z["fpe_rows"], rtol=1e-3, atol=1e-4)
+
+
+# ---------------------------------------------------------------- F2 / F3 scatterometry surrogate
+def test_surrogate_oracle_matches_reference(golden):
+    """surrogate forward, get_log_posterior and its autograd gradient (energy_grad) of the reference
+    (fixture G8, 256 rows incl. points outside the prior box) against the float64 restatement."""
+    z = golden("surrogate_io.npz")
+    params = O.surrogate_params_from_npz(golden("surrogate.npz"))
+    f = O.surrogate_forward(params, z["x"])
+    assert np.abs(f - z["f"]).max() <= 2e-6 * np.abs(z["f"]).max()
+    e, g = O.scat_log_posterior(params, z["x"], z["y"], float(z["a"]), float(z["b"]), float(z["lambd_bd"]), grad=True)
+    np.testing.assert_allclose(e, z["energy"], rtol=1e-5, atol=1e-4)
+    assert np.abs(g - z["grad"]).max() <= 1e-5 * np.abs(z["grad"]).max()
+    assert (np.abs(z["x"]) > 1).any()  # the boundary penalty is exercised
+
+
+def test_mh_oracle_replays_reference_trajectories(golden):
+    """anneal_to_energy fed its own captured draws: every chain takes the reference's path."""
+    z = golden("surrogate_io.npz")
+    params = O.surrogate_params_from_npz(golden("surrogate.npz"))
+    S = z["mh_xi"].shape[0]
+    x, ed = O.mh_sample(params, z["mh_y"], S, float(z["mh_noise_std"]), x0=z["mh_x0"], noise=z["mh_xi"],
+                        unif=z["mh_u"])
+    assert np.array_equal(x, z["mh_x"])
+    np.testing.assert_allclose(ed, z["mh_ediff"], rtol=1e-4, atol=1e-3)
+    # some proposals were accepted and some rejected
+    assert 0 < np.mean(np.any(x != z["mh_x0"], axis=1)) <= 1
