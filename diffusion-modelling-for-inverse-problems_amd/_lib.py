@@ -31,8 +31,9 @@ EXPORTED = (
     "dmip_rng_normals", "dmip_schedule", "dmip_last_error", "dmip_abi_version", "dmip_sampler_supported",
     "dmip_em_sample_stamps", "dmip_em_sample_posterior", "dmip_em_sample_cdiffe", "dmip_loss_grad",
     "dmip_loss_grad_supported", "dmip_histogram", "dmip_surrogate_create", "dmip_surrogate_destroy",
-    "dmip_surrogate_forward", "dmip_log_posterior", "dmip_mh_sample",
+    "dmip_surrogate_forward", "dmip_log_posterior", "dmip_mh_sample", "dmip_dps_sample",
 )
+DMIP_DPS_NLL, DMIP_DPS_NORM = 0, 1
 
 
 class DmipVpsde(ctypes.Structure):
@@ -97,7 +98,10 @@ def _declare(lib):
                                        _c_void_p, _c_void_p, _c_void_p]
     lib.dmip_mh_sample.argtypes = [_c_void_p, ctypes.POINTER(DmipScatNoise), _c_void_p, _i32, _i64, _i64, _i32, _f32,
                                    _u64, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p]
-    for name in ("dmip_mlp_create", "dmip_mlp_destroy", "dmip_mlp_forward", "dmip_em_sample",
+    lib.dmip_dps_sample.argtypes = [_c_void_p, _c_void_p, ctypes.POINTER(DmipScatNoise), ctypes.POINTER(DmipVpsde),
+                                    _c_void_p, _i32, _i64, _i64, _i32, _f32, _f32, _u64, _i32, _f32, _c_void_p,
+                                    _c_void_p]
+    for name in ("dmip_dps_sample", "dmip_mlp_create", "dmip_mlp_destroy", "dmip_mlp_forward", "dmip_em_sample",
                  "dmip_rng_words", "dmip_rng_normals", "dmip_schedule", "dmip_sampler_supported",
                  "dmip_em_sample_stamps", "dmip_em_sample_posterior", "dmip_em_sample_cdiffe",
                  "dmip_loss_grad", "dmip_loss_grad_supported", "dmip_histogram", "dmip_surrogate_create",
@@ -292,3 +296,11 @@ def mh_sample(handle, noise, y, n_chains, chain_offset, num_steps, noise_std, se
                                int(chain_offset), int(num_steps), float(noise_std),
                                ctypes.c_uint64(int(seed) & 0xFFFFFFFFFFFFFFFF), ptr(x_init), ptr(inj_noise),
                                ptr(inj_unif), ptr(x_out), ptr(e_out), stream_of(y.device)))
+
+
+def dps_sample(prior, surrogate, noise, sde, y, n_chains, chain_offset, num_steps, mean, std, seed, mode, zeta, out):
+    calls["dps_sample"] = calls.get("dps_sample", 0) + 1
+    check(lib().dmip_dps_sample(prior.h, surrogate.h, ctypes.byref(noise), ctypes.byref(sde), ptr(y), int(y.shape[0]),
+                                int(n_chains), int(chain_offset), int(num_steps), float(mean), float(std),
+                                ctypes.c_uint64(int(seed) & 0xFFFFFFFFFFFFFFFF), int(mode), float(zeta), ptr(out),
+                                stream_of(y.device)))

@@ -52,6 +52,22 @@ float bf2f(uint16_t b) {
   return f;
 }
 
+// f32 A-fragment images for v_mfma_f32_16x16x4_f32 (dmip_surrogate.hip): k-step (q, r) of output
+// tile o, lane l = i + 16 g, holds M[16 o + i][16 q + 4 g + r]; stored [o][q][lane][r] (one float4
+// per lane per q). M(row, col) returns 0 outside the matrix.
+template <typename F>
+std::vector<char> pack_f32_tiles(int n_tiles, int n_q, F M) {
+  std::vector<float> v((size_t)n_tiles * n_q * 64 * 4);
+  for (int o = 0; o < n_tiles; ++o)
+    for (int q = 0; q < n_q; ++q)
+      for (int l = 0; l < 64; ++l)
+        for (int r = 0; r < 4; ++r)
+          v[(((size_t)o * n_q + q) * 64 + l) * 4 + r] = M(16 * o + (l & 15), 16 * q + 4 * (l >> 4) + r);
+  std::vector<char> b(v.size() * 4);
+  std::memcpy(b.data(), v.data(), b.size());
+  return b;
+}
+
 inline int kperm(int s, int h, int j) { return 32 * (s >> 1) + 16 * (s & 1) + 8 * (j >> 2) + 4 * h + (j & 3); }
 inline int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 inline int k1s_for(int n_slots) { return (n_slots + 15) / 16; }
@@ -81,9 +97,16 @@ struct dmip_mlp {
   char* a1_full = nullptr;        // [W/32][k1s_full] KiB (every input column varying)
   float* w1 = nullptr;            // layer-1 fp32 [W][in_dim] (per-y prep of the sampler's A1)
   float* b1 = nullptr;
+  // exact-f32 images of a DPS prior (MLP2 (x, t), x 3, widths [256]*3): dmip_dps_sample
+  float* dps_l1 = nullptr;        // [16 tiles][2 k-steps][64]
+  char* dps_w2 = nullptr;         // [16][16][64][4]
+  char* dps_w3 = nullptr;
+  char* dps_w4 = nullptr;         // [1][16][64][4], rows >= 3 zero
+  float* dps_bias = nullptr;      // b2 | b3 | b4[16]
   ~dmip_mlp() {
     for (void* p : {(void*)hidden, (void*)ao_samp, (void*)ao_full, (void*)bias_hidden, (void*)bias_out_samp,
-                    (void*)bias_out_full, (void*)a1_full, (void*)w1, (void*)b1})
+                    (void*)bias_out_full, (void*)a1_full, (void*)w1, (void*)b1, (void*)dps_l1, (void*)dps_w2,
+                    (void*)dps_w3, (void*)dps_w4, (void*)dps_bias})
       if (p) (void)hipFree(p);
   }
 };
@@ -229,6 +252,27 @@ int dmip_mlp_create(int in_dim, int out_dim, int n_hidden, const int* widths, in
   }
 
   int rc = DMIP_OK;
+  if (input_layout == DMIP_INPUT_X_T && xdim == 3 && in_dim == 4 && out_dim == 3 && L == 3 && W == dmip::kDpsPriorW) {
+    // exact-f32 images for the DPS sampler's prior (dmip_surrogate.hip dps_kernel)
+    const float *P1 = weights[0], *P2 = weights[1], *P3 = weights[2], *P4 = weights[3];
+    std::vector<float> l1((size_t)16 * 2 * 64), pb((size_t)2 * W + 16, 0.0f);
+    for (int o = 0; o < 16; ++o)
+      for (int l = 0; l < 64; ++l) {
+        const int row = 16 * o + (l & 15), g = l >> 4;
+        l1[((size_t)o * 2 + 0) * 64 + l] = P1[(size_t)row * 4 + g];
+        l1[((size_t)o * 2 + 1) * 64 + l] = g == 0 ? biases[0][row] : 0.0f;
+      }
+    for (int k = 0; k < W; ++k) pb[k] = biases[1][k], pb[W + k] = biases[2][k];
+    for (int k = 0; k < 3; ++k) pb[2 * W + k] = biases[3][k];
+    const auto sqm = [W](const float* Wm) { return [Wm, W](int r, int c) { return Wm[(size_t)r * W + c]; }; };
+    if ((rc = upload(&net->dps_l1, l1)) || (rc = upload(&net->dps_bias, pb)) ||
+        (rc = upload(&net->dps_w2, pack_f32_tiles(16, 16, sqm(P2)))) ||
+        (rc = upload(&net->dps_w3, pack_f32_tiles(16, 16, sqm(P3)))) ||
+        (rc = upload(&net->dps_w4, pack_f32_tiles(1, 16, [&](int r, int c) { return r < 3 ? P4[(size_t)r * W + c] : 0.0f; })))) {
+      delete net;
+      return rc;
+    }
+  }
   std::vector<char> hid_b(hid.size() * 2), ao_sb(ao_s.size() * 2), ao_fb(ao_f.size() * 2), a1f_b(a1f.size() * 2);
   std::memcpy(hid_b.data(), hid.data(), hid_b.size());
   std::memcpy(ao_sb.data(), ao_s.data(), ao_sb.size());
@@ -528,9 +572,6 @@ int dmip_histogram(const float* x_dev, int64_t n, int d, int nbins, double lo, d
 }  // extern "C"
 
 // ------------------------------------------------------------------- scatterometry surrogate
-// f32 A-fragment images for v_mfma_f32_16x16x4_f32 (dmip_surrogate.hip): k-step (q, r) of output
-// tile o, lane l = i + 16 g, holds M[16 o + i][16 q + 4 g + r]; stored [o][q][lane][r] (one float4
-// per lane per q). M(row, col) returns 0 outside the matrix.
 struct dmip_surrogate {
   float* l1 = nullptr;
   float* bias = nullptr;
@@ -544,19 +585,6 @@ struct dmip_surrogate {
 };
 
 namespace {
-
-template <typename F>
-std::vector<char> pack_f32_tiles(int n_tiles, int n_q, F M) {
-  std::vector<float> v((size_t)n_tiles * n_q * 64 * 4);
-  for (int o = 0; o < n_tiles; ++o)
-    for (int q = 0; q < n_q; ++q)
-      for (int l = 0; l < 64; ++l)
-        for (int r = 0; r < 4; ++r)
-          v[(((size_t)o * n_q + q) * 64 + l) * 4 + r] = M(16 * o + (l & 15), 16 * q + 4 * (l >> 4) + r);
-  std::vector<char> b(v.size() * 4);
-  std::memcpy(b.data(), v.data(), b.size());
-  return b;
-}
 
 int surrogate_check(const dmip_surrogate* s, int64_t n) {
   if (!s) return fail(DMIP_ERR_INVALID, "null surrogate handle");
@@ -721,6 +749,49 @@ int dmip_mh_sample(const dmip_surrogate* s, const dmip_scat_noise* noise, const 
   p.e_out = e_out_dev;
   hipError_t e = dmip::launch_mh(p, n_y, (hipStream_t)stream);
   return e == hipSuccess ? DMIP_OK : hip_fail(e, "mh_sample launch");
+}
+
+int dmip_dps_sample(const dmip_mlp* prior, const dmip_surrogate* fwd, const dmip_scat_noise* noise,
+                    const dmip_vpsde* sde, const float* y_dev, int n_y, int64_t n_chains, int64_t chain_offset,
+                    int num_steps, float mean, float stdv, uint64_t seed, int mode, float zeta, float* x_out_dev,
+                    void* stream) {
+  if (!prior || !fwd || !sde || !y_dev || !x_out_dev) return fail(DMIP_ERR_INVALID, "null argument");
+  if (mode != DMIP_DPS_NLL && mode != DMIP_DPS_NORM) return fail(DMIP_ERR_INVALID, "unknown DPS guidance mode");
+  dmip::DpsParams p{};
+  if (mode == DMIP_DPS_NLL) {
+    if (int rc = noise_check(noise, p.s)) return rc;
+  }
+  if (!prior->dps_l1)
+    return fail(DMIP_ERR_UNSUPPORTED, "DPS prior must be an x,t network (MLP2) with xdim 3 and hidden layers [256]*3");
+  if (n_y < 1 || n_y > 65535) return fail(DMIP_ERR_INVALID, "n_y must be in [1, 65535]");
+  if (n_chains < 0 || chain_offset < 0) return fail(DMIP_ERR_INVALID, "negative chain count/offset");
+  if (num_steps < 1) return fail(DMIP_ERR_INVALID, "num_steps must be >= 1");
+  if (!(sde->T > 0.0)) return fail(DMIP_ERR_INVALID, "T must be > 0");
+  if (!(zeta >= 0.0f)) return fail(DMIP_ERR_INVALID, "zeta must be >= 0");
+  if (n_chains == 0) return DMIP_OK;
+  surrogate_params(fwd, p.s);
+  p.mode = mode;
+  p.s.y = y_dev;
+  p.s.n_chains = n_chains;
+  p.s.chain_offset = chain_offset;
+  p.s.num_steps = num_steps;
+  p.s.seed = seed;
+  p.s.x_out = x_out_dev;
+  p.pl1 = prior->dps_l1;
+  p.pw2 = prior->dps_w2;
+  p.pw3 = prior->dps_w3;
+  p.pw4 = prior->dps_w4;
+  p.pbias = prior->dps_bias;
+  p.T = (float)sde->T;
+  p.bmin = (float)sde->beta_min;
+  p.bdiff = (float)(sde->beta_max - sde->beta_min);
+  p.delta = (float)(sde->T / (double)num_steps);
+  p.sqrt_delta = (float)std::sqrt(sde->T / (double)num_steps);
+  p.mean = mean;
+  p.stdv = stdv;
+  p.zeta = zeta;
+  hipError_t e = dmip::launch_dps(p, n_y, (hipStream_t)stream);
+  return e == hipSuccess ? DMIP_OK : hip_fail(e, "dps_sample launch");
 }
 
 int dmip_rng_words(uint64_t seed, int64_t chain_offset, uint64_t stream_id, int64_t n_chains, int n_words,

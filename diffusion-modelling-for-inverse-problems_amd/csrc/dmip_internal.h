@@ -117,6 +117,23 @@ struct SurrogateParams {
   float* x_out;        // [n_y][n_chains][3]
 };
 
+// DPS sampler (config 4): the prior score network MLP2 (x, t) -> x in exact f32 with forward-mode
+// Jacobian, the surrogate residual gradient, the EM predictor (dmip_surrogate.hip dps_kernel).
+constexpr int kDpsPriorW = 256;
+
+struct DpsParams {
+  SurrogateParams s;   // surrogate images (forward + reverse) and y_obs in s.y ([n_y][23])
+  const float* pl1;    // prior layer 1 [16 tiles][2 k-steps][64]: (W1 x-cols | t-col), (b1, 0, 0, 0)
+  const char* pw2;     // prior 256 x 256 images [16][16][64][4]
+  const char* pw3;
+  const char* pw4;     // prior output [1 tile][16][64][4] (rows >= 3 zero)
+  const float* pbias;  // b2 | b3 [256] | b4 [16]
+  float T, bmin, bdiff, delta, sqrt_delta, mean, stdv, zeta;
+  int mode;            // 0: NLL guidance (zeta grad log p(y|x0) in the score), 1: Chung residual-norm step
+};
+
+hipError_t launch_dps(const DpsParams& p, int n_y, hipStream_t st);
+
 hipError_t launch_surrogate_eval(const SurrogateParams& p, int mode, int n_wg, hipStream_t st);
 int surrogate_rows_per_wg();
 hipError_t launch_mh(const SurrogateParams& p, int n_y, hipStream_t st);

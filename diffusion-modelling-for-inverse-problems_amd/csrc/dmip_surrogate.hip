@@ -24,6 +24,8 @@
 #include "dmip_device.h"
 #include "dmip_internal.h"
 
+#include <type_traits>
+
 namespace dmip {
 namespace sg {
 
@@ -49,13 +51,27 @@ constexpr int W4T_OFF = Y_OFF + 32 * 4;
 constexpr int W4T_BYTES = ST * 2 * 64 * 16;
 constexpr int W1T_OFF = W4T_OFF + W4T_BYTES;
 constexpr int W1T_BYTES = KG * 64 * 16;
-template <bool GRAD>
-struct LayoutS {
-  static constexpr int RING_OFF = GRAD ? W1T_OFF + W1T_BYTES : W4T_OFF;
-  static constexpr int TOTAL = RING_OFF + R * CHUNK;
-  static constexpr int NCT = GRAD ? NCF + NCB : NCF;
+// chunk streams (cycled once per evaluation / step): a Plan maps a chunk index of the cycle to the
+// global address of that 16 KiB chunk (wave-uniform; the pointers are kernel arguments in SGPRs)
+struct PlanFwd {  // W2 (16 tiles), W3 (16), W4 (2)
+  const char *w2, *w3, *w4;
+  static constexpr int N = NCF;
+  __device__ __forceinline__ const char* src(int c) const {
+    return c < ST ? w2 + (size_t)c * CHUNK : (c < 2 * ST ? w3 + (size_t)(c - ST) * CHUNK : w4 + (size_t)(c - 2 * ST) * CHUNK);
+  }
 };
-static_assert(LayoutS<true>::TOTAL <= 160 * 1024, "LDS budget");
+struct PlanGrad {  // + W3^T (16), W2^T (16)
+  PlanFwd f;
+  const char *w3t, *w2t;
+  static constexpr int N = NCF + NCB;
+  __device__ __forceinline__ const char* src(int c) const {
+    if (c < NCF) return f.src(c);
+    return c < NCF + ST ? w3t + (size_t)(c - NCF) * CHUNK : w2t + (size_t)(c - NCF - ST) * CHUNK;
+  }
+};
+constexpr int RING_OFF_FWD = W4T_OFF;
+constexpr int RING_OFF_GRAD = W1T_OFF + W1T_BYTES;
+static_assert(RING_OFF_GRAD + R * CHUNK <= 160 * 1024, "LDS budget");
 static_assert(W4T_OFF % 16 == 0 && L1_BYTES % 16 == 0, "LDS-DMA alignment");
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, const f32x4& c) {
@@ -64,25 +80,16 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, const f32x4& c) {
 
 __device__ __forceinline__ float shfl_xor(float v, int m) { return __shfl_xor(v, m, 64); }
 
-template <bool GRAD>
+template <bool GRAD, int RING_OFF, typename Plan>
 struct Engine {
-  using LS = LayoutS<GRAD>;
   char* lds;
-  const char* src[5];  // streamed images in chunk order: W2, W3, W4, W3^T, W2^T
+  Plan plan;
   long long gc;
   int w, lane, g;
 
-  __device__ __forceinline__ const char* chunk_src(int c) const {
-    if (c < ST) return src[0] + (size_t)c * CHUNK;
-    if (c < 2 * ST) return src[1] + (size_t)(c - ST) * CHUNK;
-    if (c < NCF) return src[2] + (size_t)(c - 2 * ST) * CHUNK;
-    if (c < NCF + ST) return src[3] + (size_t)(c - NCF) * CHUNK;
-    return src[4] + (size_t)(c - NCF - ST) * CHUNK;
-  }
-
   __device__ __forceinline__ void ring_issue(long long gi) {
-    const char* base = chunk_src((int)(gi % LS::NCT));
-    char* dst = lds + LS::RING_OFF + (int)(gi % R) * CHUNK;
+    const char* base = plan.src((int)(gi % Plan::N));
+    char* dst = lds + RING_OFF + (int)(gi % R) * CHUNK;
 #pragma unroll
     for (int q = 0; q < PPW; ++q) {
       const int piece = w * PPW + q;
@@ -98,18 +105,21 @@ struct Engine {
     wait_vmcnt<(R - 2) * PPW>();
     lds_barrier();
     ring_issue(gc + R - 1);
-    const char* slot = lds + LS::RING_OFF + (int)(gc % R) * CHUNK;
+    const char* slot = lds + RING_OFF + (int)(gc % R) * CHUNK;
     ++gc;
     return slot;
   }
 
-  __device__ __forceinline__ void prologue(const SurrogateParams& p) {
+  // stage the resident parts (plus `extra` (dst, src, bytes) blocks of the caller), then start the ring
+  __device__ __forceinline__ void prologue(const SurrogateParams& p, int n_extra = 0, char* const* xdst = nullptr,
+                                           const char* const* xsrc = nullptr, const int* xbytes = nullptr) {
     const int tid = threadIdx.x;
     stage_lds(lds + L1_OFF, (const char*)p.l1, L1_BYTES);
     if constexpr (GRAD) {
       stage_lds(lds + W4T_OFF, p.w4t, W4T_BYTES);
       stage_lds(lds + W1T_OFF, p.w1t, W1T_BYTES);
     }
+    for (int k = 0; k < n_extra; ++k) stage_lds(xdst[k], xsrc[k], xbytes[k]);
     float* bl = (float*)(lds + BIAS_OFF);
     for (int i = tid; i < BIAS_FLOATS; i += NW * 64) bl[i] = p.bias[i];
     wait_vmcnt<0>();
@@ -279,17 +289,24 @@ __device__ __forceinline__ float boundary_grad(float xd, float lam) {
   return (xd > 1.0f ? lam : 0.0f) - (xd < -1.0f ? lam : 0.0f);
 }
 
+template <typename Plan>
+__device__ __forceinline__ Plan make_plan(const SurrogateParams& p) {
+  if constexpr (std::is_same<Plan, PlanFwd>::value) return PlanFwd{p.w2, p.w3, p.w4};
+  else return PlanGrad{PlanFwd{p.w2, p.w3, p.w4}, p.w3t, p.w2t};
+}
+
 // ------------------------------------------------------------------------- evaluation kernel
 // MODE 0: f = F(x); 1: E(x, y); 2: E and dE/dx. Rows strided over the grid, 16 per wave.
 template <int MODE>
 __global__ void __launch_bounds__(NW * 64, 1) surrogate_eval_kernel(SurrogateParams p) {
   constexpr bool GRAD = MODE == 2;
-  using LS = LayoutS<GRAD>;
-  __shared__ __attribute__((aligned(16))) char lds[LS::TOTAL];
+  constexpr int RING_OFF = GRAD ? RING_OFF_GRAD : RING_OFF_FWD;
+  __shared__ __attribute__((aligned(16))) char lds[RING_OFF + R * CHUNK];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4;
-  Engine<GRAD> eng{lds, {p.w2, p.w3, p.w4, p.w3t, p.w2t}, 0, w, lane, g};
+  using Plan = typename std::conditional<GRAD, PlanGrad, PlanFwd>::type;
+  Engine<GRAD, RING_OFF, Plan> eng{lds, make_plan<Plan>(p), 0, w, lane, g};
   eng.prologue(p);
   const long long n_tiles = (p.n + 15) / 16;
   const long long per_round = (long long)gridDim.x * NW;
@@ -342,8 +359,7 @@ __global__ void __launch_bounds__(NW * 64, 1) surrogate_eval_kernel(SurrogatePar
 // INJECT: xi [S][n_y][n][3] and u [S][n_y][n] replace the RNG (replaying captured draws).
 template <bool INJECT>
 __global__ void __launch_bounds__(NW * 64, 1) mh_kernel(SurrogateParams p) {
-  using LS = LayoutS<false>;
-  __shared__ __attribute__((aligned(16))) char lds[LS::TOTAL];
+  __shared__ __attribute__((aligned(16))) char lds[RING_OFF_FWD + R * CHUNK];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4;
@@ -351,7 +367,7 @@ __global__ void __launch_bounds__(NW * 64, 1) mh_kernel(SurrogateParams p) {
   const long long c_local = (long long)blockIdx.x * (NW * 16) + w * 16 + (lane & 15);
   const bool valid = c_local < p.n_chains;
   const long long cc = valid ? c_local : 0;
-  Engine<false> eng{lds, {p.w2, p.w3, p.w4, p.w3t, p.w2t}, 0, w, lane, g};
+  Engine<false, RING_OFF_FWD, PlanFwd> eng{lds, make_plan<PlanFwd>(p), 0, w, lane, g};
   float* ylds = (float*)(lds + Y_OFF);
   for (int i = threadIdx.x; i < 32; i += NW * 64) ylds[i] = i < YD ? p.y[(size_t)yi * YD + i] : 0.0f;
   eng.prologue(p);
@@ -402,6 +418,221 @@ __global__ void __launch_bounds__(NW * 64, 1) mh_kernel(SurrogateParams p) {
   }
 }
 
+
+// ---------------------------------------------------------------------------- DPS sampler
+// BASELINE config 4 (no reference code for sampling-time guidance): diffusion
+// posterior sampling (Chung et al. 2023) on the reference's EM predictor, with the Posterior
+// estimator's prior score network MLP2(x, t) (nets.py:37-57) and the scatterometry surrogate F as the
+// measurement operator. Per step (tau = T - t_i):
+//   s, J = prior(x, tau), ds/dx            (forward-mode Jacobian, 3 tangents)
+//   x0 = (x + var(tau) s) / mean_weight(tau)                      (Tweedie)
+//   G  = dL/dx = (I + var J^T) (dL/dx0) / mean_weight             (chain rule through x0(x))
+//   x <- EM(x, a = g s) - lambda G
+// with, by `mode`,
+//   NLL:  L = 0.5 sum log pref + 0.5 sum (y - F)^2 / pref (get_log_posterior's likelihood part,
+//         utils_scatterometry.py:33-35), lambda = zeta delta g^2 -- i.e. the score s + zeta grad log
+//         p(y | x0(x)), the target the reference's PosteriorLoss.likelihood_target (losses.py:349-371)
+//         trains its likelihood network on;
+//   NORM: L = ||y - F(x0)||^2, lambda = zeta / ||y - F(x0)|| (Chung et al. Alg. 1 step-size rule).
+// Everything runs in exact f32 on the f32 MFMA. The prior network's primal and its three tangents
+// share one 16-column B operand: column j = 4c + m is chain c of the pass (4 chains per pass, 4
+// passes per 16-chain wave) with m = 0 the primal and m = 1..3 the tangent along x_{m-1}; the
+// activation derivative of a tangent column is taken from its quad's primal lane (DPP broadcast).
+constexpr int PL1_OFF = RING_OFF_GRAD;                 // prior layer 1: [16][2][64] floats
+constexpr int PL1_BYTES = ST * 2 * 64 * 4;
+constexpr int PW4_OFF = PL1_OFF + PL1_BYTES;           // prior output tile, resident
+constexpr int PW4_BYTES = KG * 64 * 16;
+constexpr int PB_OFF = PW4_OFF + PW4_BYTES;            // prior b2 | b3 | b4[16]
+constexpr int PB_FLOATS = 2 * W + 16;
+constexpr int SJ_OFF = PB_OFF + PB_FLOATS * 4;         // per-wave s / J exchange [NW][16 chains][4][4]
+constexpr int SJ_BYTES = NW * 16 * 16 * 4;
+constexpr int RING_OFF_DPS = SJ_OFF + SJ_BYTES;
+static_assert(RING_OFF_DPS + R * CHUNK <= 160 * 1024, "DPS LDS budget");
+static_assert(PL1_OFF % 16 == 0 && PW4_OFF % 16 == 0 && SJ_OFF % 16 == 0 && RING_OFF_DPS % 16 == 0, "align");
+
+struct PlanDps {  // 4 prior passes x (W2p, W3p), then the surrogate forward + reverse stream
+  const char *pw2, *pw3;
+  PlanGrad s;
+  static constexpr int NP = 4 * 2 * ST;
+  static constexpr int N = NP + PlanGrad::N;
+  __device__ __forceinline__ const char* src(int c) const {
+    if (c < NP) {
+      const int k = c % (2 * ST);
+      return k < ST ? pw2 + (size_t)k * CHUNK : pw3 + (size_t)(k - ST) * CHUNK;
+    }
+    return s.src(c - NP);
+  }
+};
+
+__device__ __forceinline__ float quad_primal(float v) {  // value of lane 4*(l/4) (DPP quad_perm 0,0,0,0)
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x00, 0xF, 0xF, true));
+}
+
+__device__ __forceinline__ float tanh_f32(float z) {  // 1 - 2 / (e^{2z} + 1): a few ulp, saturates cleanly
+  return 1.0f - __fdividef(2.0f, __expf(2.0f * z) + 1.0f);
+}
+
+// activation of one prior tile: primal columns tanh (twice on layer 1, nets.py:21-26), tangent
+// columns act'(z_primal) * z
+template <bool TWICE>
+__device__ __forceinline__ void prior_act(const f32x4& z, int m, float (&H)[4]) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float zp = quad_primal(z[r]);
+    const float t1 = tanh_f32(zp);
+    float val, d;
+    if constexpr (TWICE) {
+      const float t2 = tanh_f32(t1);
+      val = t2;
+      d = (1.0f - t2 * t2) * (1.0f - t1 * t1);
+    } else {
+      val = t1;
+      d = 1.0f - t1 * t1;
+    }
+    H[r] = m == 0 ? val : d * z[r];
+  }
+}
+
+template <typename E>
+__device__ __forceinline__ f32x4 prior_bias4(const E& eng, int layer, int tile, int m) {
+  if (m != 0) return f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  return *(const f32x4*)((const float*)(eng.lds + PB_OFF) + layer * W + 16 * tile + 4 * eng.g);
+}
+
+// one prior pass: rows 4g + r of the output tile (s_i for m = 0, ds_i/dx_{m-1} otherwise) at g = 0
+template <typename E>
+__device__ __forceinline__ f32x4 prior_pass(E& eng, const float (&xin)[XD], float tau, int m) {
+  const int g = eng.g, lane = eng.lane;
+  float Ha[ST][4], Hb[ST][4];
+  const float b0 = m == 0 ? (g == 0 ? xin[0] : (g == 1 ? xin[1] : (g == 2 ? xin[2] : tau)))
+                          : (g == m - 1 ? 1.0f : 0.0f);
+  const float b1 = (m == 0 && g == 0) ? 1.0f : 0.0f;
+#pragma unroll
+  for (int o = 0; o < ST; ++o) {
+    const float a0 = ((const float*)(eng.lds + PL1_OFF))[(o * 2 + 0) * 64 + lane];
+    const float a1 = ((const float*)(eng.lds + PL1_OFF))[(o * 2 + 1) * 64 + lane];
+    const f32x4 z = mfma4(a1, b1, mfma4(a0, b0, f32x4{0.0f, 0.0f, 0.0f, 0.0f}));
+    prior_act<true>(z, m, Ha[o]);
+  }
+#pragma unroll
+  for (int o = 0; o < ST; ++o) {
+    const char* ch = eng.chunk_sync();
+    prior_act<false>(E::tile_product(ch, lane, Ha, prior_bias4(eng, 0, o, m)), m, Hb[o]);
+  }
+#pragma unroll
+  for (int o = 0; o < ST; ++o) {
+    const char* ch = eng.chunk_sync();
+    prior_act<false>(E::tile_product(ch, lane, Hb, prior_bias4(eng, 1, o, m)), m, Ha[o]);
+  }
+  asm volatile("" ::: "memory");
+  return E::tile_product(eng.lds + PW4_OFF, lane, Ha, prior_bias4(eng, 2, 0, m));
+}
+
+__global__ void __launch_bounds__(NW * 64, 1) dps_kernel(DpsParams p) {
+  __shared__ __attribute__((aligned(16))) char lds[RING_OFF_DPS + R * CHUNK];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, j = lane & 15;
+  const int yi = blockIdx.y;
+  const long long c_local = (long long)blockIdx.x * (NW * 16) + w * 16 + j;
+  const bool valid = c_local < p.s.n_chains;
+  Engine<true, RING_OFF_DPS, PlanDps> eng{
+      lds, PlanDps{p.pw2, p.pw3, make_plan<PlanGrad>(p.s)}, 0, w, lane, g};
+  float* ylds = (float*)(lds + Y_OFF);
+  for (int i = threadIdx.x; i < 32; i += NW * 64) ylds[i] = i < YD ? p.s.y[(size_t)yi * YD + i] : 0.0f;
+  float* pb = (float*)(lds + PB_OFF);
+  for (int i = threadIdx.x; i < PB_FLOATS; i += NW * 64) pb[i] = p.pbias[i];
+  {
+    char* const xd[2] = {lds + PL1_OFF, lds + PW4_OFF};
+    const char* const xs[2] = {(const char*)p.pl1, p.pw4};
+    const int xb[2] = {PL1_BYTES, PW4_BYTES};
+    eng.prologue(p.s, 2, xd, xs, xb);
+  }
+  float* sj = (float*)(lds + SJ_OFF) + w * 256;  // [16 chains][m][r]
+
+  Rng rng = rng_init(p.s.seed, (uint64_t)(p.s.chain_offset + c_local), (uint64_t)yi);
+  float x[XD];
+  {
+    float n0[XD];
+    rng_normals<XD>(rng, n0);
+#pragma unroll
+    for (int d = 0; d < XD; ++d) x[d] = __fadd_rn(__fmul_rn(n0[d], p.stdv), p.mean);
+  }
+  for (int i = 0; i < p.s.num_steps; ++i) {
+    const StepCoef cf = step_coef(i, p.s.num_steps, p.T, p.bmin, p.bdiff);
+    // prior score and Jacobian, 4 chains per pass
+    const int m = lane & 3;
+#pragma unroll 1
+    for (int pass = 0; pass < 4; ++pass) {
+      const int src = 4 * pass + (j >> 2);
+      float xin[XD];
+#pragma unroll
+      for (int d = 0; d < XD; ++d) xin[d] = __shfl(x[d], src, 64);
+      const f32x4 o = prior_pass(eng, xin, cf.tau, m);
+      if (g == 0) {
+#pragma unroll
+        for (int r = 0; r < 3; ++r) sj[(src * 4 + m) * 4 + r] = o[r];
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    float sc[XD], J[XD][XD];
+#pragma unroll
+    for (int r = 0; r < XD; ++r) {
+      sc[r] = sj[(j * 4 + 0) * 4 + r];
+#pragma unroll
+      for (int k = 0; k < XD; ++k) J[r][k] = sj[(j * 4 + 1 + k) * 4 + r];
+    }
+    // Tweedie estimate and the residual gradient through the surrogate
+    const float mw = vp_mean_weight(cf.tau, p.bmin, p.bdiff);
+    const float sd = vp_std(cf.tau, p.bmin, p.bdiff);
+    const float var = sd * sd;
+    float x0h[XD];
+#pragma unroll
+    for (int d = 0; d < XD; ++d) x0h[d] = (x[d] + var * sc[d]) / mw;
+    f32x4 f[2], v[2];
+    uint32_t mk[3][2];
+    eng.forward(x0h, f, mk);
+    float scale;
+    if (p.mode == 0) {  // NLL: v = dNLL/df (the likelihood terms of get_log_posterior, no boundary prior)
+      (void)energy(f, ylds, x0h, p.s.a, p.s.b2, 0.0f, g, v, true);
+      scale = p.zeta * p.delta * cf.beta;  // zeta delta g^2
+    } else {            // NORM: v = d||r||^2/df = -2 r, step zeta / ||r||
+      float rr = 0.0f;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = 16 * t + 4 * g + r;
+          const float res = row < YD ? ylds[row] - f[t][r] : 0.0f;
+          rr += res * res;
+          v[t][r] = -2.0f * res;
+        }
+      rr += shfl_xor(rr, 16);
+      rr += shfl_xor(rr, 32);
+      scale = p.zeta * __frsqrt_rn(fmaxf(rr, 1e-30f));
+    }
+    float gx[XD];
+    eng.backward(v, mk, gx);
+    float xi[XD];
+    rng_normals<XD>(rng, xi);
+#pragma unroll
+    for (int k = 0; k < XD; ++k) {
+      float jt = gx[k];
+#pragma unroll
+      for (int r = 0; r < XD; ++r) jt += var * J[r][k] * gx[r];
+      const float gt = jt / mw;
+      const float xe = em_update(x[k], __fmul_rn(cf.g, sc[k]), xi[k], cf, p.delta, p.sqrt_delta);
+      x[k] = xe - scale * gt;
+    }
+  }
+  eng.epilogue();
+  if (valid && g == 0) {
+    float* dst = p.s.x_out + ((size_t)yi * p.s.n_chains + c_local) * XD;
+#pragma unroll
+    for (int d = 0; d < XD; ++d) dst[d] = x[d];
+  }
+}
 }  // namespace sg
 
 hipError_t launch_surrogate_eval(const SurrogateParams& p, int mode, int n_wg, hipStream_t st) {
@@ -415,6 +646,13 @@ hipError_t launch_surrogate_eval(const SurrogateParams& p, int mode, int n_wg, h
 }
 
 int surrogate_rows_per_wg() { return sg::NW * 16; }
+
+hipError_t launch_dps(const DpsParams& p, int n_y, hipStream_t st) {
+  const long long per_wg = sg::NW * 16;
+  const dim3 grid((unsigned)((p.s.n_chains + per_wg - 1) / per_wg), (unsigned)n_y), block(sg::NW * 64);
+  hipLaunchKernelGGL(sg::dps_kernel, grid, block, 0, st, p);
+  return hipGetLastError();
+}
 
 hipError_t launch_mh(const SurrogateParams& p, int n_y, hipStream_t st) {
   const long long per_wg = sg::NW * 16;

@@ -5,7 +5,8 @@ Sampling is the hot path and runs on the HIP device only: one launch of the fuse
 reverse-SDE kernel for all num_steps, the chain state never leaving the registers --
   * CDE: dmip_em_sample;
   * PosteriorDiffusionEstimator: dmip_em_sample_posterior (prior + likelihood networks in one kernel);
-  * CDiffE (repaired sampler): dmip_em_sample_cdiffe.
+  * CDiffE (repaired sampler): dmip_em_sample_cdiffe;
+  * DPS (BASELINE config 4, prior score net + forward-model guidance): dmip_dps_sample.
 Shapes the library has no fused kernel for (dmip_sampler_supported) step through per-step launches
 of the MFMA network kernel (dmip_mlp_forward) with the SDE update as device tensor ops.
 There is no CPU sampling path: without a HIP device the samplers raise.
@@ -303,4 +304,83 @@ class PosteriorDiffusionEstimator(BaseClassDiffusionModel):
     def train_epoch(self, optimizer, loss_fn, epoch_data_loader):
         def batch_loss(x, y):
             return loss_fn(self.sde, x, y, self.sample_t(x))
+        return self._train_loop(optimizer, epoch_data_loader, batch_loss)
+
+
+class _PriorDrift(nn.Module):
+    """a(x, y, t) = g(t) prior(x, t): the unconditional drift of a prior score network (the prior half of
+    PosteriorScore, nets.py:155-157); y is ignored."""
+
+    def __init__(self, prior_net, forward_process):
+        super().__init__()
+        self.prior_net = prior_net
+        self.forward_sde = forward_process
+
+    def forward(self, x, y, t):
+        return self.forward_sde.g(t, x) * self.prior_net(x, t)
+
+
+class DPS(BaseClassDiffusionModel):
+    """Diffusion posterior sampling (Chung et al. 2023; BASELINE config 4) for the scatterometry problem:
+    a prior score network MLP2(x, t) (the PosteriorDiffusionEstimator's prior, trained with DSM as
+    PosteriorLoss trains it, losses.py:373-377) guided at every EM step by the gradient of the
+    measurement likelihood through the surrogate forward model at the Tweedie estimate
+    x0_hat = (x + var s) / mean_weight -- the quantity PosteriorLoss.likelihood_target (losses.py:349-371)
+    trains the reference's likelihood network towards, here computed exactly on the fly.
+    Fused kernel: dmip_dps_sample (include/dmip.h), one launch for all steps, exact f32.
+
+    forward_model: the surrogate nn.Sequential (load_forward_model); params: {'a', 'b', 'lambd_bd'};
+    guidance: 'nll' (score + zeta grad log p(y | x0_hat)) or 'norm' (Chung et al.'s zeta / ||y - F(x0_hat)||
+    step on ||y - F(x0_hat)||^2)."""
+
+    def __init__(self, xdim, ydim, hidden_layers, forward_model=None, params=None, zeta=1.0, guidance='nll'):
+        super().__init__(xdim, ydim)
+        forward_process = sdes.VariancePreservingSDE()
+        prior_net = MLP2(xdim + 1, xdim, hidden_layers, nn.Tanh()).to(device)
+        self.sde = sdes.PluginReverseSDE(forward_process, _PriorDrift(prior_net, forward_process), T=1, debias=True)
+        self.forward_model = forward_model
+        self.params = dict(params or {'a': 0.2, 'b': 0.01, 'lambd_bd': 1000})
+        self.zeta = float(zeta)
+        if guidance not in ('nll', 'norm'):
+            raise ValueError("guidance must be 'nll' or 'norm'")
+        self.guidance = guidance
+
+    @property
+    def prior_net(self):
+        return self.sde.a.prior_net
+
+    @classmethod
+    def from_posterior(cls, model, forward_model, params=None, zeta=1.0, guidance='nll'):
+        """A DPS sampler on the prior network of a trained PosteriorDiffusionEstimator."""
+        pn = model.sde.a.prior_net
+        m = cls(model.xdim, model.ydim, pn.hidden_layers, forward_model, params, zeta, guidance)
+        m.sde.a.prior_net.load_state_dict(pn.state_dict())
+        m.sde.a.prior_net.to(next(pn.parameters()).device)
+        return m
+
+    def sample_device(self, y, num_samples, num_steps=200, mean=0, std=1, seed=None, chain_offset=0, noise=None):
+        if noise is not None:
+            raise ValueError("noise injection is only implemented for the fused CDE sampler")
+        from .problems import surrogate_handle
+        pn = self.sde.a.prior_net
+        dev, ys, sde, out = self._prepare(y, num_samples, num_steps, [pn])
+        if self.forward_model is None:
+            raise ValueError("DPS needs the forward model (load_forward_model) for its guidance")
+        sur = surrogate_handle(self.forward_model, dev)
+        if sur is None:
+            raise ValueError("DPS: forward_model is not the scatterometry surrogate shape (3 -> 256^3 -> 23)")
+        seed = _draw_seed() if seed is None else seed
+        prior = pn.dmip_handle(dev, self.xdim)
+        p = self.params
+        _lib.dps_sample(prior, sur, _lib.scat_noise(p['a'], p['b'], p['lambd_bd']), sde, ys, num_samples,
+                        chain_offset, num_steps, mean, std, seed,
+                        _lib.DMIP_DPS_NLL if self.guidance == 'nll' else _lib.DMIP_DPS_NORM, self.zeta, out)
+        return out
+
+    def train_epoch(self, optimizer, loss_fn, epoch_data_loader):
+        """Prior DSM epoch (the prior half of PosteriorLoss, losses.py:373-377): score = prior(x_t, t)."""
+        def batch_loss(x, y):
+            t = self.sample_t(x)
+            x_t, target, std, g = self.sde.base_sde.sample(t, x, return_noise=True)
+            return loss_fn(self.sde.a.prior_net(x_t, t), std, target).mean()
         return self._train_loop(optimizer, epoch_data_loader, batch_loss)

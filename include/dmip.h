@@ -209,6 +209,28 @@ int dmip_mh_sample(const dmip_surrogate* s, const dmip_scat_noise* noise, const 
                    const float* x_init_dev, const float* noise_dev, const float* unif_dev, float* x_out_dev,
                    float* e_out_dev, void* stream);
 
+/* Diffusion posterior sampling (DPS, Chung et al. 2023) on the reference's Euler-Maruyama predictor:
+ * BASELINE config 4. The reference has no sampling-time guidance (its "Posterior"
+ * estimator learns the likelihood score with PosteriorLoss, losses.py:293-386); this is the build's
+ * definition, computing on the fly the quantity PosteriorLoss.likelihood_target trains towards. Per step,
+ * tau = T - t_i:
+ *   s, J = prior(x, tau) and ds/dx        (prior = the PosteriorDiffusionEstimator's MLP2 prior score net)
+ *   x0_hat = (x + var(tau) s) / mean_weight(tau)                          (Tweedie, losses.py:380)
+ *   G = dL(x0_hat(x))/dx = (I + var J^T) (dL/dx0_hat) / mean_weight
+ *   x <- x + delta (g^2 s + beta x / 2) + sqrt(delta) g xi  -  lambda G
+ *   mode DMIP_DPS_NLL:  L = the likelihood part of get_log_posterior (noise model `noise`; no boundary
+ *                       prior), lambda = zeta delta g^2: the EM step of the score s + zeta grad log p(y|x0_hat)
+ *   mode DMIP_DPS_NORM: L = ||y - F(x0_hat)||^2, lambda = zeta / ||y - F(x0_hat)|| (Chung et al. Alg. 1)
+ * with F the scatterometry surrogate. One fused launch for all steps, exact f32 arithmetic.
+ *   prior   MLP handle (DMIP_INPUT_X_T, xdim 3, hidden layers [256]*3)
+ *   fwd     surrogate handle;  noise: required for DMIP_DPS_NLL;  y_dev [n_y][23];  x_out_dev [n_y][n_chains][3]
+ * RNG, sharding and the other arguments as dmip_em_sample (no injection). */
+typedef enum { DMIP_DPS_NLL = 0, DMIP_DPS_NORM = 1 } dmip_dps_mode;
+int dmip_dps_sample(const dmip_mlp* prior, const dmip_surrogate* fwd, const dmip_scat_noise* noise,
+                    const dmip_vpsde* sde, const float* y_dev, int n_y, int64_t n_chains, int64_t chain_offset,
+                    int num_steps, float mean, float stdv, uint64_t seed, int mode, float zeta, float* x_out_dev,
+                    void* stream);
+
 /* Test hooks for the parity suite (integer RNG stream, normals, schedule). */
 int dmip_rng_words(uint64_t seed, int64_t chain_offset, uint64_t stream_id, int64_t n_chains, int n_words,
                    uint32_t* out_dev, void* stream);

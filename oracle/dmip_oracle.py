@@ -629,3 +629,81 @@ def mh_sample(params, y, num_steps, noise_std, a=0.2, b=0.01, lambd_bd=1000.0, x
         x = np.where(acc[:, None], xp, x)
         e_cur = np.where(acc, e_prop, e_cur)
     return x, e_cur - e0
+
+
+# ------------------------------------------------------------------------------------------
+# config 4  DPS (Chung et al. 2023, Alg. 1) on the EM predictor -- no reference code (SURVEY.md
+#           §0 D5); the build's definition (include/dmip.h dmip_dps_sample), restated here
+# ------------------------------------------------------------------------------------------
+
+def mlp2_jet(params, x, tau):
+    """Prior score s = MLP2(cat[x, tau]) (nets.py:37-57, double tanh on layer 1) and its Jacobian
+    J[n, i, k] = ds_i / dx_k by forward-mode tangents, float64."""
+    x = np.asarray(x, np.float64)
+    n, d = x.shape
+    inp = np.concatenate([x, np.full((n, 1), np.float64(tau))], 1)
+    W, b = [np.asarray(p[0], np.float64) for p in params], [np.asarray(p[1], np.float64) for p in params]
+    z = inp @ W[0].T + b[0]
+    t1 = np.tanh(z)
+    h = np.tanh(t1)
+    dh = ((1 - h * h) * (1 - t1 * t1))[:, :, None] * W[0][None, :, :d]  # (n, W, d)
+    for l in range(1, len(W) - 1):
+        z = h @ W[l].T + b[l]
+        dz = np.einsum("ij,njk->nik", W[l], dh)
+        h = np.tanh(z)
+        dh = (1 - h * h)[:, :, None] * dz
+    s = h @ W[-1].T + b[-1]
+    J = np.einsum("ij,njk->nik", W[-1], dh)
+    return s, J
+
+
+def surrogate_residual_grad(sur_params, x, y, mode="norm", a=0.2, b=0.01):
+    """L(x) and dL/dx through the ReLU surrogate (float64): mode "norm": L = ||y - F(x)||^2;
+    mode "nll": L = 0.5 sum log pref + 0.5 sum (y - F)^2 / pref (the likelihood part of
+    get_log_posterior, utils_scatterometry.py:33-35)."""
+    f, pre = surrogate_forward(sur_params, x, keep=True)
+    r = np.asarray(y, np.float64) - f
+    if mode == "norm":
+        L = (r * r).sum(1)
+        v = -2.0 * r
+    else:
+        pref = (a * f) ** 2 + b ** 2
+        L = 0.5 * np.log(pref).sum(1) + 0.5 * (r * r / pref).sum(1)
+        v = a * a * f / pref - r / pref - a * a * f * r * r / pref ** 2
+    for i in range(len(sur_params) - 1, -1, -1):
+        v = v @ np.asarray(sur_params[i][0], np.float64)
+        if i > 0:
+            v = v * (pre[i - 1] > 0)
+    return L, v
+
+
+def dps_sample(prior_params, sur_params, y, num_samples, num_steps, seed, zeta=1.0, mode="nll", a=0.2, b=0.01,
+               mean=0.0, std=1.0, chain_offset=0, stream=0, T=1.0, beta_min=BETA_MIN, beta_max=BETA_MAX):
+    """DPS with the prior score network (include/dmip.h dmip_dps_sample): per step (tau = T - t_i)
+      s, J = prior(x, tau), ds/dx;  x0_hat = (x + var(tau) s) / mean_weight(tau)   (Tweedie)
+      G = (I + var J^T) (dL/dx0_hat) / mean_weight
+      x <- EM(x, a = g s, xi) - lambda G
+    mode "nll": L = likelihood NLL, lambda = zeta delta beta; "norm": L = ||y - F||^2,
+    lambda = zeta / ||y - F(x0_hat)||. RNG as the CDE sampler (x0 then one 3-normal draw per step)."""
+    st = rng_init(seed, np.arange(chain_offset, chain_offset + num_samples), stream)
+    x = (rng_normals(st, 3) * F32(std) + F32(mean)).astype(F32)
+    ts, tau = schedule(num_steps, T)
+    delta = float(T) / num_steps
+    y = np.asarray(y, np.float64).reshape(1, -1)
+    for i in range(num_steps):
+        s, J = mlp2_jet(prior_params, x, tau[i])
+        mw = np.float64(vp_mean_weight(tau[i], beta_min, beta_max))
+        var = np.float64(vp_var(tau[i], beta_min, beta_max))
+        x0h = (x + var * s) / mw
+        L, gx = surrogate_residual_grad(sur_params, x0h, y, mode, a, b)
+        gt = (gx + var * np.einsum("nik,ni->nk", J, gx)) / mw
+        xi = rng_normals(st, 3)
+        beta = vp_beta(tau[i], beta_min, beta_max)
+        g = np.sqrt(beta).astype(F32)
+        if mode == "nll":
+            lam = np.full(x.shape[0], np.float64(zeta) * np.float64(F32(delta)) * np.float64(beta))
+        else:
+            lam = np.float64(zeta) / np.sqrt(np.maximum(L, 1e-30))
+        xe = em_step(x, (g * s.astype(F32)).astype(F32), tau[i], delta, beta_min, beta_max, xi)
+        x = (xe - (lam[:, None] * gt).astype(F32)).astype(F32)
+    return x

@@ -119,3 +119,12 @@ def test_surrogate_entry_points_reject_bad_arguments(lib, dmip):
     assert lib.dmip_log_posterior(None, ctypes.byref(nz), None, None, 0, 4, None, None, None) == L.DMIP_ERR_INVALID
     assert lib.dmip_mh_sample(None, ctypes.byref(nz), None, 1, 10, 0, 5, 0.5, 1, None, None, None, None, None,
                               None) == L.DMIP_ERR_INVALID
+
+
+def test_dps_rejects_bad_arguments(lib, dmip):
+    L = dmip._lib
+    sde = L.vpsde(0.1, 20.0, 1.0)
+    nz = L.scat_noise(0.2, 0.01, 1000)
+    rc = lib.dmip_dps_sample(None, None, ctypes.byref(nz), ctypes.byref(sde), None, 1, 10, 0, 5, 0.0, 1.0, 1, 0, 1.0,
+                             None, None)
+    assert rc == L.DMIP_ERR_INVALID

@@ -182,3 +182,49 @@ def test_generate_gt_samples_files(dmip, golden, fm, tmp_path):
         for j in range(3):
             a = np.load(os.path.join(tmp_path, str(i), f"{j}.npy"))
             assert a.shape == (500, 3) and np.array_equal(a, x[i, j].cpu().numpy())
+
+
+# ------------------------------------------------------------------------- DPS (BASELINE config 4)
+def _dps_model(dmip, fm, seed, zeta, guidance):
+    model, _, sur_params = fm
+    torch.manual_seed(seed)
+    m = dmip.DPS(3, 23, [256] * 3, model, zeta=zeta, guidance=guidance)
+    pn = m.prior_net
+    # an untrained prior drives EM + guidance chaotic within a few steps; a small, smooth output layer
+    # keeps the comparison well conditioned while every layer and both Jacobian paths contribute
+    with torch.no_grad():
+        last = [l for l in pn if isinstance(l, torch.nn.Linear)][-1]
+        last.weight.mul_(0.1)
+        last.bias.fill_(0.1)
+    prior = [(l.weight.detach().cpu().numpy(), l.bias.detach().cpu().numpy())
+             for l in pn if isinstance(l, torch.nn.Linear)]
+    return m, prior, sur_params
+
+
+@pytest.mark.parametrize("guidance,zeta", [("nll", 1.0), ("nll", 0.0), ("norm", 0.05)])
+def test_dps_vs_oracle_product_rng(dmip, golden, fm, guidance, zeta):
+    """Fused DPS kernel (prior score + forward-mode Jacobian, Tweedie estimate, surrogate residual
+    gradient, EM) against oracle.dps_sample with the same chain-keyed RNG; 5 steps, 300 chains.
+    Both compute in f32 / f64 respectively: |x - ref| <= 1e-3 max(1, |ref|)."""
+    m, prior, sur = _dps_model(dmip, fm, 3, zeta, guidance)
+    y = golden("data_scat.npz")["y_test"][2]
+    n, S, seed = 300, 5, 21
+    before = dmip._lib.calls.get("dps_sample", 0)
+    x = m.sample_device(torch.from_numpy(y).to(DEV), n, S, seed=seed)[0].cpu().numpy()
+    assert dmip._lib.calls["dps_sample"] == before + 1
+    ref = O.dps_sample(prior, sur, y, n, S, seed, zeta=zeta, mode=guidance)
+    assert np.all(np.isfinite(x))
+    err = np.abs(x - ref)
+    assert err.max() < 1e-3 * max(1.0, np.abs(ref).max()), err.max()
+    if zeta > 0:  # the guidance is not silently skipped
+        plain = O.dps_sample(prior, sur, y, n, S, seed, zeta=0.0, mode=guidance)
+        assert np.abs(plain - ref).max() > 100 * err.max()
+
+
+def test_dps_shards_bit_identical(dmip, golden, fm):
+    m, _, _ = _dps_model(dmip, fm, 4, 1.0, "nll")
+    ys = torch.from_numpy(golden("data_scat.npz")["y_test"][:2]).to(DEV)
+    full = m.sample_device(ys, 700, 6, seed=5)
+    shard = m.sample_device(ys, 200, 6, seed=5, chain_offset=300)
+    assert torch.equal(full[:, 300:500], shard)
+    assert not torch.equal(full[0], full[1])
