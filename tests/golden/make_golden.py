@@ -18,6 +18,9 @@ Fixtures (SURVEY.md §8c "Golden fixtures"):
   G5 pinn_linear.npz       PINNLoss / DSM_PDELoss / DSMLoss components and parameter grads
   G6 data_*.npz            y_test / x_test of both problems
   G7 surrogate.npz         scatterometry surrogate weights (fp32)
+  G9 ckpt_prior_scat.npz   a scatterometry prior score network MLP2 [256]*3 (the PosteriorDiffusionEstimator's
+                           prior) trained with the reference's DSMLoss on inverse_cdf_prior samples (the
+                           prior half of PosteriorLoss, losses.py:373-377; uniform t) -- for the DPS sampler
   G8 surrogate_io.npz      surrogate forward, get_log_posterior and its autograd input gradient
                            (energy_grad) on 256 seeded rows; anneal_to_energy (random-walk MH) with
                            its captured draws (64 chains x 50 steps) and a 4000-chain x 1000-step run
@@ -367,11 +370,44 @@ def gen_surrogate(R):
     np.savez(os.path.join(OUT, "surrogate_io.npz"), **out)
 
 
+# ----------------------------------------------------------------------------------------- G9
+def train_prior(R, minutes):
+    import torch
+    torch.set_num_threads(os.cpu_count())
+    torch.manual_seed(321)
+    np.random.seed(321)
+    post = R.diffusion.PosteriorDiffusionEstimator(3, 23, [256] * 3)
+    net = post.sde.a.prior_net
+    sde = post.sde.base_sde
+    loss_fn = R.losses.DSMLoss()
+    opt = torch.optim.Adam(net.parameters(), lr=1e-3)
+    t0 = time.time()
+    it, log = 0, []
+    while time.time() - t0 < minutes * 60:
+        frac = (time.time() - t0) / (minutes * 60)
+        for gr in opt.param_groups:
+            gr["lr"] = 1e-3 * (0.05 + 0.95 * 0.5 * (1 + np.cos(np.pi * min(frac, 1.0))))
+        x = torch.tensor(R.scat.inverse_cdf_prior(np.random.uniform(size=(1000, 3)), 1000), dtype=torch.float)
+        t = 1e-4 + torch.rand(1000, 1) * (1 - 1e-4)
+        x_t, target, std, g = sde.sample(t, x, return_noise=True)
+        loss = loss_fn(net(x_t, t), std, target).mean()
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        it += 1
+        if it % 2000 == 0:
+            log.append((it, float(loss)))
+            print("prior", it, float(loss), f"{time.time() - t0:.0f}s", flush=True)
+    np.savez(os.path.join(OUT, "ckpt_prior_scat.npz"), **state_to_npz_dict(net.state_dict()),
+             train_log=np.array(log, dtype=np.float64))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--what", default="all")
     ap.add_argument("--minutes-lin", type=float, default=4.0)
     ap.add_argument("--minutes-scat", type=float, default=12.0)
+    ap.add_argument("--minutes-prior", type=float, default=6.0)
     a = ap.parse_args()
     R = import_reference()
     w = a.what
@@ -393,6 +429,8 @@ def main():
         gen_samples(R)
     if w in ("all", "surrogate"):
         gen_surrogate(R)
+    if w in ("all", "prior"):
+        train_prior(R, a.minutes_prior)
 
 
 if __name__ == "__main__":
