@@ -330,10 +330,12 @@ class DPS(BaseClassDiffusionModel):
     Fused kernel: dmip_dps_sample (include/dmip.h), one launch for all steps, exact f32.
 
     forward_model: the surrogate nn.Sequential (load_forward_model); params: {'a', 'b', 'lambd_bd'};
-    guidance: 'nll' (score + zeta grad log p(y | x0_hat)) or 'norm' (Chung et al.'s zeta / ||y - F(x0_hat)||
-    step on ||y - F(x0_hat)||^2)."""
+    guidance: 'norm' (default; Chung et al.'s zeta / ||y - F(x0_hat)|| step on ||y - F(x0_hat)||^2) or 'nll'
+    (score + zeta grad log p(y | x0_hat), the reference PosteriorLoss target; unstable for zeta >~ 0.01 on
+    scatterometry because of the 1/mean_weight amplification at large diffusion times). Measured quality
+    against the fused MH ground truth: DESIGN.md §4c."""
 
-    def __init__(self, xdim, ydim, hidden_layers, forward_model=None, params=None, zeta=1.0, guidance='nll'):
+    def __init__(self, xdim, ydim, hidden_layers, forward_model=None, params=None, zeta=0.005, guidance='norm'):
         super().__init__(xdim, ydim)
         forward_process = sdes.VariancePreservingSDE()
         prior_net = MLP2(xdim + 1, xdim, hidden_layers, nn.Tanh()).to(device)
@@ -350,7 +352,7 @@ class DPS(BaseClassDiffusionModel):
         return self.sde.a.prior_net
 
     @classmethod
-    def from_posterior(cls, model, forward_model, params=None, zeta=1.0, guidance='nll'):
+    def from_posterior(cls, model, forward_model, params=None, zeta=0.005, guidance='norm'):
         """A DPS sampler on the prior network of a trained PosteriorDiffusionEstimator."""
         pn = model.sde.a.prior_net
         m = cls(model.xdim, model.ydim, pn.hidden_layers, forward_model, params, zeta, guidance)

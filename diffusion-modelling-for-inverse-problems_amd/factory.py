@@ -1,8 +1,8 @@
 """Config -> (model, loss_fn) factory with the reference's dispatch (utils.py:22-48).
 
 Extension (not in the reference): config['model'] == 'DPS' builds the guided sampler of BASELINE config 4
-(estimators.DPS) on `forward_model`, with optional config keys 'zeta' (default 1.0) and 'guidance'
-('nll' | 'norm'); its training loss is the prior DSM (DSMLoss)."""
+(estimators.DPS) on `forward_model`, with optional config keys 'zeta' (default 0.005) and 'guidance'
+('norm' | 'nll', default 'norm'); its training loss is the prior DSM (DSMLoss)."""
 from .estimators import CDE, DPS, CDiffE, PosteriorDiffusionEstimator
 from .losses import DSM_PDELoss, DSMLoss, PINNLoss, PINNLoss2
 
@@ -12,7 +12,7 @@ _MODELS = {'CDE': CDE, 'CDiffE': CDiffE, 'Posterior': PosteriorDiffusionEstimato
 def get_model_from_args(config, forward_model_params, score_posterior, forward_model):
     if config['model'] == 'DPS':
         model = DPS(forward_model_params['xdim'], forward_model_params['ydim'], config['hidden_layers'], forward_model,
-                    forward_model_params, zeta=config.get('zeta', 1.0), guidance=config.get('guidance', 'nll'))
+                    forward_model_params, zeta=config.get('zeta', 0.005), guidance=config.get('guidance', 'norm'))
         return model, DSMLoss()
     cls = _MODELS.get(config['model'])
     if cls is None:

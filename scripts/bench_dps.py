@@ -8,7 +8,7 @@ Weights: the fixture-trained prior (tests/golden/ckpt_prior_scat.npz, DSM on inv
 samples) or random init. Algorithmic flops per chain-step: prior forward + input VJP (2 F_prior,
 F_prior = 2 (4*256 + 2*256^2 + 256*3)) + surrogate forward + VJP (2 F_sur, F_sur = 275,456); the kernel
 executes 4 F_prior for the prior (primal + 3 forward tangents).
-    python scripts/bench_dps.py [--samples 262144] [--steps 1000] [--zeta 1.0] [--guidance nll]
+    python scripts/bench_dps.py [--samples 262144] [--steps 1000] [--zeta 0.005] [--guidance norm]
     torchrun --nproc-per-node 4 scripts/bench_dps.py"""
 import argparse
 import importlib
@@ -32,11 +32,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--samples", type=int, default=262144, help="total samples (all ranks)")
     ap.add_argument("--steps", type=int, default=1000)
-    ap.add_argument("--zeta", type=float, default=1.0)
-    ap.add_argument("--guidance", default="nll")
+    ap.add_argument("--zeta", type=float, default=0.005)
+    ap.add_argument("--guidance", default="norm")
     ap.add_argument("--y-index", type=int, default=0)
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--gt-chains", type=int, default=30000)
+    ap.add_argument("--compare-cde", action="store_true", help="also score the fixture-trained CDE on the same y")
     a = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -102,8 +103,22 @@ def main():
         # two independent MH runs: the histogram-noise floor of KL2 at this sample size
         gt2 = pkg.mh_sample(fm, prm, y[None], a.gt_chains, 1000, 0.5, seed=98)[0]
         kl0, _ = ev.hist_kl(ev.histograms(gt, 75, (-1.2, 1.2))[0], ev.histograms(gt2, 75, (-1.2, 1.2))[0])
+        def w1(u, v):  # per-dimension 1-D Wasserstein distance on equal-size samples
+            return [float((torch.sort(u[:, k])[0] - torch.sort(v[:, k])[0]).abs().mean()) for k in range(3)]
         out["quality"] = {"KL2_vs_mcmc": kl, "KL_reverse": klr, "KL2_mcmc_vs_mcmc": kl0, "n": a.gt_chains,
-                          "y_index": a.y_index, "mean": xs.mean(0).tolist(), "mcmc_mean": gt.mean(0).tolist()}
+                          "y_index": a.y_index, "W1_vs_mcmc": w1(xs, gt), "W1_mcmc_vs_mcmc": w1(gt2, gt),
+                          "mean": xs.mean(0).tolist(), "mcmc_mean": gt.mean(0).tolist(),
+                          "std": xs.std(0).tolist(), "mcmc_std": gt.std(0).tolist()}
+        if a.compare_cde:
+            cde = pkg.CDE(3, 23, [256] * 3)
+            zc = np.load(os.path.join(gold, "ckpt_scat.npz"))
+            cde.sde.a.load_state_dict({k.replace("_", "."): torch.from_numpy(zc[k]) for k in zc.files
+                                       if k.split("_")[0].isdigit()})
+            cde.sde.a.to(dev)
+            xc = cde.sample_device(y, a.gt_chains, a.steps, seed=5)[0]
+            klc, _ = ev.hist_kl(ev.histograms(gt, 75, (-1.2, 1.2))[0], ev.histograms(xc, 75, (-1.2, 1.2))[0])
+            out["quality_cde"] = {"KL2_vs_mcmc": klc, "W1_vs_mcmc": w1(xc, gt), "mean": xc.mean(0).tolist(),
+                                  "std": xc.std(0).tolist()}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
