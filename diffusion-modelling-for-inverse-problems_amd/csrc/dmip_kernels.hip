@@ -90,8 +90,10 @@ struct Engine {
   int w, lane;
 
   __device__ __forceinline__ void ring_issue(long long g) {
-    const int c = (int)(g % L::NCT);
-    const char* src = hidden[c / L::NC] + (size_t)(c % L::NC) * L::CHUNK;
+    // chunk index and network select stay scalar (the counter is wave-uniform; the segment loop of
+    // the balanced sampler hides that from the divergence analysis)
+    const int c = __builtin_amdgcn_readfirstlane((int)(g % L::NCT));
+    const char* src = (c < L::NC ? hidden[0] : hidden[1]) + (size_t)(c % L::NC) * L::CHUNK;
     char* dst = lds + L::W_OFF + (int)(g % R) * L::CHUNK;
 #pragma unroll
     for (int q = 0; q < PPW; ++q) {
@@ -313,30 +315,61 @@ constexpr int k1s_of(int slots) { return (slots + 15) / 16; }
 //   MODE_CDIFFE:    y_t ~ q(y_t | y) at T-t, a = net(x, y_t, T-t)[:xdim]   (repaired
 //                   models/diffusion.py:158-180; the y part of the joint update is discarded)
 // then mu = g a + 0.5 beta x, x <- x + delta mu + sqrt(delta) g xi.
+//
+// Work distribution (persistent, preemptive): the grid.x workgroups of a y split its 32-chain tiles
+// into contiguous ranges of K tiles. A tile is a job of S steps; a workgroup's K S wave-steps are cut
+// into NW equal segments of C = ceil(K S / NW) steps (McNaughton's wrap-around rule), one per wave,
+// so every wave stays busy to the end: a chain count that is not a multiple of the CU's 256-chain
+// capacity no longer leaves a half-empty second round. A tile cut by a segment boundary runs its
+// first part at the START of the earlier wave's segment and its second part at the END of the next
+// wave's; with K > NW, C > S, so at least one whole step -- whose ring barriers order the LDS write
+// before the read -- separates the hand-over of its state (x, RNG) from its resumption. All waves of
+// a workgroup run the same number of steps (idle steps compute on a dummy tile), keeping the weight
+// ring's barriers paired. A chain's arithmetic does not depend on which wave runs it: results are
+// bit-identical to an unsplit run.
 // STAMP: diagnostic build only (dmip_em_sample_stamps) -- per-wave cycle sums of the step phases
 // [layer 1 + B1, hidden layers, output layer + RNG + EM update], written to p.stamps.
 // TUNE (development variants): bit 0 = complementary tile order per wave half (Engine SPLIT),
 // bit 1 = s_setprio 1 for the second-dispatched wave half.
+template <int MODE, int W, int NL, int D, int M, int NW, int R, bool RES>
+struct SamplerLds {
+  static constexpr int NNET = MODE == MODE_POSTERIOR ? 2 : 1;
+  static constexpr int NV = MODE == MODE_CDIFFE ? D + M + 1 : D + 1;  // inputs that vary per chain
+  static constexpr int K1S = k1s_of(3 * NV + 2);
+  using L = Lay<W, NL, K1S, NNET, R, RES>;
+  // Step-split balancing needs the ring's per-chunk barriers to keep the waves in lockstep: only the
+  // streaming (non-resident) kernels balance; resident ones run one tile per wave.
+  static constexpr bool BALANCE = !RES;
+  static constexpr int HANDOFF_WORDS = D + 4;   // x[D] + the xoshiro128** state, per lane
+  static constexpr int HANDOFF_OFF = L::TOTAL;  // [NW][HANDOFF_WORDS][64] words
+  static constexpr int TOTAL = HANDOFF_OFF + (BALANCE ? NW * HANDOFF_WORDS * 64 * 4 : 0);
+};
+
+// segment of a wave's schedule: tile, first step, end step, kind (0 whole tile, 1 first part handed
+// over, 2 second part taken over, 3 idle)
+struct Seg {
+  int job, s0, s1, kind;
+};
+
 template <int MODE, int W, int NL, int D, int M, int NW, int R, bool RES, bool NOISE, bool STAMP = false,
           int DIAG = 0, int TUNE = 0>
 __global__ void __launch_bounds__(NW * 64, (NW * 64 + 255) / 256)
 em_sampler_kernel(SamplerParams p) {
-  constexpr int NNET = MODE == MODE_POSTERIOR ? 2 : 1;
-  constexpr int NV = MODE == MODE_CDIFFE ? D + M + 1 : D + 1;  // inputs that vary per chain
-  constexpr int K1S = k1s_of(3 * NV + 2);
-  using L = Lay<W, NL, K1S, NNET, R, RES>;
-  static_assert(L::TOTAL <= 160 * 1024, "LDS budget");
+  using SL = SamplerLds<MODE, W, NL, D, M, NW, R, RES>;
+  constexpr int NNET = SL::NNET;
+  constexpr int NV = SL::NV;
+  constexpr int K1S = SL::K1S;
+  using L = typename SL::L;
+  static_assert(SL::TOTAL <= 160 * 1024, "LDS budget");
   static_assert(RES || (L::KS % NW == 0), "ring pieces per wave");
   static_assert(D <= 4, "sampler output rows are duplicated into both lane halves (D <= 4)");
   static_assert(!(NOISE && MODE != MODE_CDE), "noise injection: CDE only");
-  __shared__ __attribute__((aligned(16))) char lds[L::TOTAL];
+  __shared__ __attribute__((aligned(16))) char lds[SL::TOTAL];
 
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int h = lane >> 5;
   const int yi = blockIdx.y;
-  const long long c_local = (long long)blockIdx.x * (NW * 32) + w * 32 + (lane & 31);
-  const bool valid = c_local < p.n_chains;
 
   Engine<W, NL, K1S, NNET, NW, R, RES, NOISE, DIAG, (TUNE & 1) != 0> eng{lds, {p.hidden, p.hidden2}, 0, w, lane};
   if constexpr ((TUNE & 2) != 0) {
@@ -350,13 +383,84 @@ em_sampler_kernel(SamplerParams p) {
     const float* const bo[2] = {p.bias_out, p.bias_out2};
     eng.prologue(a1, ao, bh, bo);
   }
+  // CDiffE: this workgroup's observation, read from LDS every step (wave-uniform broadcast)
+  __shared__ float yobs[M > 0 ? M : 1];
+  if constexpr (MODE == MODE_CDIFFE) {
+    stage_floats(yobs, p.y_obs + (size_t)yi * M, M, threadIdx.x, NW * 64);
+    __syncthreads();
+  }
+  float* handoff = (float*)(lds + SL::HANDOFF_OFF);
 
+  // ---- this wave's schedule (wave-uniform)
+  const int S = p.num_steps;
+  const long long tiles_y = (p.n_chains + 31) / 32;
+  const long long t_base = tiles_y * blockIdx.x / gridDim.x;
+  const int K = (int)(tiles_y * (blockIdx.x + 1) / gridDim.x - t_base);
+  long long C = S;
+  int a_job = -1, a_len = 0, b_job = -1, b_from = 0, f_first = 0, n_full = 0;
+  if (!SL::BALANCE || K <= NW) {  // (unbalanced grids give every workgroup <= NW tiles)
+    if (w < K) f_first = w, n_full = 1;
+  } else {
+    C = ((long long)K * S + NW - 1) / NW;  // > S
+    const long long lo = (long long)w * C;
+    const long long hi = lo + C < (long long)K * S ? lo + C : (long long)K * S;
+    if (lo < hi) {
+      const int j_lo = (int)(lo / S), r_lo = (int)(lo % S);
+      const int j_hi = (int)(hi / S), r_hi = (int)(hi % S);
+      if (r_lo > 0) b_job = j_lo, b_from = r_lo;
+      if (r_hi > 0) a_job = j_hi, a_len = r_hi;
+      f_first = r_lo > 0 ? j_lo + 1 : j_lo;
+      n_full = j_hi - f_first > 0 ? j_hi - f_first : 0;
+    }
+  }
+  const long long used = (long long)a_len + (long long)n_full * S + (b_job >= 0 ? S - b_from : 0);
+  const int n_seg = __builtin_amdgcn_readfirstlane((a_job >= 0) + n_full + (b_job >= 0) + (C > used));
+  // order: A, whole tiles, idle, B -- B must END at step C (the last wave's segment is short)
+  auto segment = [&](int k) -> Seg {
+    if (a_job >= 0) {
+      if (k == 0) return Seg{a_job, 0, a_len, 1};
+      --k;
+    }
+    if (k < n_full) return Seg{f_first + k, 0, S, 0};
+    k -= n_full;
+    if (C > used) {
+      if (k == 0) return Seg{-1, 0, (int)(C - used), 3};
+      --k;
+    }
+    return Seg{b_job, b_from, S, 2};
+  };
+
+  unsigned long long ph[3] = {0, 0, 0};
+  unsigned long long clk0 = 0, rt0 = 0;
+  if constexpr (STAMP) {
+    clk0 = stamp();
+    rt0 = __builtin_amdgcn_s_memrealtime();
+  }
+  const size_t noise_step = (size_t)gridDim.y * p.n_chains * D;
+
+  for (int sgi = 0; sgi < n_seg; ++sgi) {
+  // wave-uniform by construction; say so, or the ring's chunk counter would be treated as divergent
+  const Seg s_ = segment(sgi);
+  const Seg sg{__builtin_amdgcn_readfirstlane(s_.job), __builtin_amdgcn_readfirstlane(s_.s0),
+               __builtin_amdgcn_readfirstlane(s_.s1), __builtin_amdgcn_readfirstlane(s_.kind)};
+  const long long c_local = (t_base + (sg.job >= 0 ? sg.job : 0)) * 32 + (lane & 31);
+  const bool valid = sg.job >= 0 && c_local < p.n_chains;
+  const long long c_rd = valid ? c_local : 0;
   float x[D];
-  Rng rng = rng_init(p.seed, (uint64_t)(p.chain_offset + c_local), (uint64_t)yi);
-  {
+  Rng rng;
+  if (sg.kind == 2) {  // resume the tile wave w - 1 handed over (>= 1 step of barriers ago)
+    const float* src = handoff + (size_t)(w - 1) * SL::HANDOFF_WORDS * 64;
+#pragma unroll
+    for (int k = 0; k < D; ++k) x[k] = src[k * 64 + lane];
+    rng.s0 = __float_as_uint(src[(D + 0) * 64 + lane]);
+    rng.s1 = __float_as_uint(src[(D + 1) * 64 + lane]);
+    rng.s2 = __float_as_uint(src[(D + 2) * 64 + lane]);
+    rng.s3 = __float_as_uint(src[(D + 3) * 64 + lane]);
+  } else {
+    rng = rng_init(p.seed, (uint64_t)(p.chain_offset + c_local), (uint64_t)yi);
     float n[D];
     if constexpr (NOISE) {
-      const float* src = p.noise + (((size_t)yi * p.n_chains + (valid ? c_local : 0)) * D);
+      const float* src = p.noise + (((size_t)yi * p.n_chains + c_rd) * D);
 #pragma unroll
       for (int k = 0; k < D; ++k) n[k] = src[k];
     } else {
@@ -365,24 +469,11 @@ em_sampler_kernel(SamplerParams p) {
 #pragma unroll
     for (int k = 0; k < D; ++k) x[k] = __fadd_rn(__fmul_rn(n[k], p.stdv), p.mean);
   }
-  const size_t noise_step = (size_t)gridDim.y * p.n_chains * D;
-  // CDiffE: this workgroup's observation, read from LDS every step (wave-uniform broadcast)
-  __shared__ float yobs[M > 0 ? M : 1];
-  if constexpr (MODE == MODE_CDIFFE) {
-    stage_floats(yobs, p.y_obs + (size_t)yi * M, M, threadIdx.x, NW * 64);
-    __syncthreads();
-  }
 
-  unsigned long long ph[3] = {0, 0, 0};
-  unsigned long long clk0 = 0, rt0 = 0;
-  if constexpr (STAMP) {
-    clk0 = stamp();
-    rt0 = __builtin_amdgcn_s_memrealtime();
-  }
-  for (int i = 0; i < p.num_steps; ++i) {
+  for (int i = sg.s0; i < sg.s1; ++i) {
     unsigned long long t0 = 0, t1 = 0, t2 = 0;
     if constexpr (STAMP) t0 = stamp();
-    const StepCoef cf = step_coef(i, p.num_steps, p.T, p.bmin, p.bdiff);
+    const StepCoef cf = step_coef(sg.kind == 3 ? 0 : i, S, p.T, p.bmin, p.bdiff);
     float v[NV];
 #pragma unroll
     for (int k = 0; k < D; ++k) v[k] = x[k];
@@ -430,7 +521,7 @@ em_sampler_kernel(SamplerParams p) {
     if constexpr (STAMP) t2 = stamp();
     float xi[D];
     if constexpr (NOISE) {
-      const float* src = p.noise + noise_step * (i + 1) + (((size_t)yi * p.n_chains + (valid ? c_local : 0)) * D);
+      const float* src = p.noise + noise_step * (sg.kind == 3 ? 1 : i + 1) + (((size_t)yi * p.n_chains + c_rd) * D);
 #pragma unroll
       for (int k = 0; k < D; ++k) xi[k] = src[k];
     } else {
@@ -449,6 +540,21 @@ em_sampler_kernel(SamplerParams p) {
       ph[2] += t3 - t2;
     }
   }
+
+  if (sg.kind == 1) {  // hand the tile over to wave w + 1
+    float* dst = handoff + (size_t)w * SL::HANDOFF_WORDS * 64;
+#pragma unroll
+    for (int k = 0; k < D; ++k) dst[k * 64 + lane] = x[k];
+    dst[(D + 0) * 64 + lane] = __uint_as_float(rng.s0);
+    dst[(D + 1) * 64 + lane] = __uint_as_float(rng.s1);
+    dst[(D + 2) * 64 + lane] = __uint_as_float(rng.s2);
+    dst[(D + 3) * 64 + lane] = __uint_as_float(rng.s3);
+  } else if (sg.kind != 3 && valid && h == 0) {
+    float* dst = p.x_out + ((size_t)yi * p.n_chains + c_local) * D;
+#pragma unroll
+    for (int k = 0; k < D; ++k) dst[k] = x[k];
+  }
+  }  // segments
   eng.epilogue();
   if constexpr (STAMP) {
     const unsigned long long clk1 = stamp();
@@ -461,11 +567,6 @@ em_sampler_kernel(SamplerParams p) {
       o[3] = clk1 - clk0;  // shader clock ticks over the step loop
       o[4] = rt1 - rt0;    // 100 MHz constant clock over the same span
     }
-  }
-  if (valid && h == 0) {
-    float* dst = p.x_out + ((size_t)yi * p.n_chains + c_local) * D;
-#pragma unroll
-    for (int k = 0; k < D; ++k) dst[k] = x[k];
   }
 }
 
@@ -621,10 +722,32 @@ __global__ void schedule_kernel(int S, float T, float bmin, float bdiff, float* 
 }
 
 // ------------------------------------------------------------------------------ dispatch
+// workgroups per y: enough to fill every CU slot once (the kernel balances the work inside a
+// workgroup), never more than one per NW tiles
+template <typename Kern>
+static unsigned sampler_wgs_per_y(Kern kern, int nthreads, long long n_chains, int n_y, bool balance = true) {
+  if (!balance) return (unsigned)((((n_chains + 31) / 32) + nthreads / 64 - 1) / (nthreads / 64));
+  static int slots = -1;  // one value per kernel instantiation
+  if (slots < 0) {
+    int dev = 0, n_cu = 256, per_cu = 1;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, nthreads, 0) != hipSuccess || per_cu < 1) per_cu = 1;
+    slots = (n_cu > 0 ? n_cu : 256) * per_cu;
+  }
+  const long long nw = nthreads / 64;
+  const long long tiles = (n_chains + 31) / 32;
+  long long g = slots / (n_y > 0 ? n_y : 1);
+  const long long cap = (tiles + nw - 1) / nw;
+  if (g > cap) g = cap;
+  if (g < 1) g = 1;
+  return (unsigned)g;
+}
+
 template <int MODE, int W, int NL, int D, int M, int NW, int R, bool RES>
 static hipError_t launch_sampler_t(const SamplerParams& p, int n_y, hipStream_t st) {
-  const long long per_wg = NW * 32;
-  dim3 grid((unsigned)((p.n_chains + per_wg - 1) / per_wg), (unsigned)n_y);
+  const dim3 grid(sampler_wgs_per_y(em_sampler_kernel<MODE, W, NL, D, M, NW, R, RES, false>, NW * 64, p.n_chains, n_y,
+                                    SamplerLds<MODE, W, NL, D, M, NW, R, RES>::BALANCE),
+                  (unsigned)n_y);
   if constexpr (MODE == MODE_CDE) {
     if (p.stamps)
       hipLaunchKernelGGL((em_sampler_kernel<MODE, W, NL, D, M, NW, R, RES, false, true>), grid, dim3(NW * 64), 0, st, p);
@@ -679,8 +802,12 @@ hipError_t launch_sampler(const SamplerParams& p, int mode, int width, int n_hid
                           hipStream_t st, bool* supported) {
   *supported = true;
   const int var = sampler_variant();
+  const auto variant_grid = [&]() {
+    return dim3(sampler_wgs_per_y(em_sampler_kernel<MODE_CDE, 256, 3, 3, 0, 8, 4, false, false>, 512, p.n_chains, n_y),
+                (unsigned)n_y);
+  };
   if (mode == MODE_CDE && width == 256 && n_hidden == 3 && xdim == 3 && var >= 101 && var <= 107) {
-    dim3 grid((unsigned)((p.n_chains + 255) / 256), (unsigned)n_y);
+    const dim3 grid = variant_grid();
     switch (var - 100) {
 #define DG(d) \
   case d: hipLaunchKernelGGL((em_sampler_kernel<MODE_CDE, 256, 3, 3, 0, 8, 4, false, false, false, d>), grid, dim3(512), 0, st, p); break;
@@ -691,7 +818,7 @@ hipError_t launch_sampler(const SamplerParams& p, int mode, int width, int n_hid
     return hipGetLastError();
   }
   if (mode == MODE_CDE && width == 256 && n_hidden == 3 && xdim == 3 && var >= 201 && var <= 203) {
-    dim3 grid((unsigned)((p.n_chains + 255) / 256), (unsigned)n_y);
+    const dim3 grid = variant_grid();
     switch (var - 200) {
 #define TG(t) \
   case t: hipLaunchKernelGGL((em_sampler_kernel<MODE_CDE, 256, 3, 3, 0, 8, 4, false, false, false, 0, t>), grid, dim3(512), 0, st, p); break;

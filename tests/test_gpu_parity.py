@@ -565,3 +565,18 @@ def test_evaluate_linear_driver(dmip, golden, tmp_path):
     xt = post.sample((20000,)).numpy()
     kl_ref, _ = O.hist_kl(xt, s["samples"], lim=(-3.5, 3.5))
     assert kl < 1.5 * kl_ref + 0.02, (kl, kl_ref)
+
+
+@pytest.mark.parametrize("n,S", [(100000, 20), (70001, 9), (150000, 3)])
+def test_balanced_schedule_matches_unsplit_runs(dmip, golden, n, S):
+    """Chain counts above the GPU's one-round capacity (256 CUs x 256 chains) make the persistent
+    sampler split tiles between waves (step-split schedule with an LDS hand-over). Every chain must
+    come out bit-identical to a launch small enough to run each tile whole on one wave."""
+    m = _cde(dmip, "scat", golden("ckpt_scat.npz"), "")
+    y = torch.from_numpy(golden("data_scat.npz")["y_test"][1]).to(DEV)
+    full = m.sample_device(y, n, S, seed=13)[0]
+    for lo in (0, 12345, n - 777):
+        k = min(1000, n - lo)
+        part = m.sample_device(y, k, S, seed=13, chain_offset=lo)[0]
+        assert torch.equal(full[lo:lo + k], part), lo
+    assert torch.isfinite(full).all()
