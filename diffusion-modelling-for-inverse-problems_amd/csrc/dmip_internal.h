@@ -33,6 +33,10 @@ struct SamplerParams {
   float T, bmin, bdiff, delta, sqrt_delta, mean, stdv;
   unsigned long long seed;
   unsigned long long* stamps; // diagnostic build only: [n_wg * NW][3] phase cycle sums, else null
+  // hand-over of split tiles between waves (set by launch_sampler): per y and wave of the grid, the
+  // chain state [D + 4][64] words and a ready flag (zeroed before the launch)
+  float* xfer;
+  unsigned int* xflag;
 };
 
 struct ForwardParams {

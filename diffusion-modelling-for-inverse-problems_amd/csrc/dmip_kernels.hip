@@ -316,17 +316,17 @@ constexpr int k1s_of(int slots) { return (slots + 15) / 16; }
 //                   models/diffusion.py:158-180; the y part of the joint update is discarded)
 // then mu = g a + 0.5 beta x, x <- x + delta mu + sqrt(delta) g xi.
 //
-// Work distribution (persistent, preemptive): the grid.x workgroups of a y split its 32-chain tiles
-// into contiguous ranges of K tiles. A tile is a job of S steps; a workgroup's K S wave-steps are cut
-// into NW equal segments of C = ceil(K S / NW) steps (McNaughton's wrap-around rule), one per wave,
-// so every wave stays busy to the end: a chain count that is not a multiple of the CU's 256-chain
-// capacity no longer leaves a half-empty second round. A tile cut by a segment boundary runs its
-// first part at the START of the earlier wave's segment and its second part at the END of the next
-// wave's; with K > NW, C > S, so at least one whole step -- whose ring barriers order the LDS write
-// before the read -- separates the hand-over of its state (x, RNG) from its resumption. All waves of
-// a workgroup run the same number of steps (idle steps compute on a dummy tile), keeping the weight
-// ring's barriers paired. A chain's arithmetic does not depend on which wave runs it: results are
-// bit-identical to an unsplit run.
+// Work distribution (persistent, preemptive): the G = grid.x workgroups of a y -- at most as many as
+// the GPU holds at once -- share its 32-chain tiles. A tile is a job of S steps; the y's tiles * S
+// wave-steps are cut into G * NW equal segments of C = ceil(tiles S / (G NW)) steps (McNaughton's
+// wrap-around rule), one per wave, so every wave of every CU stays busy to the end: a chain count
+// that is not a multiple of the GPU's one-round capacity no longer costs a half-empty extra round.
+// A tile cut by a segment boundary runs its first part at the START of the earlier wave's segment
+// and its second part at the END of the next wave's (order-safe since C >= S); the state (x, RNG)
+// goes through global memory with a release/acquire flag (the consumer normally finds it set: the
+// first part ended C - S steps before it is needed). All waves of a workgroup run C steps (idle
+// steps compute on a dummy tile), keeping the weight ring's barriers paired. A chain's arithmetic
+// does not depend on which wave runs it: results are bit-identical to an unsplit run.
 // STAMP: diagnostic build only (dmip_em_sample_stamps) -- per-wave cycle sums of the step phases
 // [layer 1 + B1, hidden layers, output layer + RNG + EM update], written to p.stamps.
 // TUNE (development variants): bit 0 = complementary tile order per wave half (Engine SPLIT),
@@ -337,13 +337,9 @@ struct SamplerLds {
   static constexpr int NV = MODE == MODE_CDIFFE ? D + M + 1 : D + 1;  // inputs that vary per chain
   static constexpr int K1S = k1s_of(3 * NV + 2);
   using L = Lay<W, NL, K1S, NNET, R, RES>;
-  // Step-split balancing needs the ring's per-chunk barriers to keep the waves in lockstep: only the
-  // streaming (non-resident) kernels balance; resident ones run one tile per wave.
-  static constexpr bool BALANCE = !RES;
-  static constexpr int HANDOFF_WORDS = D + 4;   // x[D] + the xoshiro128** state, per lane
-  static constexpr int HANDOFF_OFF = L::TOTAL;  // [NW][HANDOFF_WORDS][64] words
-  static constexpr int TOTAL = HANDOFF_OFF + (BALANCE ? NW * HANDOFF_WORDS * 64 * 4 : 0);
+  static constexpr int TOTAL = L::TOTAL;
 };
+constexpr int sampler_xfer_words(int D) { return (D + 4) * 64; }  // x[D] + xoshiro128** state, per lane
 
 // segment of a wave's schedule: tile, first step, end step, kind (0 whole tile, 1 first part handed
 // over, 2 second part taken over, 3 idle)
@@ -389,21 +385,20 @@ em_sampler_kernel(SamplerParams p) {
     stage_floats(yobs, p.y_obs + (size_t)yi * M, M, threadIdx.x, NW * 64);
     __syncthreads();
   }
-  float* handoff = (float*)(lds + SL::HANDOFF_OFF);
-
   // ---- this wave's schedule (wave-uniform)
   const int S = p.num_steps;
   const long long tiles_y = (p.n_chains + 31) / 32;
-  const long long t_base = tiles_y * blockIdx.x / gridDim.x;
-  const int K = (int)(tiles_y * (blockIdx.x + 1) / gridDim.x - t_base);
+  const long long n_waves = (long long)gridDim.x * NW;  // waves sharing this y
+  const long long gw = (long long)blockIdx.x * NW + w;  // this wave among them
+  constexpr int XW = sampler_xfer_words(D);
   long long C = S;
   int a_job = -1, a_len = 0, b_job = -1, b_from = 0, f_first = 0, n_full = 0;
-  if (!SL::BALANCE || K <= NW) {  // (unbalanced grids give every workgroup <= NW tiles)
-    if (w < K) f_first = w, n_full = 1;
+  if (tiles_y <= n_waves) {
+    if (gw < tiles_y) f_first = (int)gw, n_full = 1;
   } else {
-    C = ((long long)K * S + NW - 1) / NW;  // > S
-    const long long lo = (long long)w * C;
-    const long long hi = lo + C < (long long)K * S ? lo + C : (long long)K * S;
+    C = (tiles_y * S + n_waves - 1) / n_waves;  // > S
+    const long long lo = gw * C;
+    const long long hi = lo + C < tiles_y * S ? lo + C : tiles_y * S;
     if (lo < hi) {
       const int j_lo = (int)(lo / S), r_lo = (int)(lo % S);
       const int j_hi = (int)(hi / S), r_hi = (int)(hi % S);
@@ -443,13 +438,18 @@ em_sampler_kernel(SamplerParams p) {
   const Seg s_ = segment(sgi);
   const Seg sg{__builtin_amdgcn_readfirstlane(s_.job), __builtin_amdgcn_readfirstlane(s_.s0),
                __builtin_amdgcn_readfirstlane(s_.s1), __builtin_amdgcn_readfirstlane(s_.kind)};
-  const long long c_local = (t_base + (sg.job >= 0 ? sg.job : 0)) * 32 + (lane & 31);
+  const long long c_local = (long long)(sg.job >= 0 ? sg.job : 0) * 32 + (lane & 31);
   const bool valid = sg.job >= 0 && c_local < p.n_chains;
   const long long c_rd = valid ? c_local : 0;
   float x[D];
   Rng rng;
-  if (sg.kind == 2) {  // resume the tile wave w - 1 handed over (>= 1 step of barriers ago)
-    const float* src = handoff + (size_t)(w - 1) * SL::HANDOFF_WORDS * 64;
+  if (sg.kind == 2) {  // resume the tile the previous wave of the grid handed over
+    const size_t slot = (size_t)yi * n_waves + gw - 1;
+    for (unsigned spins = 0; __hip_atomic_load(p.xflag + slot, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0u;) {
+      if (++spins > (1u << 22)) break;  // bounded: never hang the GPU (the flag is set C - S steps early)
+      __builtin_amdgcn_s_sleep(8);
+    }
+    const float* src = p.xfer + slot * XW;
 #pragma unroll
     for (int k = 0; k < D; ++k) x[k] = src[k * 64 + lane];
     rng.s0 = __float_as_uint(src[(D + 0) * 64 + lane]);
@@ -541,14 +541,17 @@ em_sampler_kernel(SamplerParams p) {
     }
   }
 
-  if (sg.kind == 1) {  // hand the tile over to wave w + 1
-    float* dst = handoff + (size_t)w * SL::HANDOFF_WORDS * 64;
+  if (sg.kind == 1) {  // hand the tile over to the next wave of the grid
+    const size_t slot = (size_t)yi * n_waves + gw;
+    float* dst = p.xfer + slot * XW;
 #pragma unroll
     for (int k = 0; k < D; ++k) dst[k * 64 + lane] = x[k];
     dst[(D + 0) * 64 + lane] = __uint_as_float(rng.s0);
     dst[(D + 1) * 64 + lane] = __uint_as_float(rng.s1);
     dst[(D + 2) * 64 + lane] = __uint_as_float(rng.s2);
     dst[(D + 3) * 64 + lane] = __uint_as_float(rng.s3);
+    __threadfence();  // every lane's state is visible device-wide before the flag
+    if (lane == 0) __hip_atomic_store(p.xflag + slot, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   } else if (sg.kind != 3 && valid && h == 0) {
     float* dst = p.x_out + ((size_t)yi * p.n_chains + c_local) * D;
 #pragma unroll
@@ -725,8 +728,7 @@ __global__ void schedule_kernel(int S, float T, float bmin, float bdiff, float* 
 // workgroups per y: enough to fill every CU slot once (the kernel balances the work inside a
 // workgroup), never more than one per NW tiles
 template <typename Kern>
-static unsigned sampler_wgs_per_y(Kern kern, int nthreads, long long n_chains, int n_y, bool balance = true) {
-  if (!balance) return (unsigned)((((n_chains + 31) / 32) + nthreads / 64 - 1) / (nthreads / 64));
+static unsigned sampler_wgs_per_y(Kern kern, int nthreads, long long n_chains, int n_y) {
   static int slots = -1;  // one value per kernel instantiation
   if (slots < 0) {
     int dev = 0, n_cu = 256, per_cu = 1;
@@ -743,11 +745,25 @@ static unsigned sampler_wgs_per_y(Kern kern, int nthreads, long long n_chains, i
   return (unsigned)g;
 }
 
+// the hand-over buffers of a launch: per y and grid wave, the state words and a flag (zeroed)
+static hipError_t with_xfer(SamplerParams& p, const dim3& grid, int nw, int d, hipStream_t st, char** buf) {
+  const size_t slots = (size_t)grid.x * grid.y * nw;
+  const size_t state_bytes = slots * sampler_xfer_words(d) * sizeof(float);
+  hipError_t e = hipMallocAsync((void**)buf, state_bytes + slots * sizeof(unsigned), st);
+  if (e != hipSuccess) return e;
+  p.xfer = (float*)*buf;
+  p.xflag = (unsigned*)(*buf + state_bytes);
+  return hipMemsetAsync(p.xflag, 0, slots * sizeof(unsigned), st);
+}
+
 template <int MODE, int W, int NL, int D, int M, int NW, int R, bool RES>
-static hipError_t launch_sampler_t(const SamplerParams& p, int n_y, hipStream_t st) {
-  const dim3 grid(sampler_wgs_per_y(em_sampler_kernel<MODE, W, NL, D, M, NW, R, RES, false>, NW * 64, p.n_chains, n_y,
-                                    SamplerLds<MODE, W, NL, D, M, NW, R, RES>::BALANCE),
+static hipError_t launch_sampler_t(const SamplerParams& p_in, int n_y, hipStream_t st) {
+  const dim3 grid(sampler_wgs_per_y(em_sampler_kernel<MODE, W, NL, D, M, NW, R, RES, false>, NW * 64, p_in.n_chains, n_y),
                   (unsigned)n_y);
+  SamplerParams p = p_in;
+  char* buf = nullptr;
+  hipError_t e = with_xfer(p, grid, NW, D, st, &buf);
+  if (e != hipSuccess) return e;
   if constexpr (MODE == MODE_CDE) {
     if (p.stamps)
       hipLaunchKernelGGL((em_sampler_kernel<MODE, W, NL, D, M, NW, R, RES, false, true>), grid, dim3(NW * 64), 0, st, p);
@@ -758,7 +774,9 @@ static hipError_t launch_sampler_t(const SamplerParams& p, int n_y, hipStream_t 
   } else {
     hipLaunchKernelGGL((em_sampler_kernel<MODE, W, NL, D, M, NW, R, RES, false>), grid, dim3(NW * 64), 0, st, p);
   }
-  return hipGetLastError();
+  e = hipGetLastError();
+  (void)hipFreeAsync(buf, st);
+  return e;
 }
 
 template <int W, int NL, int IN, int NW, int R, bool RES, bool SPLIT = true>
@@ -798,36 +816,35 @@ static int sampler_variant() {
   return e ? atoi(e) : 0;
 }
 
-hipError_t launch_sampler(const SamplerParams& p, int mode, int width, int n_hidden, int xdim, int ydim, int n_y,
+hipError_t launch_sampler(const SamplerParams& p_in, int mode, int width, int n_hidden, int xdim, int ydim, int n_y,
                           hipStream_t st, bool* supported) {
   *supported = true;
   const int var = sampler_variant();
-  const auto variant_grid = [&]() {
-    return dim3(sampler_wgs_per_y(em_sampler_kernel<MODE_CDE, 256, 3, 3, 0, 8, 4, false, false>, 512, p.n_chains, n_y),
-                (unsigned)n_y);
-  };
-  if (mode == MODE_CDE && width == 256 && n_hidden == 3 && xdim == 3 && var >= 101 && var <= 107) {
-    const dim3 grid = variant_grid();
-    switch (var - 100) {
+  if (mode == MODE_CDE && width == 256 && n_hidden == 3 && xdim == 3 &&
+      ((var >= 101 && var <= 107) || (var >= 201 && var <= 203))) {
+    const dim3 grid(sampler_wgs_per_y(em_sampler_kernel<MODE_CDE, 256, 3, 3, 0, 8, 4, false, false>, 512,
+                                      p_in.n_chains, n_y),
+                    (unsigned)n_y);
+    SamplerParams p = p_in;
+    char* buf = nullptr;
+    hipError_t e = with_xfer(p, grid, 8, 3, st, &buf);
+    if (e != hipSuccess) return e;
+    switch (var) {
 #define DG(d) \
-  case d: hipLaunchKernelGGL((em_sampler_kernel<MODE_CDE, 256, 3, 3, 0, 8, 4, false, false, false, d>), grid, dim3(512), 0, st, p); break;
+  case 100 + d: hipLaunchKernelGGL((em_sampler_kernel<MODE_CDE, 256, 3, 3, 0, 8, 4, false, false, false, d>), grid, dim3(512), 0, st, p); break;
       DG(1) DG(2) DG(3) DG(4) DG(5) DG(6) DG(7)
 #undef DG
-      default: break;
-    }
-    return hipGetLastError();
-  }
-  if (mode == MODE_CDE && width == 256 && n_hidden == 3 && xdim == 3 && var >= 201 && var <= 203) {
-    const dim3 grid = variant_grid();
-    switch (var - 200) {
 #define TG(t) \
-  case t: hipLaunchKernelGGL((em_sampler_kernel<MODE_CDE, 256, 3, 3, 0, 8, 4, false, false, false, 0, t>), grid, dim3(512), 0, st, p); break;
+  case 200 + t: hipLaunchKernelGGL((em_sampler_kernel<MODE_CDE, 256, 3, 3, 0, 8, 4, false, false, false, 0, t>), grid, dim3(512), 0, st, p); break;
       TG(1) TG(2) TG(3)
 #undef TG
       default: break;
     }
-    return hipGetLastError();
+    e = hipGetLastError();
+    (void)hipFreeAsync(buf, st);
+    return e;
   }
+  const SamplerParams& p = p_in;
 #define X(MODEv, Wv, NLv, Dv, Mv, NWv, Rv, RESv)                                                  \
   if (mode == MODEv && width == Wv && n_hidden == NLv && xdim == Dv && (Mv == 0 || ydim == Mv)) \
     return launch_sampler_t<MODEv, Wv, NLv, Dv, Mv, NWv, Rv, RESv>(p, n_y, st);
