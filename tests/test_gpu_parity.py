@@ -580,3 +580,37 @@ def test_balanced_schedule_matches_unsplit_runs(dmip, golden, n, S):
         part = m.sample_device(y, k, S, seed=13, chain_offset=lo)[0]
         assert torch.equal(full[lo:lo + k], part), lo
     assert torch.isfinite(full).all()
+
+
+def test_balanced_schedule_injected_noise_vs_oracle(dmip, golden):
+    """Noise injection through the split-tile schedule (70,001 chains > one round): every checked
+    chain equals an unsplit run fed the same normals (bit-exact) and follows the oracle."""
+    ck = golden("ckpt_scat.npz")
+    m = _cde(dmip, "scat", ck, "")
+    y = golden("data_scat.npz")["y_test"][2]
+    n, S = 70001, 50
+    g = np.random.default_rng(17)
+    noise = torch.from_numpy(g.normal(size=(S + 1, 1, n, 3)).astype(np.float32)).to(DEV)
+    yd = torch.from_numpy(y).to(DEV)
+    out = m.sample_device(yd, n, S, noise=noise)[0]
+    params = O.mlp_params_from_state(ck)
+    for lo in (0, 35000, n - 64):
+        sl = slice(lo, lo + 64)
+        part = m.sample_device(yd, 64, S, chain_offset=lo, noise=noise[:, :, sl].contiguous())[0]
+        assert torch.equal(out[sl], part), lo
+        nz = noise[:, 0, sl].cpu().numpy()
+        ref = O.em_sample(lambda x, tau: O.cde_a(params, x, y, tau), nz[0], S, noise=nz[1:])
+        # bf16 network vs the fp32 oracle over 50 steps: the injected-trajectory tolerance (5 %)
+        assert np.abs(out[sl].cpu().numpy() - ref).max() < 0.05 * max(1.0, np.abs(ref).max())
+
+
+@pytest.mark.parametrize("cls", ["PosteriorDiffusionEstimator", "CDiffE"])
+def test_balanced_schedule_other_samplers(dmip, cls):
+    torch.manual_seed(21)
+    m = getattr(dmip, cls)(3, 23, [256] * 3)
+    y = torch.from_numpy(np.random.default_rng(2).uniform(0, 1, 23).astype(np.float32)).to(DEV)
+    n, S = 70001, 5
+    full = m.sample_device(y, n, S, seed=3)[0]
+    for lo in (0, 40000, n - 500):
+        part = m.sample_device(y, 500, S, seed=3, chain_offset=lo)[0]
+        assert torch.equal(full[lo:lo + 500], part), lo
