@@ -89,3 +89,73 @@ def fused_loss_grad(model, loss_fn, cfg, x, y, t, eps):
     if cfg.kind == _lib.DMIP_LOSS_PINN:
         return loss, {'PDE-Loss': pde, 'Initial Condition': ic, 'DSM-Loss': dsm}
     return loss, {'PDE-Loss': pde, 'Initial Condition': ic, 'DSM_eval': dsm}
+
+
+# ------------------------------------------------------------------ training drivers
+class _Log:
+    """torch SummaryWriter when tensorboard is installed, else JSON lines in log_dir/train_log.jsonl
+    (same scalar tags: 'Train/Loss', 'Train/<component>')."""
+
+    def __init__(self, log_dir):
+        self.w, self.f = None, None
+        try:
+            from torch.utils.tensorboard import SummaryWriter
+            self.w = SummaryWriter(log_dir)
+        except Exception:
+            if log_dir:
+                os.makedirs(log_dir, exist_ok=True)
+                self.f = open(os.path.join(log_dir, 'train_log.jsonl'), 'a')
+
+    def add_scalar(self, tag, value, step):
+        value = float(value)
+        if self.w is not None:
+            self.w.add_scalar(tag, value, step)
+        elif self.f is not None:
+            import json
+            self.f.write(json.dumps({"tag": tag, "value": value, "step": int(step)}) + "\n")
+
+    def close(self):
+        if self.f is not None:
+            self.f.close()
+
+
+def _epochs(model, optim, loss_fn, loader_fn, num_epochs, log, step_offset=0):
+    for i in range(num_epochs):
+        loss, logger_info = model.train_epoch(optim, loss_fn, loader_fn())
+        log.add_scalar('Train/Loss', loss, i + step_offset)
+        for key, value in logger_info.items():
+            log.add_scalar('Train/' + key, value, i + step_offset)
+
+
+def train_linear(model, optim, loss_fn, forward_model_params, save_dir, log_dir, num_epochs, batch_size, xs, ys,
+                 resume_training=False):
+    """main_diffusion_linear.py:19-51 `train`: per epoch a shuffled loader with fresh observation noise
+    (datasets.py:44-54), `model.train_epoch`, scalar logging (steps offset by 5000 when resuming, as the
+    reference logs them); the state_dict goes to save_dir/current_model.pt."""
+    from .problems import get_dataloader_linear
+    model.sde.train()
+    log = _Log(log_dir)
+    _epochs(model, optim, loss_fn,
+            lambda: get_dataloader_linear(xs, ys, forward_model_params['scale'], batch_size),
+            num_epochs, log, 5000 if resume_training else 0)
+    log.close()
+    os.makedirs(save_dir, exist_ok=True)
+    torch.save(model.sde.a.state_dict(), os.path.join(save_dir, 'current_model.pt'))
+    return model
+
+
+def train_scatterometry(model, optimizer, loss_fn, forward_model_params, save_dir, log_dir, num_epochs, batch_size,
+                        forward_model):
+    """main_diffusion_scatterometry.py:19-38 `train`: per epoch 8 batches of prior samples pushed
+    through the surrogate with fresh noise (datasets.py:26-34); the state_dict goes to
+    save_dir/diffusion.pt."""
+    from .problems import get_dataloader_scatterometry
+    log = _Log(log_dir)
+    _epochs(model, optimizer, loss_fn,
+            lambda: get_dataloader_scatterometry(batch_size, forward_model, forward_model_params['a'],
+                                                 forward_model_params['b'], forward_model_params['lambd_bd']),
+            num_epochs, log)
+    log.close()
+    os.makedirs(save_dir, exist_ok=True)
+    torch.save(model.sde.a.state_dict(), os.path.join(save_dir, 'diffusion.pt'))
+    return model
