@@ -159,15 +159,28 @@ __device__ __forceinline__ float act_t_twice(float zs) {
   return __builtin_copysignf(__builtin_fmaf(-e, q, q), zs);
 }
 
+// two f32 -> one dword of two bf16 (v_cvt_pk_bf16_f32, round to nearest even; a in the low half).
+// Converting explicit pairs keeps the packed conversion without letting the SLP vectoriser also
+// fuse the neighbouring scalar FMAs into v_pk_fma_f32 (a measured anti-lever beside MFMAs).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{a, b}, bf16x2));
+}
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
 template <bool TWICE, bool CAST_ONLY = false>
 __device__ __forceinline__ void act_pack(const f32x16& acc, bf16x8& lo, bf16x8& hi) {
+  auto act = [](float z) { return CAST_ONLY ? z : (TWICE ? act_t_twice(z) : act_r(z)); };
+  u32x4 l, h;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const float a = CAST_ONLY ? acc[j] : (TWICE ? act_t_twice(acc[j]) : act_r(acc[j]));
-    const float b = CAST_ONLY ? acc[8 + j] : (TWICE ? act_t_twice(acc[8 + j]) : act_r(acc[8 + j]));
-    lo[j] = (__bf16)a;
-    hi[j] = (__bf16)b;
+  for (int i = 0; i < 4; ++i) {
+    l[i] = cvt_pk_bf16(act(acc[2 * i]), act(acc[2 * i + 1]));
+    h[i] = cvt_pk_bf16(act(acc[8 + 2 * i]), act(acc[8 + 2 * i + 1]));
   }
+  lo = __builtin_bit_cast(bf16x8, l);
+  hi = __builtin_bit_cast(bf16x8, h);
 }
 
 // ------------------------------------------------------------------------ sync primitives
