@@ -89,24 +89,35 @@ struct Engine {
   long long gc;  // global chunk counter (ring mode)
   int w, lane;
 
-  __device__ __forceinline__ void ring_issue(long long g) {
-    // chunk index and network select stay scalar (the counter is wave-uniform; the segment loop of
-    // the balanced sampler hides that from the divergence analysis)
-    const int c = __builtin_amdgcn_readfirstlane((int)(g % L::NCT));
-    const char* src = (c < L::NC ? hidden[0] : hidden[1]) + (size_t)(c % L::NC) * L::CHUNK;
-    char* dst = lds + L::W_OFF + (int)(g % R) * L::CHUNK;
+  // Every network evaluation streams exactly NCT chunks, so when NCT % R == 0 the k-th chunk of an
+  // evaluation always sits in slot k % R: with k a compile-time constant after unrolling, every ring
+  // address is a constant offset (no per-chunk 64-bit counter arithmetic: that was ~30 scalar
+  // instructions per chunk, issued by all waves at once right after the barrier).
+  static constexpr bool STATIC_RING = (L::NCT % R) == 0;
+
+  // issue chunk c (in [0, NCT)) of the evaluation into ring slot `slot`
+  __device__ __forceinline__ void ring_issue_at(int c, int slot) {
+    // opaque wave-uniform base, re-materialised at every issue: otherwise the compiler hoists every
+    // chunk's 64-bit source address out of the step loop and holds them all in registers (2 VGPRs
+    // per chunk with a per-lane address, 2 SGPRs -- spilled to VGPR lanes -- with a constant one)
+    const char* base = c < L::NC ? hidden[0] : hidden[1];
+    asm volatile("" : "+s"(base));
+    char* dst = lds + L::W_OFF + slot * L::CHUNK;
 #pragma unroll
     for (int q = 0; q < PPW; ++q) {
       const int piece = w * PPW + q;
-      // opaque wave-uniform base: otherwise the compiler hoists every chunk's 64-bit per-lane source
-      // address out of the step loop and holds them all in VGPRs (2 per chunk)
-      const char* g = src + piece * 1024;
-      asm volatile("" : "+s"(g));
-      glds16(g, dst + piece * 1024, lane);
+      glds16(base + (size_t)(c % L::NC) * L::CHUNK + piece * 1024, dst + piece * 1024, lane);
     }
   }
 
-  __device__ __forceinline__ const char* chunk_sync() {
+  __device__ __forceinline__ void ring_issue(long long g) {
+    // chunk index and network select stay scalar (the counter is wave-uniform; the segment loop of
+    // the balanced sampler hides that from the divergence analysis)
+    ring_issue_at(__builtin_amdgcn_readfirstlane((int)(g % L::NCT)), __builtin_amdgcn_readfirstlane((int)(g % R)));
+  }
+
+  // k: index of the chunk within the current network evaluation (a constant after unrolling)
+  __device__ __forceinline__ const char* chunk_sync(int k) {
     if constexpr (DIAG & 1) {
       asm volatile("" ::: "memory");
       return lds + L::W_OFF + (int)((gc++) % R) * L::CHUNK;
@@ -114,10 +125,15 @@ struct Engine {
       if constexpr (CONSERVATIVE) wait_vmcnt<0>();
       else wait_vmcnt<(R - 2) * PPW>();
       lds_barrier();
-      ring_issue(gc + R - 1);
-      const char* slot = lds + L::W_OFF + (int)(gc % R) * L::CHUNK;
-      ++gc;
-      return slot;
+      if constexpr (STATIC_RING) {
+        ring_issue_at((k + R - 1) % L::NCT, (k + R - 1) % R);
+        return lds + L::W_OFF + (k % R) * L::CHUNK;
+      } else {
+        ring_issue(gc + R - 1);
+        const char* slot = lds + L::W_OFF + (int)(gc % R) * L::CHUNK;
+        ++gc;
+        return slot;
+      }
     }
   }
 
@@ -143,7 +159,7 @@ struct Engine {
         asm volatile("" ::: "memory");
         wb = lds + L::W_OFF + ((NI * (NL - 1) + LI) * T + rt) * L::CHUNK;
       } else {
-        wb = chunk_sync();
+        wb = chunk_sync((NI * (NL - 1) + LI) * T + rt);
       }
       if constexpr (SPLIT) {
         if (w >= NW / 2) {  // activation first
