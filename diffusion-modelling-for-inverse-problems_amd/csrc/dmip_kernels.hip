@@ -54,18 +54,46 @@ __device__ __forceinline__ void stage_floats(float* lds, const float* g, int n, 
 }
 
 // acc += sum_s A[s] * H[s] over one 32-row tile: A fragments streamed from LDS (1 KiB apart)
-// with an explicit prefetch distance of PF reads, so the MFMA chain does not wait on each
-// fragment's LDS latency.
-template <int KS, int PF = 3>
-__device__ __forceinline__ void mfma_row_tile(const char* a_lane, const bf16x8 (&H)[KS], f32x16& acc) {
-  bf16x8 a[PF + 1];
-#pragma unroll
-  for (int s = 0; s < PF && s < KS; ++s) a[s] = *(const bf16x8*)(a_lane + s * 1024);
-#pragma unroll
-  for (int s = 0; s < KS; ++s) {
-    if (s + PF < KS) a[(s + PF) % (PF + 1)] = *(const bf16x8*)(a_lane + (s + PF) * 1024);
-    acc = mfma32(a[s % (PF + 1)], H[s], acc);
+// with PF reads kept in flight, so the MFMA chain does not wait on each fragment's LDS latency.
+// The reads and their counted waits are explicit: left to itself the compiler (at ~234 VGPRs)
+// schedules each read right before its MFMA behind an lgkmcnt(0), which exposes the full LDS
+// latency on every MFMA. A wait names the fragment it guards ("+v"), so the MFMA that uses the
+// fragment cannot be scheduled above it. Younger LDS operations the compiler adds in between only
+// make a counted wait stricter (LDS returns in order).
+typedef __attribute__((address_space(3))) const char* lds_cptr;
+
+template <int OFF>
+__device__ __forceinline__ bf16x8 lds_read_b128(lds_cptr p) {
+  bf16x8 r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(p), "i"(OFF));
+  return r;
+}
+
+template <int N>
+__device__ __forceinline__ void lds_wait(bf16x8& guarded) {
+  asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(guarded) : "i"(N));
+}
+
+template <int KS, int PF, int S = 0>
+__device__ __forceinline__ void mfma_chain(lds_cptr a_lane, const bf16x8 (&H)[KS], f32x16& acc, bf16x8 (&a)[PF + 1]) {
+  if constexpr (S < KS) {
+    if constexpr (S + PF < KS) a[(S + PF) % (PF + 1)] = lds_read_b128<(S + PF) * 1024>(a_lane);
+    constexpr int younger = (KS - 1 - S) < PF ? (KS - 1 - S) : PF;  // reads issued after fragment S
+    lds_wait<younger>(a[S % (PF + 1)]);
+    acc = mfma32(a[S % (PF + 1)], H[S], acc);
+    mfma_chain<KS, PF, S + 1>(a_lane, H, acc, a);
   }
+}
+
+template <int KS, int PF = 3>
+__device__ __forceinline__ void mfma_row_tile(const char* a_lane_g, const bf16x8 (&H)[KS], f32x16& acc) {
+  const lds_cptr a_lane = (lds_cptr)a_lane_g;
+  bf16x8 a[PF + 1];
+  if constexpr (PF >= 1) a[0] = lds_read_b128<0>(a_lane);
+  if constexpr (PF >= 2 && KS > 1) a[1] = lds_read_b128<1024>(a_lane);
+  if constexpr (PF >= 3 && KS > 2) a[2] = lds_read_b128<2048>(a_lane);
+  static_assert(PF >= 1 && PF <= 3, "prefetch depth");
+  mfma_chain<KS, PF>(a_lane, H, acc, a);
 }
 
 // ------------------------------------------------------------------- network evaluation engine
