@@ -68,6 +68,33 @@ def pmc_traffic(kernel_match="em_sampler"):
     return z["hbm_bytes_per_launch"]
 
 
+def ks_vs_reference(x, num_steps, weights):
+    """Per-dimension two-sample KS statistic of the timed run's samples against the reference
+    sampler's own stored draws (tests/golden/samples_scat.npz: 20k of a 100k-chain run of the
+    reference's models/diffusion.py:27-46 loop, same y and the same fixture weights), with the
+    alpha = 0.01 critical value. The 'KS vs ref' half of BASELINE.json's metric; computed after
+    the timed region. None when the weights or the step count differ from the fixture's."""
+    p = os.path.join(ROOT, "tests", "golden", "samples_scat.npz")
+    if not os.path.exists(p) or not weights.startswith("fixture"):
+        return None
+    z = np.load(p)
+    if int(z["num_steps"]) != num_steps:
+        return None
+    ref = np.sort(z["samples"].astype(np.float64), axis=0)
+    x = np.sort(np.asarray(x, np.float64), axis=0)
+    stats = []
+    for k in range(ref.shape[1]):
+        both = np.concatenate([x[:, k], ref[:, k]])
+        ca = np.searchsorted(x[:, k], both, side="right") / x.shape[0]
+        cb = np.searchsorted(ref[:, k], both, side="right") / ref.shape[0]
+        stats.append(float(np.max(np.abs(ca - cb))))
+    n1, n2 = x.shape[0], ref.shape[0]
+    crit = 1.63 * float(np.sqrt((n1 + n2) / (n1 * n2)))
+    return {"stat": stats, "crit_alpha_0.01": crit, "pass": bool(max(stats) < crit),
+            "n_samples": n1, "n_ref": n2,
+            "ref": "reference sampler's own draws (tests/golden/samples_scat.npz, same y, same weights)"}
+
+
 def cpu_baseline(num_steps, n_chains):
     """Reference-order torch-CPU sampler (oracle/torch_cpu.py) on a bounded sample."""
     from oracle import torch_cpu
@@ -139,9 +166,10 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    x_last = None
     for i in range(args.steps):
         ev[i][0].record(stream)
-        model.sample_device(y, n_local, S, seed=i, chain_offset=lo) if world == 1 else one_step(i)
+        x_last = model.sample_device(y, n_local, S, seed=i, chain_offset=lo) if world == 1 else one_step(i)
         ev[i][1].record(stream)
     torch.cuda.synchronize()
     if world > 1:
@@ -180,6 +208,8 @@ def main():
                      "kernel": "em_sampler_kernel<256,3,3,8,4> (+a1_prep, inside the events)",
                      "launch_ms": launch_ms, "flops_per_launch": flops_launch},
     }
+    if rank == 0:
+        line["ks_vs_ref"] = ks_vs_reference(x_last.reshape(-1, XDIM).cpu().numpy(), S, weights)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(S, args.cpu_chains)
     if rank == 0:

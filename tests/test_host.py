@@ -202,3 +202,23 @@ def test_training_drivers_write_reference_checkpoints(dmip, tmp_path):
     tr.train_scatterometry(ms, opt, dmip.DSMLoss(), dict(pr.SCAT_PARAMS), str(tmp_path / "scat"),
                            str(tmp_path / "log2"), 1, 50, fm)
     assert (tmp_path / "scat" / "diffusion.pt").exists()
+
+
+def test_bench_ks_vs_reference_field(golden):
+    """bench.py's `ks_vs_ref` (the KS half of BASELINE.json's metric) agrees with the oracle's
+    two-sample KS, is 0 on the reference's own draws, and fails a shifted posterior."""
+    import importlib
+    import oracle as O
+    bench = importlib.import_module("bench")
+    ref = golden("samples_scat.npz")["samples"]
+    w = "fixture-trained (tests/golden/ckpt_scat.npz)"
+    same = bench.ks_vs_reference(ref, 1000, w)
+    assert same["pass"] and max(same["stat"]) == 0.0
+    rng = np.random.default_rng(0)
+    x = ref[rng.integers(0, ref.shape[0], 50000)] + rng.normal(0, 1e-3, (50000, 3)).astype(np.float32)
+    r = bench.ks_vs_reference(x, 1000, w)
+    for k in range(3):
+        assert abs(r["stat"][k] - O.ks_2samp_stat(x[:, k], ref[:, k])) < 1e-12
+    shifted = bench.ks_vs_reference(ref + 0.2, 1000, w)
+    assert not shifted["pass"]
+    assert bench.ks_vs_reference(ref, 200, w) is None and bench.ks_vs_reference(ref, 1000, "random-init") is None
