@@ -67,3 +67,19 @@ def sample_sharded(model, y, num_samples, num_steps, mean, std, seed=None, **sam
     local = model.sample_device(y, hi - lo, num_steps, mean, std, seed=seed, chain_offset=lo, **sampler_kwargs)
     full = gather_shards(local, num_samples, dev)
     return full[0] if torch.as_tensor(y).ndim == 1 else full
+
+
+def map_sharded(n, fn, width):
+    """Evaluate-style multi-y runs (shard over (y, chain) pairs): rank r computes
+    `fn(i)` -> `width` floats for its contiguous range of the n items (each item = one y with all
+    its repeats in one sampler launch), and every rank receives the (n, width) float64 table in
+    item order. One all_gather of n * width floats at the end; nothing per step."""
+    import numpy as np
+    rank, ws = world()
+    lo, hi = shard_range(n, rank, ws)
+    rows = [np.asarray(fn(i), dtype=np.float64).reshape(width) for i in range(lo, hi)]
+    local = torch.from_numpy(np.stack(rows) if rows else np.zeros((0, width)))
+    if ws == 1:
+        return local.numpy()
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+    return gather_shards(local[None].to(dev), n, dev)[0].cpu().numpy()

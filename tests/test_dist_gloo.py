@@ -67,3 +67,48 @@ def test_sharded_sampling_gathers_full_run(world, n):
     assert len(set(ref[:, 1].tolist())) == 1                 # one seed for the whole run
     for r in range(1, world):
         assert (res[r] == ref).all()
+
+
+def _map_worker(rank, world, port, n, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import importlib
+    par = importlib.import_module("diffusion-modelling-for-inverse-problems_amd.parallel")
+    seen = []
+
+    def fn(i):  # one y of an evaluate driver: its metric row (a pure function of i)
+        seen.append(i)
+        return [i, i * 0.5, -float(i) ** 2, rank]
+
+    out = par.map_sharded(n, fn, 4)
+    q.put((rank, out, seen))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n", [(2, 7), (3, 2), (2, 1)])
+def test_map_sharded_evaluate_rows(world, n):
+    """evaluate_* under world_size > 1 (parallel.map_sharded): every y is scored by exactly one rank,
+    and all ranks receive the full per-y metric table in y order."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if root not in sys.path:
+        sys.path.insert(0, root)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_map_worker, args=(r, world, port, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {r: (out, seen) for r, out, seen in (q.get(timeout=120) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    owned = sorted(i for _, seen in res.values() for i in seen)
+    assert owned == list(range(n))  # each y exactly once over all ranks
+    ref = res[0][0]
+    assert ref.shape == (n, 4) and ref.dtype.name == "float64"
+    assert (ref[:, 0] == list(range(n))).all() and (ref[:, 2] == -ref[:, 0] ** 2).all()
+    for r in range(world):
+        assert (res[r][0] == ref).all()
+        assert all(ref[i, 3] == r for i in res[r][1])  # row i came from the rank that owned y i
