@@ -535,7 +535,7 @@ int dmip_loss_grad(int in_dim, int out_dim, int n_hidden, const int* widths, int
   for (int i = 0; i < 4; ++i) p.icA[i] = cfg->ic_A[i], p.icS[i] = cfg->ic_Sinv[i];
   p.icb[0] = cfg->ic_b[0];
   p.icb[1] = cfg->ic_b[1];
-  // one 2-wave workgroup per CU (LDS-bound), 16-sample tiles strided over the waves
+  // one workgroup per CU (LDS-bound; one wave per SIMD), 16-sample tiles strided over the waves
   int n_cu = 256;
   {
     int dev = 0;
@@ -548,10 +548,14 @@ int dmip_loss_grad(int in_dim, int out_dim, int n_hidden, const int* widths, int
   const int64_t per_wg = dmip::train_waves_per_wg();
   int n_wg = (int)std::min<int64_t>((int64_t)n_cu, (tiles + per_wg - 1) / per_wg);
   if (n_wg < 1) n_wg = 1;
-  const size_t part_bytes = (size_t)n_wg * dmip::train_partial_stride(n_hidden) * sizeof(float);
+  const size_t part_bytes =
+      (size_t)n_wg * dmip::train_partials_per_wg() * dmip::train_partial_stride(n_hidden) * sizeof(float);
+  // one scratch allocation: the partial rows, then the packed LDS image of the weights
+  const size_t part_pad = (part_bytes + 255) / 256 * 256;
   float* partials = nullptr;
-  hipError_t e = hipMallocAsync((void**)&partials, part_bytes, st);
+  hipError_t e = hipMallocAsync((void**)&partials, part_pad + (size_t)dmip::train_packed_bytes(n_hidden), st);
   if (e != hipSuccess) return fail(DMIP_ERR_ALLOC, std::string("hipMallocAsync: ") + hipGetErrorString(e));
+  p.packed = (char*)partials + part_pad;
   e = dmip::launch_loss_grad(p, n_hidden, grad_out_dev, loss_out_dev, partials, n_wg, st);
   (void)hipFreeAsync(partials, st);
   if (e != hipSuccess) return hip_fail(e, "loss_grad launch");

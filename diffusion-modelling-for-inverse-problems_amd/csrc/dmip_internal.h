@@ -79,11 +79,14 @@ struct TrainParams {
   float lam, lam2;
   float icA[4], icb[2], icS[4];  // linear-problem IC target: -x + ((y - (A x + b)) S^T) A
   float* partials;            // [n_waves][partial stride]
+  char* packed;               // the shared LDS image of the weight fragments (written by the pack kernel)
 };
 
 int train_nparam(int n_hidden);
 int train_partial_stride(int n_hidden);
 int train_waves_per_wg();
+int train_partials_per_wg();
+int train_packed_bytes(int n_hidden);
 hipError_t launch_loss_grad(const TrainParams& p, int n_hidden, float* grads, float* loss_out, float* partials,
                             int n_wg, hipStream_t st);
 

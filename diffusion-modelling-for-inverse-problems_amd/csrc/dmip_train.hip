@@ -42,7 +42,14 @@ constexpr int D = kTrainXdim;   // xdim
 constexpr int M = kTrainYdim;   // ydim
 constexpr int IN = D + M + 1;   // cat[x, y, t] (nets.py:33)
 constexpr int OUT = D;          // CDE drift
-constexpr int NWV = 2;          // waves per workgroup
+#ifndef DMIP_TRAIN_NWV
+#define DMIP_TRAIN_NWV 4
+#endif
+// waves per workgroup: 4 = one wave on each SIMD of the CU, with the per-wave gradient partial in
+// global memory (its own row of `partials`, L2/MALL-resident); 2 = the partial in LDS, which limits
+// the workgroup to 2 waves (2 of 4 SIMDs) by its 158 KiB of LDS
+constexpr int NWV = DMIP_TRAIN_NWV;
+constexpr bool GACC_GLOBAL = NWV > 2;
 constexpr int NS = 16;          // samples per tile
 constexpr int NSTREAM = 8;      // P, V, C, E0, E1, E00, E01, E11
 static_assert(W == 64 && D == 2, "compiled for the linear problem's width-64 CDE");
@@ -65,8 +72,8 @@ struct TL {
   static constexpr int BIAS = AOT + 4096;                // fp32 [NL + 1][64]: b_l of hidden l, b_out at NL
   static constexpr int COL = BIAS + (NL + 1) * W * 4;    // fp32 [D][64]: layer-1 weight columns of x
   static constexpr int WAVE = COL + D * W * 4;
-  static constexpr int GACC = 0;                         // per wave: fp32 gradient partial (param order)
-  static constexpr int SCR = ((PART * 4 + 15) / 16) * 16;    // per wave: 6 transposed [64][16] bf16
+  static constexpr int GACC = 0;                         // per wave: fp32 gradient partial (param order, LDS mode)
+  static constexpr int SCR = GACC_GLOBAL ? 0 : ((PART * 4 + 15) / 16) * 16;  // per wave: 6 transposed [64][16] bf16
   static constexpr int WAVE_BYTES = SCR + 6 * W * NS * 2;
   static constexpr int TOTAL = WAVE + NWV * WAVE_BYTES;
   static_assert(TOTAL <= 160 * 1024, "LDS budget");
@@ -157,22 +164,17 @@ __device__ __forceinline__ bf16x8 tread(const __bf16* scr, int row, bool ok, int
   return *(const bf16x8*)(scr + row * NS + 8 * hh);
 }
 
+// The shared part of the LDS image (weight fragments, biases, layer-1 columns), packed ONCE per
+// launch into a global buffer by train_pack_kernel; every workgroup then copies it into LDS with
+// coalesced 16-byte loads (instead of each workgroup converting the fp32 weights with strided reads).
 template <int NL>
-__global__ void __launch_bounds__(NWV * 64, 1) loss_grad_kernel(TrainParams p) {
+__device__ __forceinline__ void pack_weights(const TrainParams& p, char* base, int tid, int nth) {
   using L = TL<NL>;
-  __shared__ __attribute__((aligned(16))) char lds[L::TOTAL];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int c16 = lane & 15, g = lane >> 4;
-  const int i32 = lane & 31, hh = lane >> 5;
-
-  // ---- pack the weights (fp32 device params, nn.Linear layout) into LDS fragments
   {
-    __bf16* wf = (__bf16*)(lds + L::WF);
-    __bf16* wfl = (__bf16*)(lds + L::WFL);
-    __bf16* wt = (__bf16*)(lds + L::WT);
-    for (int e = tid; e < (NL - 1) * 4096; e += NWV * 64) {
+    __bf16* wf = (__bf16*)(base + L::WF);
+    __bf16* wfl = (__bf16*)(base + L::WFL);
+    __bf16* wt = (__bf16*)(base + L::WT);
+    for (int e = tid; e < (NL - 1) * 4096; e += nth) {
       const int l = e / 4096, r0 = e % 4096;
       const int R = r0 / 1024, s = (r0 / 512) & 1, ln = (r0 / 8) & 63, j = r0 & 7;
       const int row = 16 * R + (ln & 15), k = kp(s, ln >> 4, j);
@@ -181,8 +183,8 @@ __global__ void __launch_bounds__(NWV * 64, 1) loss_grad_kernel(TrainParams p) {
       wfl[e] = bf_lo(Wl[row * W + k]);
       wt[e] = (__bf16)Wl[k * W + row];
     }
-    __bf16* a1 = (__bf16*)(lds + L::A1);
-    for (int e = tid; e < 2048; e += NWV * 64) {
+    __bf16* a1 = (__bf16*)(base + L::A1);
+    for (int e = tid; e < 2048; e += nth) {
       const int R = e / 512, ln = (e / 8) & 63, j = e & 7;
       const int row = 16 * R + (ln & 15), k = 8 * (ln >> 4) + j;
       const float* W0 = p.w[0] + row * IN;
@@ -194,33 +196,63 @@ __global__ void __launch_bounds__(NWV * 64, 1) loss_grad_kernel(TrainParams p) {
       else if (k == 3 * IN + 1) o = bf_lo(p.b[0][row]);
       a1[e] = o;
     }
-    __bf16* ao = (__bf16*)(lds + L::AO);
-    __bf16* aol = (__bf16*)(lds + L::AOL);
-    for (int e = tid; e < 1024; e += NWV * 64) {
+    __bf16* ao = (__bf16*)(base + L::AO);
+    __bf16* aol = (__bf16*)(base + L::AOL);
+    for (int e = tid; e < 1024; e += nth) {
       const int s = e / 512, ln = (e / 8) & 63, j = e & 7;
       const int o = (ln & 15) & 3;
       const float v = o < OUT ? p.w[NL][o * W + kp(s, ln >> 4, j)] : 0.0f;
       ao[e] = bf_hi(v);
       aol[e] = bf_lo(v);
     }
-    __bf16* aot = (__bf16*)(lds + L::AOT);
-    for (int e = tid; e < 2048; e += NWV * 64) {
+    __bf16* aot = (__bf16*)(base + L::AOT);
+    for (int e = tid; e < 2048; e += nth) {
       const int R = e / 512, ln = (e / 8) & 63, j = e & 7;
       const int unit = 16 * R + (ln & 15), k = 8 * (ln >> 4) + j;
       aot[e] = k < OUT ? (__bf16)p.w[NL][k * W + unit] : (__bf16)0.0f;
     }
-    float* bias = (float*)(lds + L::BIAS);
-    for (int e = tid; e < (NL + 1) * W; e += NWV * 64) {
+    float* bias = (float*)(base + L::BIAS);
+    for (int e = tid; e < (NL + 1) * W; e += nth) {
       const int l = e / W, u = e % W;
       float v = 0.0f;
       if (l >= 1 && l < NL) v = p.b[l][u];
       else if (l == NL && u < OUT) v = p.b[NL][u];
       bias[e] = v;
     }
-    float* col = (float*)(lds + L::COL);
-    for (int e = tid; e < D * W; e += NWV * 64) col[e] = p.w[0][(e % W) * IN + e / W];
-    float* gacc = (float*)(lds + L::WAVE + w * L::WAVE_BYTES + L::GACC);
-    for (int e = lane; e < L::PART; e += 64) gacc[e] = 0.0f;
+    float* col = (float*)(base + L::COL);
+    for (int e = tid; e < D * W; e += nth) col[e] = p.w[0][(e % W) * IN + e / W];
+  }
+}
+
+template <int NL>
+__global__ void __launch_bounds__(256) train_pack_kernel(TrainParams p) {
+  pack_weights<NL>(p, p.packed, blockIdx.x * blockDim.x + threadIdx.x, gridDim.x * blockDim.x);
+}
+
+template <int NL>
+__global__ void __launch_bounds__(NWV * 64, 1) loss_grad_kernel(TrainParams p) {
+  using L = TL<NL>;
+  __shared__ __attribute__((aligned(16))) char lds[L::TOTAL];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int c16 = lane & 15, g = lane >> 4;
+  const int i32 = lane & 31, hh = lane >> 5;
+
+  // ---- the shared LDS image (packed once per launch by train_pack_kernel): 16-byte copies
+  {
+    static_assert(L::WAVE % 16 == 0, "LDS image is a whole number of 16-byte pieces");
+    const uint4* src = (const uint4*)p.packed;
+    uint4* dst = (uint4*)lds;
+#pragma unroll 4
+    for (int e = tid; e < L::WAVE / 16; e += NWV * 64) dst[e] = src[e];
+    if constexpr (!GACC_GLOBAL) {
+      float* gacc = (float*)(lds + L::WAVE + w * L::WAVE_BYTES + L::GACC);
+      for (int e = lane; e < L::PART; e += 64) gacc[e] = 0.0f;
+    } else {
+      float* gacc = p.partials + ((size_t)blockIdx.x * NWV + w) * L::PART;
+      for (int e = lane; e < L::PART; e += 64) gacc[e] = 0.0f;
+    }
   }
   __syncthreads();
 
@@ -232,7 +264,7 @@ __global__ void __launch_bounds__(NWV * 64, 1) loss_grad_kernel(TrainParams p) {
   const float* bias = (const float*)(lds + L::BIAS);
   const float* col = (const float*)(lds + L::COL);
   char* wave_base = lds + L::WAVE + w * L::WAVE_BYTES;
-  float* gacc = (float*)(wave_base + L::GACC);
+  float* gacc = GACC_GLOBAL ? p.partials + ((size_t)blockIdx.x * NWV + w) * L::PART : (float*)(wave_base + L::GACC);
   __bf16* scr = (__bf16*)(wave_base + L::SCR);
   auto S_ = [&](int k) { return scr + k * W * NS; };
 
@@ -679,6 +711,7 @@ __global__ void __launch_bounds__(NWV * 64, 1) loss_grad_kernel(TrainParams p) {
     for (int m = 1; m < 64; m <<= 1) v += __shfl_xor(v, m, 64);
     if (lane == 0) gacc[L::NPARAM + k] = v;
   }
+  if constexpr (GACC_GLOBAL) return;  // each wave's row of `partials` is its partial
   // one partial per workgroup: wave 0's region + wave 1's region, in that order (deterministic)
   __syncthreads();
   float* part = p.partials + (size_t)blockIdx.x * L::PART;
@@ -735,12 +768,19 @@ hipError_t launch_loss_grad(const TrainParams& p, int n_hidden, float* grads, fl
   TrainParams q = p;
   q.partials = partials;
   if (n_hidden == 3)
+    hipLaunchKernelGGL(train_pack_kernel<3>, dim3(32), dim3(256), 0, st, q);
+  else
+    hipLaunchKernelGGL(train_pack_kernel<2>, dim3(32), dim3(256), 0, st, q);
+  hipError_t e0 = hipGetLastError();
+  if (e0 != hipSuccess) return e0;
+  if (n_hidden == 3)
     hipLaunchKernelGGL(loss_grad_kernel<3>, dim3(n_wg), dim3(NWV * 64), 0, st, q);
   else
     hipLaunchKernelGGL(loss_grad_kernel<2>, dim3(n_wg), dim3(NWV * 64), 0, st, q);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(loss_grad_reduce_kernel, dim3((nparam + 3 + 63) / 64), dim3(256), 0, st, partials, n_wg, part,
+  hipLaunchKernelGGL(loss_grad_reduce_kernel, dim3((nparam + 3 + 63) / 64), dim3(256), 0, st, partials,
+                     n_wg * train_partials_per_wg(), part,
                      nparam, grads, loss_out, p.inv_n);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
@@ -749,6 +789,8 @@ hipError_t launch_loss_grad(const TrainParams& p, int n_hidden, float* grads, fl
 }
 
 int train_partial_stride(int n_hidden) { return n_hidden == 3 ? train::TL<3>::PART : train::TL<2>::PART; }
+int train_packed_bytes(int n_hidden) { return n_hidden == 3 ? train::TL<3>::WAVE : train::TL<2>::WAVE; }
+int train_partials_per_wg() { return train::GACC_GLOBAL ? train::NWV : 1; }
 int train_waves_per_wg() { return train::NWV; }
 
 }  // namespace dmip
