@@ -23,8 +23,8 @@
 // lane & 15), which repack into the next layer's B operand with no lane movement (k-permuted weight
 // fragments, as in the sampler). Weight-gradient products contract over samples and use
 // v_mfma_f32_32x32x16_bf16 (K = the tile's 16 samples). Each wave accumulates its gradient partial
-// in its own LDS region (deterministic); the two waves' regions are summed in wave order into one
-// partial per workgroup, and loss_grad_reduce_kernel sums the partials in a fixed order.
+// in its own row of `partials` (global, 4-wave build) or LDS region (2-wave build, summed in wave
+// order per workgroup); loss_grad_reduce_kernel sums the rows in a fixed order (deterministic).
 #include "dmip_device.h"
 #include "dmip_internal.h"
 
