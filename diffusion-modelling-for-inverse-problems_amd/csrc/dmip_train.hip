@@ -711,7 +711,20 @@ __global__ void __launch_bounds__(NWV * 64, 1) loss_grad_kernel(TrainParams p) {
     for (int m = 1; m < 64; m <<= 1) v += __shfl_xor(v, m, 64);
     if (lane == 0) gacc[L::NPARAM + k] = v;
   }
-  if constexpr (GACC_GLOBAL) return;  // each wave's row of `partials` is its partial
+  if constexpr (GACC_GLOBAL) {
+    // fold the workgroup's NWV rows into its first row, in wave order (deterministic), so the
+    // reduction reads one row per workgroup
+    __threadfence_block();
+    __syncthreads();
+    float* rows = p.partials + (size_t)blockIdx.x * NWV * L::PART;
+    for (int e = tid; e < L::PART; e += NWV * 64) {
+      float v = rows[e];
+#pragma unroll
+      for (int ww = 1; ww < NWV; ++ww) v += rows[(size_t)ww * L::PART + e];
+      rows[e] = v;
+    }
+    return;
+  }
   // one partial per workgroup: wave 0's region + wave 1's region, in that order (deterministic)
   __syncthreads();
   float* part = p.partials + (size_t)blockIdx.x * L::PART;
@@ -779,8 +792,8 @@ hipError_t launch_loss_grad(const TrainParams& p, int n_hidden, float* grads, fl
     hipLaunchKernelGGL(loss_grad_kernel<2>, dim3(n_wg), dim3(NWV * 64), 0, st, q);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(loss_grad_reduce_kernel, dim3((nparam + 3 + 63) / 64), dim3(256), 0, st, partials,
-                     n_wg * train_partials_per_wg(), part,
+  hipLaunchKernelGGL(loss_grad_reduce_kernel, dim3((nparam + 3 + 63) / 64), dim3(256), 0, st, partials, n_wg,
+                     part * train_partials_per_wg(),
                      nparam, grads, loss_out, p.inv_n);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
