@@ -1,27 +1,38 @@
 """Benchmark: posterior samples/s of the fused reverse-SDE sampler (BASELINE.json metric).
 
-Workload (BASELINE.json configs[1]): scatterometry CDE, MLP 27 -> [256]*3 -> 3 (tanh, double tanh
-on layer 1), 1000 Euler-Maruyama steps, 100,000 chains per GPU for one y (y_test[0] of the
+Default workload (BASELINE.json configs[1]): scatterometry CDE, MLP 27 -> [256]*3 -> 3 (tanh, double
+tanh on layer 1), 1000 Euler-Maruyama steps, 100,000 chains per GPU for one y (y_test[0] of the
 reference's seeded test set, tests/golden/data_scat.npz), weights = the fixture-trained checkpoint
-(tests/golden/ckpt_scat.npz; random init if absent -- timing does not depend on the weights).
-One "step" = one full sampling call (x0 draw + 1000 SDE steps + output in HBM). With --gpus N the
-chains are sharded by global chain index (weak scaling: 100k chains per GPU) and the shards are
-gathered to every rank with one RCCL all_gather inside the timed region.
+(tests/golden/ckpt_scat.npz; random init if absent -- timing does not depend on the weights), bf16
+MFMA operands (north_star: "MFMA bf16 GEMMs"). One "step" = one full sampling call (x0 draw + 1000
+SDE steps + output in HBM). With --gpus N the chains are sharded by global chain index (weak
+scaling: 100k chains per GPU) and the shards are gathered to every rank with one RCCL all_gather
+inside the timed region.
 
-Prints ONE JSON line on rank 0 (driver contract) with `roofline` (MFMA-bound; algorithmic flops per
-launch / HIP-event-timed average launch) and `cpu_baseline` (reference-order torch-CPU sampler on a
-bounded sample, rank 0, N=1 only).
+Launch: `python bench.py --gpus N` starts N rank processes itself (one per GPU, RCCL over xGMI) when
+it is not already running under torch.distributed.run; the parent never touches the GPU.
+
+Prints ONE JSON line on rank 0 (driver contract) with
+  * `roofline`: MFMA-bound; algorithmic flops per launch / HIP-event-timed average launch;
+  * `cpu_baseline`: reference-order torch-CPU sampler on a bounded sample (rank 0, N = 1 only);
+  * `ks_vs_ref` / `w1_vs_ref` / `parity`: the timed run's samples against the reference sampler's own
+    draws (tests/golden/samples_scat.npz: 20k draws and the 1001 quantiles of its 100k-chain run, same
+    y and weights): per-dimension KS (alpha = 0.01), per-dimension and sliced W1 with their null levels;
+  * `fp32_mode`: the same workload in the exact-f32 parity mode (DMIP_PREC_F32), timed after the
+    headline with its own parity report.
+Other workloads (not the headline): --workload cdiffe-pc (BASELINE config 3: CDiffE + 1 Langevin
+corrector step, --chains-total 1000000 sharded over the ranks: strong scaling) and --workload dps
+(config 4: DPS with surrogate guidance, exact f32, --chains-total 262144).
 """
 import argparse
 import importlib
 import json
 import os
+import subprocess
 import sys
 import time
 
 import numpy as np
-import torch
-import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -29,13 +40,57 @@ PKG = "diffusion-modelling-for-inverse-problems_amd"
 
 XDIM, YDIM, WIDTH, NH = 3, 23, 256, 3
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, no sparsity)
+PEAK_F32_TFLOPS = 157.3    # MI355X f32 MFMA (= the f32 vector rate)
 
 
 def flops_per_sample_step(in_dim=XDIM + YDIM + 1, w=WIDTH, nh=NH, out=XDIM):
     return 2 * (in_dim * w + (nh - 1) * w * w + w * out)
 
 
+F_PRIOR = flops_per_sample_step(XDIM + 1, WIDTH, NH, XDIM)
+F_SUR = 2 * (3 * 256 + 2 * 256 * 256 + 256 * 23)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default="cde", choices=["cde", "cdiffe-pc", "dps"])
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--chains", type=int, default=100000, help="chains per GPU (weak scaling)")
+    ap.add_argument("--chains-total", type=int, default=0, help="total chains over all GPUs (strong scaling)")
+    ap.add_argument("--num-steps", type=int, default=1000, help="SDE steps per sample")
+    ap.add_argument("--cpu-chains", type=int, default=16384)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-fp32", action="store_true", help="skip the exact-f32 run beside the headline")
+    ap.add_argument("--fp32-steps", type=int, default=2)
+    ap.add_argument("--master-port", type=int, default=29511)
+    ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)  # CPU/gloo launcher test only
+    return ap.parse_args()
+
+
+# ------------------------------------------------------------------------------ launcher
+def launch_ranks(args):
+    """Start args.gpus rank processes (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* in their environment) and
+    wait for all of them; the parent initialises no GPU state. Exit status: the worst child's."""
+    env0 = dict(os.environ)
+    env0.setdefault("MASTER_ADDR", "127.0.0.1")
+    env0.setdefault("MASTER_PORT", str(args.master_port))
+    env0.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    procs = []
+    for r in range(args.gpus):
+        env = dict(env0, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus), LOCAL_WORLD_SIZE=str(args.gpus))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    for p in procs:
+        rc = max(rc, p.wait())
+    return rc
+
+
+# ------------------------------------------------------------------------------ workloads
 def load_model(pkg, dev):
+    import torch
     model = pkg.CDE(XDIM, YDIM, [WIDTH] * NH)
     ck = os.path.join(ROOT, "tests", "golden", "ckpt_scat.npz")
     weights = "random-init"
@@ -68,35 +123,42 @@ def pmc_traffic(kernel_match="em_sampler"):
     return z["hbm_bytes_per_launch"]
 
 
-def ks_vs_reference(x, num_steps, weights):
-    """Per-dimension two-sample KS statistic of the timed run's samples against the reference
-    sampler's own stored draws (tests/golden/samples_scat.npz: 20k of a 100k-chain run of the
-    reference's models/diffusion.py:27-46 loop, same y and the same fixture weights), with the
-    alpha = 0.01 critical value. The 'KS vs ref' half of BASELINE.json's metric; computed after
-    the timed region. None when the weights or the step count differ from the fixture's."""
+def parity_vs_reference(metrics, x, num_steps, weights):
+    """The timed run's samples against the reference sampler's own stored draws (tests/golden/
+    samples_scat.npz: 20k draws of a 100k-chain run of the reference's models/diffusion.py:27-46 loop
+    and that run's 1001 quantiles, same y and the same fixture weights). None when the weights or the
+    step count differ from the fixture's."""
     p = os.path.join(ROOT, "tests", "golden", "samples_scat.npz")
     if not os.path.exists(p) or not weights.startswith("fixture"):
         return None
     z = np.load(p)
     if int(z["num_steps"]) != num_steps:
         return None
-    ref = np.sort(z["samples"].astype(np.float64), axis=0)
-    x = np.sort(np.asarray(x, np.float64), axis=0)
-    stats = []
-    for k in range(ref.shape[1]):
-        both = np.concatenate([x[:, k], ref[:, k]])
-        ca = np.searchsorted(x[:, k], both, side="right") / x.shape[0]
-        cb = np.searchsorted(ref[:, k], both, side="right") / ref.shape[0]
-        stats.append(float(np.max(np.abs(ca - cb))))
-    n1, n2 = x.shape[0], ref.shape[0]
-    crit = 1.63 * float(np.sqrt((n1 + n2) / (n1 * n2)))
-    return {"stat": stats, "crit_alpha_0.01": crit, "pass": bool(max(stats) < crit),
-            "n_samples": n1, "n_ref": n2,
+    return metrics.parity_report(x, z["samples"], z["quantiles"], int(z["n_total"]))
+
+
+def ks_field(rep):
+    if rep is None:
+        return None
+    k = rep["ks_draws"]
+    return {"stat": k["stat"], "crit_alpha_0.01": k["crit"], "pass": bool(max(k["stat"]) < k["crit"]),
+            "n_samples": rep["n"], "n_ref": rep["n_ref"],
+            "vs_100k_quantiles": rep.get("ks_quantiles"),
             "ref": "reference sampler's own draws (tests/golden/samples_scat.npz, same y, same weights)"}
+
+
+def w1_field(rep):
+    if rep is None:
+        return None
+    return {"per_dim": rep["w1_draws"]["stat"], "per_dim_null": rep["w1_draws"]["null"],
+            "sliced": rep["sliced_w1_draws"]["stat"], "sliced_null": rep["sliced_w1_draws"]["null"],
+            "vs_100k_quantiles": rep.get("w1_quantiles"),
+            "bound": "3x the expected W1 of two same-distribution samples of these sizes (metrics.w1_null)"}
 
 
 def cpu_baseline(num_steps, n_chains):
     """Reference-order torch-CPU sampler (oracle/torch_cpu.py) on a bounded sample."""
+    import torch
     from oracle import torch_cpu
     threads = torch.get_num_threads()
     gen = torch.Generator().manual_seed(0)
@@ -122,55 +184,86 @@ def cpu_baseline(num_steps, n_chains):
                       f"(oracle/torch_cpu.py), {dt:.1f} s"}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--chains", type=int, default=100000, help="chains per GPU")
-    ap.add_argument("--num-steps", type=int, default=1000, help="SDE steps per sample")
-    ap.add_argument("--cpu-chains", type=int, default=16384)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    args = ap.parse_args()
+class Workload:
+    """One sampling call per step on this rank's chain range [lo, hi) of n_total (+ the gather)."""
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
-    pkg = importlib.import_module(PKG)
-    from importlib import import_module
-    parallel = import_module(PKG + ".parallel")
+    def __init__(self, args, pkg, dev, rank, world):
+        import torch
+        par = importlib.import_module(PKG + ".parallel")
+        self.args, self.dev, self.world = args, dev, world
+        S = args.num_steps
+        gold = os.path.join(ROOT, "tests", "golden")
+        self.y = torch.from_numpy(synthetic_y()).to(dev)
+        if args.chains_total > 0:
+            self.n_total, self.scaling = args.chains_total, "strong"
+        else:
+            self.n_total, self.scaling = args.chains * world, "weak"
+        self.lo, self.hi = par.shard_range(self.n_total, rank, world)
+        self.n_local = self.hi - self.lo
+        self.weights = "random-init"
+        self.kw = {}
+        if args.workload == "cde":
+            self.model, self.weights = load_model(pkg, dev)
+            self.flops_sample_step = flops_per_sample_step()
+            self.peak = PEAK_BF16_TFLOPS if args.precision == "bf16" else PEAK_F32_TFLOPS
+            self.kernel = ("em_sampler_kernel<0,256,3,3,0,8,4,false> (+a1_prep, inside the events)"
+                           if args.precision == "bf16" else "f32_sampler_kernel<0,256,3,0,false> (+l1_prep)")
+            self.workload = "scatterometry CDE posterior sampling (BASELINE configs[1])"
+            self.kw = {"precision": args.precision}
+        elif args.workload == "cdiffe-pc":
+            torch.manual_seed(0)
+            self.model = pkg.CDiffE(XDIM, YDIM, [WIDTH] * NH)
+            self.model.sde.a.to(dev)
+            self.kw = {"corrector_steps": 1, "snr": 0.16, "precision": args.precision}
+            self.flops_sample_step = 2 * flops_per_sample_step(XDIM + YDIM + 1, WIDTH, NH, XDIM + YDIM)
+            self.peak = PEAK_BF16_TFLOPS if args.precision == "bf16" else PEAK_F32_TFLOPS
+            self.kernel = "em_sampler_kernel<2,256,3,3,23,8,4,false> (CDiffE + Langevin corrector)"
+            self.workload = "scatterometry CDiffE predictor-corrector (BASELINE configs[2])"
+        else:  # dps
+            fm, prm = pkg.load_forward_model(gold)
+            self.model = pkg.DPS(XDIM, YDIM, [WIDTH] * NH, fm.to(dev), prm)
+            ck = os.path.join(gold, "ckpt_prior_scat.npz")
+            if os.path.exists(ck):
+                z = np.load(ck)
+                self.model.prior_net.load_state_dict({k.replace("_", "."): torch.from_numpy(z[k]) for k in z.files
+                                                      if k.split("_")[0].isdigit()})
+                self.weights = "fixture-trained prior (tests/golden/ckpt_prior_scat.npz)"
+            self.model.prior_net.to(dev)
+            self.flops_sample_step = 2 * F_PRIOR + 2 * F_SUR
+            self.peak = PEAK_F32_TFLOPS
+            self.kernel = "dps_kernel (exact f32)"
+            self.workload = "scatterometry DPS, surrogate guidance (BASELINE configs[3])"
+        self.par = par
 
-    model, weights = load_model(pkg, dev)
-    y = torch.from_numpy(synthetic_y()).to(dev)
-    n_local, S = args.chains, args.num_steps
-    n_total = n_local * world
-    lo = rank * n_local
+    def sample_local(self, seed, **over):
+        kw = dict(self.kw, **over)
+        return self.model.sample_device(self.y, self.n_local, self.args.num_steps, seed=seed, chain_offset=self.lo,
+                                        **kw)
 
-    def one_step(seed):
-        x = model.sample_device(y, n_local, S, seed=seed, chain_offset=lo)
-        if world > 1:
-            x = parallel.gather_shards(x, n_total, dev)
+    def step(self, seed, **over):
+        x = self.sample_local(seed, **over)
+        if self.world > 1:
+            x = self.par.gather_shards(x, self.n_total, self.dev)
         return x
 
-    for i in range(args.warmup):
-        one_step(1000 + i)
-    torch.cuda.synchronize()
 
+def timed(wl, steps, dist, world, dev, seed0=0, **over):
+    """barrier + sync, K steps (HIP events around each sampling call on its stream), sync + barrier;
+    (elapsed max over ranks, mean launch ms, last output)."""
+    import torch
     stream = torch.cuda.current_stream(dev)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    x_last = None
-    for i in range(args.steps):
+    x = None
+    for i in range(steps):
         ev[i][0].record(stream)
-        x_last = model.sample_device(y, n_local, S, seed=i, chain_offset=lo) if world == 1 else one_step(i)
+        x = wl.sample_local(seed0 + i, **over)
         ev[i][1].record(stream)
+        if world > 1:
+            x = wl.par.gather_shards(x, wl.n_total, dev)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -180,11 +273,39 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     launch_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    return elapsed, launch_ms, x
+
+
+def main_worker(args):
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.stub:
+        return stub_worker(args, rank, world)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    pkg = importlib.import_module(PKG)
+    lib = importlib.import_module(PKG + "._lib")
+    metrics = importlib.import_module(PKG + ".metrics")
+    wl = Workload(args, pkg, dev, rank, world)
+    S = args.num_steps
+
+    for i in range(args.warmup):
+        wl.step(1000 + i)
+    torch.cuda.synchronize()
+    elapsed, launch_ms, x_last = timed(wl, args.steps, dist, world, dev)
+    lib.device_status(dev)  # no asynchronous kernel failure in the timed region
 
     ms_per_step = elapsed / args.steps * 1e3
-    value = n_total * args.steps / elapsed
-    flops_launch = flops_per_sample_step() * S * n_local
+    value = wl.n_total * args.steps / elapsed
+    flops_launch = wl.flops_sample_step * S * wl.n_local
     achieved = flops_launch / (launch_ms * 1e-3) / 1e12
+    dtype = "bf16" if (args.workload != "dps" and args.precision == "bf16") else "f32"
     line = {
         "metric": "posterior samples/sec (1000-step reverse SDE)",
         "value": value,
@@ -194,28 +315,82 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": wl.scaling,
         "vs_baseline": None,
-        "dtype": "bf16",
-        "data": f"synthetic y (reference seeded y_test[0]); weights {weights}",
-        "config": {"workload": "scatterometry CDE posterior sampling (BASELINE configs[1])",
-                   "xdim": XDIM, "ydim": YDIM, "hidden_layers": [WIDTH] * NH, "sde_steps": S,
-                   "chains_per_gpu": n_local, "chains_total": n_total,
+        "dtype": dtype,
+        "data": f"synthetic y (reference seeded y_test[0]); weights {wl.weights}",
+        "config": {"workload": wl.workload, "xdim": XDIM, "ydim": YDIM, "hidden_layers": [WIDTH] * NH,
+                   "sde_steps": S, "chains_per_gpu": wl.n_local, "chains_total": wl.n_total,
                    "parallelism": f"sample-parallel x{world}" + (" + RCCL all_gather" if world > 1 else ""),
-                   "arith": "bf16 MFMA operands, fp32 accumulate; fp32 chain state / SDE update"},
-        "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / PEAK_BF16_TFLOPS, "traffic": pmc_traffic(),
-                     "kernel": "em_sampler_kernel<256,3,3,8,4> (+a1_prep, inside the events)",
-                     "launch_ms": launch_ms, "flops_per_launch": flops_launch},
+                   "arith": ("bf16 MFMA operands, fp32 accumulate; fp32 chain state / SDE update" if dtype == "bf16"
+                             else "exact f32 MFMA (v_mfma_f32_16x16x4_f32); fp32 chain state / SDE update")},
+        "roofline": {"bound": "mfma", "achieved": achieved, "peak": wl.peak, "unit": "TFLOP/s",
+                     "frac": achieved / wl.peak,
+                     "traffic": pmc_traffic() if (args.workload == "cde" and dtype == "bf16") else None,
+                     "kernel": wl.kernel, "launch_ms": launch_ms, "flops_per_launch": flops_launch},
     }
-    if rank == 0:
-        line["ks_vs_ref"] = ks_vs_reference(x_last.reshape(-1, XDIM).cpu().numpy(), S, weights)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    rep = None
+    if args.workload == "cde" and rank == 0:
+        rep = parity_vs_reference(metrics, x_last.reshape(-1, XDIM).cpu().numpy(), S, wl.weights)
+        line["ks_vs_ref"] = ks_field(rep)
+        line["w1_vs_ref"] = w1_field(rep)
+        line["parity"] = {"pass": rep["pass"]} if rep else None
+    if args.workload == "cde" and args.precision == "bf16" and not args.no_fp32:
+        # the exact-f32 parity mode on the same workload, timed beside the headline (not the headline)
+        wl.step(2000, precision="fp32")
+        el32, lm32, x32 = timed(wl, args.fp32_steps, dist, world, dev, seed0=100, precision="fp32")
+        lib.device_status(dev)
+        if rank == 0:
+            a32 = flops_launch / (lm32 * 1e-3) / 1e12
+            rep32 = parity_vs_reference(metrics, x32.reshape(-1, XDIM).cpu().numpy(), S, wl.weights)
+            line["fp32_mode"] = {
+                "value": wl.n_total * args.fp32_steps / el32, "unit": "samples/s", "steps": args.fp32_steps,
+                "ms_per_step": el32 / args.fp32_steps * 1e3, "launch_ms": lm32, "kernel": "f32_sampler_kernel",
+                "roofline": {"bound": "mfma", "achieved": a32, "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s",
+                             "frac": a32 / PEAK_F32_TFLOPS},
+                "ks_vs_ref": ks_field(rep32), "w1_vs_ref": w1_field(rep32),
+                "parity": {"pass": rep32["pass"]} if rep32 else None}
+    if rank == 0 and world == 1 and args.workload == "cde" and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(S, args.cpu_chains)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return 0
+
+
+def stub_worker(args, rank, world):
+    """CPU / gloo stand-in for the sampler (launcher test only): every rank contributes its chain
+    range [lo, hi) as x[c] = (c, c, c); rank 0 checks the gathered tensor and prints the line."""
+    import torch
+    import torch.distributed as dist
+    par = importlib.import_module(PKG + ".parallel")
+    if world > 1:
+        dist.init_process_group("gloo")
+    n_total = args.chains_total if args.chains_total > 0 else args.chains * world
+    lo, hi = par.shard_range(n_total, rank, world)
+    local = torch.arange(lo, hi, dtype=torch.float32)[None, :, None].expand(1, hi - lo, XDIM).contiguous()
+    x = par.gather_shards(local, n_total, torch.device("cpu")) if world > 1 else local
+    ok = bool(torch.equal(x[0, :, 0], torch.arange(n_total, dtype=torch.float32)))
+    if world > 1:
+        dist.barrier()
+    if rank == 0:
+        print(json.dumps({"metric": "stub", "n_gpus": world, "chains_total": n_total,
+                          "gathered_shape": list(x.shape), "gather_ok": ok}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0 if ok else 1
+
+
+def main():
+    args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus != world:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; run it as `python bench.py --gpus N` "
+                 "or under torch.distributed.run with --nproc-per-node N")
+    sys.exit(main_worker(args))
 
 
 if __name__ == "__main__":

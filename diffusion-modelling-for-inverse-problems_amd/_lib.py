@@ -18,9 +18,10 @@ LIB_PATH = os.environ.get("DMIP_LIB", os.path.join(_HERE, "libdmip.so"))
 DMIP_OK, DMIP_ERR_INVALID, DMIP_ERR_UNSUPPORTED, DMIP_ERR_HIP, DMIP_ERR_ALLOC = range(5)
 DMIP_INPUT_X_Y_T, DMIP_INPUT_X_T = 0, 1
 DMIP_ACT_TANH_TWICE_FIRST, DMIP_ACT_TANH = 0, 1
-DMIP_PREC_BF16 = 0
+DMIP_PREC_BF16, DMIP_PREC_F32 = 0, 1
+PRECISIONS = {"bf16": DMIP_PREC_BF16, "fp32": DMIP_PREC_F32}
 DMIP_SAMPLER_CDE, DMIP_SAMPLER_POSTERIOR, DMIP_SAMPLER_CDIFFE = 0, 1, 2
-ABI_VERSION = 4
+ABI_VERSION = 5
 DMIP_LOSS_DSM, DMIP_LOSS_DSM_PDE, DMIP_LOSS_PINN, DMIP_LOSS_PINN2 = 0, 1, 2, 3
 DMIP_PDE_NONE, DMIP_PDE_FPE, DMIP_PDE_CFPE = 0, 1, 2
 DMIP_METRIC_L1, DMIP_METRIC_L2 = 0, 1
@@ -31,7 +32,8 @@ EXPORTED = (
     "dmip_rng_normals", "dmip_schedule", "dmip_last_error", "dmip_abi_version", "dmip_sampler_supported",
     "dmip_em_sample_stamps", "dmip_em_sample_posterior", "dmip_em_sample_cdiffe", "dmip_loss_grad",
     "dmip_loss_grad_supported", "dmip_histogram", "dmip_surrogate_create", "dmip_surrogate_destroy",
-    "dmip_surrogate_forward", "dmip_log_posterior", "dmip_mh_sample", "dmip_dps_sample",
+    "dmip_surrogate_forward", "dmip_log_posterior", "dmip_mh_sample", "dmip_dps_sample", "dmip_device_status",
+    "dmip_sampler_supported_f32",
 )
 DMIP_DPS_NLL, DMIP_DPS_NORM = 0, 1
 
@@ -63,6 +65,8 @@ def _declare(lib):
     lib.dmip_last_error.restype = ctypes.c_char_p
     lib.dmip_abi_version.restype = _i32
     lib.dmip_sampler_supported.argtypes = [_i32, _i32, _i32, _i32, _i32]
+    lib.dmip_sampler_supported_f32.argtypes = [_i32, _i32, _i32, _i32, _i32]
+    lib.dmip_device_status.argtypes = [_c_void_p]
     lib.dmip_mlp_create.argtypes = [_i32, _i32, _i32, ctypes.POINTER(_i32), _i32, _i32, _i32,
                                     ctypes.POINTER(_c_void_p), ctypes.POINTER(_c_void_p),
                                     ctypes.POINTER(_c_void_p)]
@@ -101,7 +105,7 @@ def _declare(lib):
     lib.dmip_dps_sample.argtypes = [_c_void_p, _c_void_p, ctypes.POINTER(DmipScatNoise), ctypes.POINTER(DmipVpsde),
                                     _c_void_p, _i32, _i64, _i64, _i32, _f32, _f32, _u64, _i32, _f32, _c_void_p,
                                     _c_void_p]
-    for name in ("dmip_dps_sample", "dmip_mlp_create", "dmip_mlp_destroy", "dmip_mlp_forward", "dmip_em_sample",
+    for name in ("dmip_device_status", "dmip_sampler_supported_f32", "dmip_dps_sample", "dmip_mlp_create", "dmip_mlp_destroy", "dmip_mlp_forward", "dmip_em_sample",
                  "dmip_rng_words", "dmip_rng_normals", "dmip_schedule", "dmip_sampler_supported",
                  "dmip_em_sample_stamps", "dmip_em_sample_posterior", "dmip_em_sample_cdiffe",
                  "dmip_loss_grad", "dmip_loss_grad_supported", "dmip_histogram", "dmip_surrogate_create",
@@ -183,42 +187,65 @@ class MlpHandle:
             self.h = None
 
 
-def mlp_forward(handle, x, y, t, out, y_stride, t_stride):
+def precision_code(precision):
+    """'bf16' (bf16 MFMA operands, the throughput mode) or 'fp32' (exact f32, the reference's arithmetic)."""
+    if precision not in PRECISIONS:
+        raise ValueError(f"precision must be one of {sorted(PRECISIONS)}, got {precision!r}")
+    return PRECISIONS[precision]
+
+
+def mlp_forward(handle, x, y, t, out, y_stride, t_stride, precision="fp32"):
     calls["mlp_forward"] += 1
     check(lib().dmip_mlp_forward(handle.h, ptr(x), ptr(y), y_stride, ptr(t), t_stride, x.shape[0],
-                                 ptr(out), DMIP_PREC_BF16, stream_of(x.device)))
+                                 ptr(out), precision_code(precision), stream_of(x.device)))
 
 
-def em_sample(handle, sde, y, n_chains, chain_offset, num_steps, mean, std, seed, out, noise=None):
+def em_sample(handle, sde, y, n_chains, chain_offset, num_steps, mean, std, seed, out, noise=None,
+              precision="bf16"):
     calls["em_sample"] += 1
     n_y, ydim = y.shape
     check(lib().dmip_em_sample(handle.h, ctypes.byref(sde), ptr(y), n_y, ydim, handle.xdim,
                                int(n_chains), int(chain_offset), int(num_steps), float(mean),
                                float(std), ctypes.c_uint64(int(seed) & 0xFFFFFFFFFFFFFFFF),
-                               DMIP_PREC_BF16, ptr(noise), ptr(out), stream_of(y.device)))
+                               precision_code(precision), ptr(noise), ptr(out), stream_of(y.device)))
 
 
-def em_sample_posterior(prior, likelihood, sde, y, n_chains, chain_offset, num_steps, mean, std, seed, out):
+def em_sample_posterior(prior, likelihood, sde, y, n_chains, chain_offset, num_steps, mean, std, seed, out,
+                        precision="bf16"):
     calls["em_sample_posterior"] += 1
     n_y, ydim = y.shape
     check(lib().dmip_em_sample_posterior(prior.h, likelihood.h, ctypes.byref(sde), ptr(y), n_y, ydim,
                                          likelihood.xdim, int(n_chains), int(chain_offset), int(num_steps),
                                          float(mean), float(std), ctypes.c_uint64(int(seed) & 0xFFFFFFFFFFFFFFFF),
-                                         DMIP_PREC_BF16, ptr(out), stream_of(y.device)))
+                                         precision_code(precision), ptr(out), stream_of(y.device)))
 
 
 def em_sample_cdiffe(handle, sde, y, n_chains, chain_offset, num_steps, mean, std, seed, out, corrector_steps=0,
-                     snr=0.16):
+                     snr=0.16, precision="bf16"):
     calls["em_sample_cdiffe"] += 1
     n_y, ydim = y.shape
     check(lib().dmip_em_sample_cdiffe(handle.h, ctypes.byref(sde), ptr(y), n_y, ydim, handle.xdim,
                                       int(n_chains), int(chain_offset), int(num_steps), float(mean), float(std),
-                                      ctypes.c_uint64(int(seed) & 0xFFFFFFFFFFFFFFFF), DMIP_PREC_BF16,
+                                      ctypes.c_uint64(int(seed) & 0xFFFFFFFFFFFFFFFF), precision_code(precision),
                                       int(corrector_steps), float(snr), ptr(out), stream_of(y.device)))
 
 
-def sampler_supported(width, n_hidden, xdim, ydim=0, mode=DMIP_SAMPLER_CDE):
-    return bool(lib().dmip_sampler_supported(mode, width, n_hidden, xdim, ydim))
+def sampler_supported(width, n_hidden, xdim, ydim=0, mode=DMIP_SAMPLER_CDE, precision="bf16"):
+    fn = lib().dmip_sampler_supported_f32 if precision_code(precision) == DMIP_PREC_F32 else lib().dmip_sampler_supported
+    return bool(fn(mode, width, n_hidden, xdim, ydim))
+
+
+def device_status(device):
+    """Synchronise the device's current stream and raise if a kernel reported an asynchronous failure
+    (dmip_device_status: today the balanced sampler's hand-over timeout)."""
+    check(lib().dmip_device_status(stream_of(device)))
+
+
+def rng_normals(seed, chain_offset, stream_id, n_chains, n_pairs, out):
+    """(n_chains, 2 n_pairs) standard normals of the kernels' chain-keyed generator (dmip_rng_normals)."""
+    check(lib().dmip_rng_normals(ctypes.c_uint64(int(seed) & 0xFFFFFFFFFFFFFFFF), int(chain_offset),
+                                 ctypes.c_uint64(int(stream_id) & 0xFFFFFFFFFFFFFFFF), int(n_chains), int(n_pairs),
+                                 ptr(out), stream_of(out.device)))
 
 
 def loss_grad_supported(in_dim, out_dim, widths, xdim):

@@ -15,7 +15,9 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <new>
 #include <string>
 #include <vector>
@@ -72,6 +74,33 @@ inline int kperm(int s, int h, int j) { return 32 * (s >> 1) + 16 * (s & 1) + 8 
 inline int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 inline int k1s_for(int n_slots) { return (n_slots + 15) / 16; }
 
+// One device status word per device (kernels report asynchronous failures into it; read and
+// cleared by dmip_device_status). Allocated on first use, never freed (4 bytes per device).
+std::mutex g_status_mu;
+unsigned* g_status[dmip::kMaxDevices] = {};
+
+unsigned* status_word(int dev) {
+  if (dev < 0 || dev >= dmip::kMaxDevices) return nullptr;
+  std::lock_guard<std::mutex> lk(g_status_mu);
+  if (!g_status[dev]) {
+    int cur = dev;
+    (void)hipGetDevice(&cur);
+    if (cur != dev) (void)hipSetDevice(dev);
+    unsigned* w = nullptr;
+    if (hipMalloc((void**)&w, sizeof(unsigned)) == hipSuccess && hipMemset(w, 0, sizeof(unsigned)) == hipSuccess)
+      g_status[dev] = w;
+    if (cur != dev) (void)hipSetDevice(cur);
+  }
+  return g_status[dev];
+}
+
+// test hook (not ABI): DMIP_DEBUG_NO_HANDOVER=1 makes the balanced sampler's producers never publish
+// their hand-over, with a short spin bound, so the consumer's timeout path runs
+int debug_no_handover() {
+  const char* e = getenv("DMIP_DEBUG_NO_HANDOVER");
+  return e && e[0] == '1' ? 1 : 0;
+}
+
 template <typename T>
 int upload(T** dst, const std::vector<T>& src) {
   *dst = nullptr;
@@ -103,22 +132,88 @@ struct dmip_mlp {
   char* dps_w3 = nullptr;
   char* dps_w4 = nullptr;         // [1][16][64][4], rows >= 3 zero
   float* dps_bias = nullptr;      // b2 | b3 | b4[16]
+  // exact-f32 images (DMIP_PREC_F32, dmip_f32.h): every input column + bias as layer 1
+  float* f32_l1 = nullptr;        // [W/16][k1q][64]
+  char* f32_stream = nullptr;     // [(L-1) W/16 + f32_ot chunks][W/16][64][4]
+  float* f32_bias = nullptr;      // [(L-1)][W] | [16 f32_ot]
+  int f32_k1q = 0, f32_ot = 0;
   ~dmip_mlp() {
     for (void* p : {(void*)hidden, (void*)ao_samp, (void*)ao_full, (void*)bias_hidden, (void*)bias_out_samp,
                     (void*)bias_out_full, (void*)a1_full, (void*)w1, (void*)b1, (void*)dps_l1, (void*)dps_w2,
-                    (void*)dps_w3, (void*)dps_w4, (void*)dps_bias})
+                    (void*)dps_w3, (void*)dps_w4, (void*)dps_bias, (void*)f32_l1, (void*)f32_stream,
+                    (void*)f32_bias})
       if (p) (void)hipFree(p);
   }
 };
+
+namespace {
+
+// exact-f32 images of a network (dmip_f32.h FEngine): layer 1 over every input column then the bias
+// column; the W x W layers and the output layer as 16-row chunks in stream order; the biases.
+int pack_f32_net(dmip_mlp* net, const float* const* weights, const float* const* biases) {
+  const int W = net->width, L = net->n_hidden, IN = net->in_dim, OUT = net->out_dim, ST = W / 16;
+  const int K1Q = (IN + 1 + 3) / 4, OT = (OUT + 15) / 16;
+  net->f32_k1q = K1Q;
+  net->f32_ot = OT;
+  std::vector<float> l1((size_t)ST * K1Q * 64);
+  for (int o = 0; o < ST; ++o)
+    for (int s = 0; s < K1Q; ++s)
+      for (int l = 0; l < 64; ++l) {
+        const int u = 16 * o + (l & 15), c = 4 * s + (l >> 4);
+        l1[((size_t)o * K1Q + s) * 64 + l] = c < IN ? weights[0][(size_t)u * IN + c] : (c == IN ? biases[0][u] : 0.0f);
+      }
+  std::vector<char> stream;
+  for (int li = 1; li < L; ++li) {
+    const float* Wl = weights[li];
+    std::vector<char> img = pack_f32_tiles(ST, ST, [Wl, W](int r, int c) { return Wl[(size_t)r * W + c]; });
+    stream.insert(stream.end(), img.begin(), img.end());
+  }
+  const float* Wo = weights[L];
+  std::vector<char> oimg =
+      pack_f32_tiles(OT, ST, [Wo, W, OUT](int r, int c) { return r < OUT ? Wo[(size_t)r * W + c] : 0.0f; });
+  stream.insert(stream.end(), oimg.begin(), oimg.end());
+  std::vector<float> bias((size_t)(L - 1) * W + 16 * OT, 0.0f);
+  for (int li = 1; li < L; ++li)
+    for (int k = 0; k < W; ++k) bias[(size_t)(li - 1) * W + k] = biases[li][k];
+  for (int k = 0; k < OUT; ++k) bias[(size_t)(L - 1) * W + k] = biases[L][k];
+  int rc = DMIP_OK;
+  if ((rc = upload(&net->f32_l1, l1)) || (rc = upload(&net->f32_stream, stream)) || (rc = upload(&net->f32_bias, bias)))
+    return rc;
+  return DMIP_OK;
+}
+
+dmip::F32Net f32_net(const dmip_mlp* n) { return dmip::F32Net{n->f32_l1, n->f32_stream, n->f32_bias}; }
+
+}  // namespace
 
 extern "C" {
 
 const char* dmip_last_error(void) { return g_err.c_str(); }
 
+int dmip_device_status(void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  hipError_t e = hipStreamSynchronize(st);
+  if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+  unsigned* w = status_word(dmip::stream_device(st));
+  if (!w) return fail(DMIP_ERR_ALLOC, "device status word");
+  unsigned v = 0;
+  if ((e = hipMemcpy(&v, w, sizeof(unsigned), hipMemcpyDeviceToHost)) != hipSuccess) return hip_fail(e, "hipMemcpy");
+  if (v == 0) return DMIP_OK;
+  (void)hipMemset(w, 0, sizeof(unsigned));
+  if (v == dmip::kErrHandover)
+    return fail(DMIP_ERR_HIP, "sampler: a split tile's hand-over never arrived (workgroups of the balanced schedule "
+                              "were not co-resident); the affected chains were written as NaN");
+  return fail(DMIP_ERR_HIP, "device status " + std::to_string(v));
+}
+
 int dmip_abi_version(void) { return DMIP_ABI_VERSION; }
 
 int dmip_sampler_supported(int mode, int width, int n_hidden, int xdim, int ydim) {
   return dmip::sampler_shape_supported(mode, width, n_hidden, xdim, ydim) ? 1 : 0;
+}
+
+int dmip_sampler_supported_f32(int mode, int width, int n_hidden, int xdim, int ydim) {
+  return dmip::f32_sampler_supported(mode, width, n_hidden, xdim, ydim) ? 1 : 0;
 }
 
 int dmip_mlp_create(int in_dim, int out_dim, int n_hidden, const int* widths, int act_mode, int input_layout,
@@ -282,7 +377,7 @@ int dmip_mlp_create(int in_dim, int out_dim, int n_hidden, const int* widths, in
   if ((rc = upload(&net->hidden, hid_b)) || (rc = upload(&net->ao_samp, ao_sb)) || (rc = upload(&net->ao_full, ao_fb)) ||
       (rc = upload(&net->bias_hidden, bh)) || (rc = upload(&net->bias_out_samp, bo_s)) ||
       (rc = upload(&net->bias_out_full, bo_f)) || (rc = upload(&net->a1_full, a1f_b)) ||
-      (rc = upload(&net->w1, w1v)) || (rc = upload(&net->b1, b1v))) {
+      (rc = upload(&net->w1, w1v)) || (rc = upload(&net->b1, b1v)) || (rc = pack_f32_net(net, weights, biases))) {
     delete net;
     return rc;
   }
@@ -298,13 +393,37 @@ int dmip_mlp_destroy(dmip_mlp* net) {
 int dmip_mlp_forward(const dmip_mlp* net, const float* x_dev, const float* y_dev, int64_t y_stride,
                      const float* t_dev, int t_stride, int64_t n, float* out_dev, int precision, void* stream) {
   if (!net || !x_dev || !t_dev || !out_dev) return fail(DMIP_ERR_INVALID, "null argument");
-  if (precision != DMIP_PREC_BF16) return fail(DMIP_ERR_UNSUPPORTED, "unknown precision");
+  if (precision != DMIP_PREC_BF16 && precision != DMIP_PREC_F32) return fail(DMIP_ERR_INVALID, "unknown precision");
   if (n < 0) return fail(DMIP_ERR_INVALID, "n < 0");
   if (n == 0) return DMIP_OK;
   const int ydim = net->layout == DMIP_INPUT_X_Y_T ? net->in_dim - net->xdim - 1 : 0;
   if (ydim > 0 && !y_dev) return fail(DMIP_ERR_INVALID, "y required for an X_Y_T network");
   if (ydim > 0 && y_stride != 0 && y_stride != ydim) return fail(DMIP_ERR_INVALID, "y_stride must be 0 or ydim");
   if (t_stride != 0 && t_stride != 1) return fail(DMIP_ERR_INVALID, "t_stride must be 0 or 1");
+  if (precision == DMIP_PREC_F32) {
+    dmip::F32ForwardParams q{};
+    q.net = f32_net(net);
+    q.n_hidden = net->n_hidden;
+    q.x = x_dev;
+    q.y = y_dev;
+    q.t = t_dev;
+    q.out = out_dev;
+    q.n = n;
+    q.y_stride = y_stride;
+    q.t_stride = t_stride;
+    q.xdim = net->xdim;
+    q.ydim = ydim;
+    q.out_dim = net->out_dim;
+    q.k1q = net->f32_k1q;
+    bool ok = false;
+    hipError_t e = dmip::launch_f32_forward(q, net->width, net->f32_ot, (hipStream_t)stream, &ok);
+    if (!ok)
+      return fail(DMIP_ERR_UNSUPPORTED, "no compiled f32 forward kernel for width " + std::to_string(net->width) +
+                                            ", layers " + std::to_string(net->n_hidden) + ", in_dim " +
+                                            std::to_string(net->in_dim) + ", out_dim " + std::to_string(net->out_dim));
+    if (e != hipSuccess) return hip_fail(e, "mlp_forward (f32) launch");
+    return DMIP_OK;
+  }
   dmip::ForwardParams p{};
   p.hidden = net->hidden;
   p.a1 = net->a1_full;
@@ -347,12 +466,67 @@ struct SampleArgs {
   float snr = 0.16f;
 };
 
+static void fill_schedule(const SampleArgs& a, float& T, float& bmin, float& bdiff, float& delta, float& sqrt_delta) {
+  T = (float)a.sde->T;
+  bmin = (float)a.sde->beta_min;
+  bdiff = (float)(a.sde->beta_max - a.sde->beta_min);
+  delta = (float)(a.sde->T / (double)a.num_steps);
+  sqrt_delta = (float)std::sqrt(a.sde->T / (double)a.num_steps);
+}
+
+// exact-f32 samplers (dmip_f32.h): same loop, RNG and sharding as the bf16 kernels; arguments
+// already validated by em_sample_impl
+static int em_sample_f32(int mode, const dmip_mlp* net0, const dmip_mlp* net1, const SampleArgs& a) {
+  const int xdim = a.xdim, ydim = a.ydim;
+  if (!dmip::f32_sampler_supported(mode, net0->width, net0->n_hidden, xdim, ydim))
+    return fail(DMIP_ERR_UNSUPPORTED, "no compiled f32 sampler (mode " + std::to_string(mode) + ") for width " +
+                                          std::to_string(net0->width) + ", layers " + std::to_string(net0->n_hidden) +
+                                          ", xdim " + std::to_string(xdim) + ", ydim " + std::to_string(ydim));
+  hipStream_t st = (hipStream_t)a.stream;
+  dmip::F32SamplerParams p{};
+  p.net[0] = f32_net(net0);
+  if (net1) p.net[1] = f32_net(net1);
+  p.n_hidden = net0->n_hidden;
+  float* l1y = nullptr;
+  if (mode != DMIP_SAMPLER_CDIFFE) {
+    // y is constant per y index: layer 1 over (x, t) with W1_y y + b1 folded into the bias column
+    const int k1q = (xdim + 2 + 3) / 4;
+    hipError_t e = hipMallocAsync((void**)&l1y, (size_t)a.n_y * (net0->width / 16) * k1q * 64 * sizeof(float), st);
+    if (e != hipSuccess) return fail(DMIP_ERR_ALLOC, std::string("hipMallocAsync: ") + hipGetErrorString(e));
+    dmip::F32L1PrepParams lp{net0->w1, net0->b1, a.y_dev, l1y, net0->width, net0->in_dim, xdim, ydim, k1q};
+    if ((e = dmip::launch_f32_l1_prep(lp, a.n_y, st)) != hipSuccess) {
+      (void)hipFreeAsync(l1y, st);
+      return hip_fail(e, "f32 layer-1 prep launch");
+    }
+    p.l1y = l1y;
+  }
+  p.y_obs = a.y_dev;
+  p.n_corr = a.n_corr;
+  p.snr = a.snr;
+  p.noise = a.noise_dev;
+  p.x_out = a.x_out_dev;
+  p.n_chains = a.n_chains;
+  p.chain_offset = a.chain_offset;
+  p.num_steps = a.num_steps;
+  fill_schedule(a, p.T, p.bmin, p.bdiff, p.delta, p.sqrt_delta);
+  p.mean = a.mean;
+  p.stdv = a.stdv;
+  p.seed = a.seed;
+  bool ok = false;
+  hipError_t e = dmip::launch_f32_sampler(p, mode, net0->width, net0->n_hidden, xdim, ydim, a.n_y, st, &ok);
+  if (l1y) (void)hipFreeAsync(l1y, st);
+  if (!ok) return fail(DMIP_ERR_UNSUPPORTED, "no compiled f32 sampler");
+  if (e != hipSuccess) return hip_fail(e, "f32 sampler launch");
+  return DMIP_OK;
+}
+
 // net0: the CDE / CDiffE network or the Posterior likelihood; net1: the Posterior prior (else null)
 static int em_sample_impl(int mode, const dmip_mlp* net0, const dmip_mlp* net1, const SampleArgs& a) {
   const int xdim = a.xdim, ydim = a.ydim;
   if (!net0 || !a.sde || !a.y_dev || !a.x_out_dev || (mode == DMIP_SAMPLER_POSTERIOR && !net1))
     return fail(DMIP_ERR_INVALID, "null argument");
-  if (a.precision != DMIP_PREC_BF16) return fail(DMIP_ERR_UNSUPPORTED, "unknown precision");
+  if (a.precision != DMIP_PREC_BF16 && a.precision != DMIP_PREC_F32) return fail(DMIP_ERR_INVALID, "unknown precision");
+  if (a.noise_dev && mode != DMIP_SAMPLER_CDE) return fail(DMIP_ERR_INVALID, "noise injection: CDE sampler only");
   if (net0->layout != DMIP_INPUT_X_Y_T) return fail(DMIP_ERR_INVALID, "sampler needs an x,y,t network");
   const int out_expected = mode == DMIP_SAMPLER_CDIFFE ? xdim + ydim : xdim;
   if (xdim != net0->xdim || net0->out_dim != out_expected)
@@ -369,6 +543,7 @@ static int em_sample_impl(int mode, const dmip_mlp* net0, const dmip_mlp* net1, 
   if (a.num_steps < 1) return fail(DMIP_ERR_INVALID, "num_steps must be >= 1");
   if (!(a.sde->T > 0.0)) return fail(DMIP_ERR_INVALID, "T must be > 0");
   if (a.n_chains == 0) return DMIP_OK;
+  if (a.precision == DMIP_PREC_F32) return em_sample_f32(mode, net0, net1, a);
   if (!dmip::sampler_shape_supported(mode, net0->width, net0->n_hidden, xdim, ydim))
     return fail(DMIP_ERR_UNSUPPORTED, "no compiled sampler (mode " + std::to_string(mode) + ") for width " +
                                           std::to_string(net0->width) + ", layers " + std::to_string(net0->n_hidden) +
@@ -435,6 +610,13 @@ static int em_sample_impl(int mode, const dmip_mlp* net0, const dmip_mlp* net1, 
   p.stdv = a.stdv;
   p.seed = a.seed;
   p.stamps = (unsigned long long*)a.stamps;
+  p.err = status_word(dmip::stream_device(st));
+  if (!p.err) {
+    if (a1) (void)hipFreeAsync(a1, st);
+    return fail(DMIP_ERR_ALLOC, "device status word");
+  }
+  p.debug_flags = debug_no_handover();
+  p.spin_limit = p.debug_flags ? (1u << 10) : (1u << 22);
   bool ok = false;
   hipError_t e = dmip::launch_sampler(p, mode, net0->width, net0->n_hidden, xdim, ydim, a.n_y, st, &ok);
   if (a1) (void)hipFreeAsync(a1, st);

@@ -3,7 +3,40 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 namespace dmip {
+
+constexpr int kMaxDevices = 64;
+
+// the device a stream belongs to (the current device for the null stream)
+inline int stream_device(hipStream_t st) {
+  int dev = 0;
+  hipDevice_t d = 0;
+  if (st != nullptr && hipStreamGetDevice(st, &d) == hipSuccess) return (int)d;
+  (void)hipGetDevice(&dev);
+  return dev;
+}
+
+// number of workgroups of `kern` the stream's device holds at once (CUs x occupancy), cached per
+// device and kernel instantiation (thread-safe: a racing first query computes the same value)
+template <typename Kern>
+int resident_slots(Kern kern, int nthreads, hipStream_t st) {
+  static std::atomic<int> cache[kMaxDevices];
+  const int dev = stream_device(st);
+  const int di = dev >= 0 && dev < kMaxDevices ? dev : 0;
+  const int v = cache[di].load(std::memory_order_relaxed);
+  if (v > 0) return v;
+  int n_cu = 256, per_cu = 1, cur = dev;
+  (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+  (void)hipGetDevice(&cur);
+  if (cur != dev) (void)hipSetDevice(dev);  // the occupancy query is for the current device
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, nthreads, 0) != hipSuccess || per_cu < 1) per_cu = 1;
+  if (cur != dev) (void)hipSetDevice(cur);
+  const int slots = (n_cu > 0 ? n_cu : 256) * per_cu;
+  cache[di].store(slots, std::memory_order_relaxed);
+  return slots;
+}
 
 // Sampler modes (dmip_kernels.hip em_sampler_kernel)
 enum { SAMPLER_CDE = 0, SAMPLER_POSTERIOR = 1, SAMPLER_CDIFFE = 2 };
@@ -37,7 +70,15 @@ struct SamplerParams {
   // chain state [D + 4][64] words and a ready flag (zeroed before the launch)
   float* xfer;
   unsigned int* xflag;
+  // device status word (dmip_device_status): set to kErrHandover when a consumer wave gives up
+  // waiting for a hand-over flag; the tile's chains are then written as NaN
+  unsigned int* err;
+  unsigned int spin_limit;    // s_sleep(8) rounds before a consumer gives up (default 2^22, ~1 s)
+  int debug_flags;            // test hook only: bit 0 = producers never publish (forces the timeout)
 };
+
+// device status codes written by kernels into the per-device status word
+constexpr unsigned kErrHandover = 1u;
 
 struct ForwardParams {
   const char* hidden;
@@ -144,6 +185,54 @@ hipError_t launch_dps(const DpsParams& p, int n_y, hipStream_t st);
 hipError_t launch_surrogate_eval(const SurrogateParams& p, int mode, int n_wg, hipStream_t st);
 int surrogate_rows_per_wg();
 hipError_t launch_mh(const SurrogateParams& p, int n_y, hipStream_t st);
+
+// Exact-f32 networks (dmip_f32.hip, DMIP_PREC_F32): images packed by dmip_capi.cpp pack_f32_net.
+struct F32Net {
+  const float* l1;     // [W/16 tiles][K1Q][64]: layer 1 over every input column, then the bias column
+  const char* stream;  // [(L-1) W/16 hidden tiles + OT output tiles][W/16 q][64][4] floats
+  const float* bias;   // [(L-1)][W] hidden biases, then [16 OT] output bias (rows >= out_dim zero)
+};
+
+struct F32SamplerParams {
+  F32Net net[2];              // net 0: CDE / CDiffE / likelihood; net 1: the Posterior prior
+  const float* l1y;           // CDE / likelihood: per-y layer-1 images [n_y][W/16][K1Q][64] (y folded in)
+  int n_hidden;
+  const float* y_obs;         // CDiffE observations [n_y][ydim]
+  int n_corr;
+  float snr;
+  const float* noise;         // CDE: injected normals [S+1][n_y][n_chains][D] or null
+  float* x_out;               // [n_y][n_chains][D]
+  long long n_chains, chain_offset;
+  int num_steps;
+  float T, bmin, bdiff, delta, sqrt_delta, mean, stdv;
+  unsigned long long seed;
+};
+
+struct F32ForwardParams {
+  F32Net net;
+  int n_hidden;
+  const float* x;
+  const float* y;
+  const float* t;
+  float* out;
+  long long n, y_stride;
+  int t_stride, xdim, ydim, out_dim;
+  int k1q;                    // layer-1 k-steps of the image: ceil((in_dim + 1) / 4)
+};
+
+struct F32L1PrepParams {
+  const float* w1;  // [width][in_dim] (nn.Linear layout)
+  const float* b1;
+  const float* y;   // [n_y][ydim]
+  float* l1y;       // out: [n_y][width/16][k1q][64]
+  int width, in_dim, xdim, ydim, k1q;
+};
+
+hipError_t launch_f32_sampler(const F32SamplerParams& p, int mode, int width, int n_hidden, int xdim, int ydim,
+                              int n_y, hipStream_t st, bool* supported);
+bool f32_sampler_supported(int mode, int width, int n_hidden, int xdim, int ydim);
+hipError_t launch_f32_forward(const F32ForwardParams& p, int width, int ot, hipStream_t st, bool* supported);
+hipError_t launch_f32_l1_prep(const F32L1PrepParams& p, int n_y, hipStream_t st);
 
 hipError_t launch_histogram(const float* x, long long n, int d, int nbins, double lo, double hi, int n_hist,
                             unsigned int* counts, hipStream_t st);

@@ -487,15 +487,22 @@ em_sampler_kernel(SamplerParams p) {
   const long long c_rd = valid ? c_local : 0;
   float x[D];
   Rng rng;
+  bool lost = false;  // the hand-over never arrived: the tile's output is poisoned and reported
   if (sg.kind == 2) {  // resume the tile the previous wave of the grid handed over
     const size_t slot = (size_t)yi * n_waves + gw - 1;
     for (unsigned spins = 0; __hip_atomic_load(p.xflag + slot, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0u;) {
-      if (++spins > (1u << 22)) break;  // bounded: never hang the GPU (the flag is set C - S steps early)
+      // bounded: never hang the GPU (the flag is normally set C - S steps early). Giving up is an
+      // error the host sees through dmip_device_status, never silently wrong chains.
+      if (++spins > p.spin_limit) {
+        lost = true;
+        break;
+      }
       __builtin_amdgcn_s_sleep(8);
     }
+    if (lost && lane == 0) __hip_atomic_store(p.err, kErrHandover, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const float* src = p.xfer + slot * XW;
 #pragma unroll
-    for (int k = 0; k < D; ++k) x[k] = src[k * 64 + lane];
+    for (int k = 0; k < D; ++k) x[k] = lost ? __builtin_nanf("") : src[k * 64 + lane];
     rng.s0 = __float_as_uint(src[(D + 0) * 64 + lane]);
     rng.s1 = __float_as_uint(src[(D + 1) * 64 + lane]);
     rng.s2 = __float_as_uint(src[(D + 2) * 64 + lane]);
@@ -595,7 +602,8 @@ em_sampler_kernel(SamplerParams p) {
     dst[(D + 2) * 64 + lane] = __uint_as_float(rng.s2);
     dst[(D + 3) * 64 + lane] = __uint_as_float(rng.s3);
     __threadfence();  // every lane's state is visible device-wide before the flag
-    if (lane == 0) __hip_atomic_store(p.xflag + slot, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0 && !(p.debug_flags & 1))
+      __hip_atomic_store(p.xflag + slot, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   } else if (sg.kind != 3 && valid && h == 0) {
     float* dst = p.x_out + ((size_t)yi * p.n_chains + c_local) * D;
 #pragma unroll
@@ -772,14 +780,10 @@ __global__ void schedule_kernel(int S, float T, float bmin, float bdiff, float* 
 // workgroups per y: enough to fill every CU slot once (the kernel balances the work inside a
 // workgroup), never more than one per NW tiles
 template <typename Kern>
-static unsigned sampler_wgs_per_y(Kern kern, int nthreads, long long n_chains, int n_y) {
-  static int slots = -1;  // one value per kernel instantiation
-  if (slots < 0) {
-    int dev = 0, n_cu = 256, per_cu = 1;
-    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, nthreads, 0) != hipSuccess || per_cu < 1) per_cu = 1;
-    slots = (n_cu > 0 ? n_cu : 256) * per_cu;
-  }
+static unsigned sampler_wgs_per_y(Kern kern, int nthreads, long long n_chains, int n_y, hipStream_t st) {
+  // the hand-over schedule needs every workgroup of the grid resident at once, so the slot count is
+  // that of the stream's device (cached per device and kernel instantiation)
+  const int slots = resident_slots(kern, nthreads, st);
   const long long nw = nthreads / 64;
   const long long tiles = (n_chains + 31) / 32;
   long long g = slots / (n_y > 0 ? n_y : 1);
@@ -797,12 +801,13 @@ static hipError_t with_xfer(SamplerParams& p, const dim3& grid, int nw, int d, h
   if (e != hipSuccess) return e;
   p.xfer = (float*)*buf;
   p.xflag = (unsigned*)(*buf + state_bytes);
-  return hipMemsetAsync(p.xflag, 0, slots * sizeof(unsigned), st);
+  // state and flags zeroed: nothing in the buffer is ever uninitialised memory
+  return hipMemsetAsync(*buf, 0, state_bytes + slots * sizeof(unsigned), st);
 }
 
 template <int MODE, int W, int NL, int D, int M, int NW, int R, bool RES>
 static hipError_t launch_sampler_t(const SamplerParams& p_in, int n_y, hipStream_t st) {
-  const dim3 grid(sampler_wgs_per_y(em_sampler_kernel<MODE, W, NL, D, M, NW, R, RES, false>, NW * 64, p_in.n_chains, n_y),
+  const dim3 grid(sampler_wgs_per_y(em_sampler_kernel<MODE, W, NL, D, M, NW, R, RES, false>, NW * 64, p_in.n_chains, n_y, st),
                   (unsigned)n_y);
   SamplerParams p = p_in;
   char* buf = nullptr;
@@ -867,7 +872,7 @@ hipError_t launch_sampler(const SamplerParams& p_in, int mode, int width, int n_
   if (mode == MODE_CDE && width == 256 && n_hidden == 3 && xdim == 3 &&
       ((var >= 101 && var <= 107) || (var >= 201 && var <= 203))) {
     const dim3 grid(sampler_wgs_per_y(em_sampler_kernel<MODE_CDE, 256, 3, 3, 0, 8, 4, false, false>, 512,
-                                      p_in.n_chains, n_y),
+                                      p_in.n_chains, n_y, st),
                     (unsigned)n_y);
     SamplerParams p = p_in;
     char* buf = nullptr;

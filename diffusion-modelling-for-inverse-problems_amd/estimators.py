@@ -7,8 +7,13 @@ reverse-SDE kernel for all num_steps, the chain state never leaving the register
   * PosteriorDiffusionEstimator: dmip_em_sample_posterior (prior + likelihood networks in one kernel);
   * CDiffE (repaired sampler): dmip_em_sample_cdiffe;
   * DPS (BASELINE config 4, prior score net + forward-model guidance): dmip_dps_sample.
-Shapes the library has no fused kernel for (dmip_sampler_supported) step through per-step launches
-of the MFMA network kernel (dmip_mlp_forward) with the SDE update as device tensor ops.
+Precision (`model.precision`, or `precision=` per call; default from $DMIP_PRECISION, else "bf16"):
+"bf16" runs the network GEMMs with bf16 MFMA operands (the throughput mode, BASELINE headline);
+"fp32" runs them in exact f32 (v_mfma_f32_16x16x4_f32), the reference's own arithmetic (the parity
+mode). A shape with a fused f32 kernel but no fused bf16 one (the Posterior / CDiffE samplers at width
+512) runs the f32 kernel. Shapes with no fused kernel at all step through per-step launches of the
+network kernel (dmip_mlp_forward) with the SDE update as device tensor ops and the kernels'
+chain-keyed RNG (so sharding stays bit-identical there too).
 There is no CPU sampling path: without a HIP device the samplers raise.
 
 RNG: the reference draws x0 and the per-step noise from torch's global generator. Here every chain
@@ -16,6 +21,8 @@ has its own counter-keyed stream (seed, global chain index, y index); the seed i
 torch's global generator, so torch.manual_seed(s) still makes a sampling call reproducible, and the
 samples of a chain do not depend on how chains are split over workgroups or GPUs.
 """
+import os
+
 import numpy as np
 import torch
 from torch import nn
@@ -39,6 +46,21 @@ def _draw_seed():
     return int(torch.randint(0, 2 ** 62, (1,)).item())
 
 
+def default_precision():
+    return os.environ.get("DMIP_PRECISION", "bf16")
+
+
+def _fused_precision(precision, mode, width, n_hidden, xdim, ydim):
+    """The precision a fused kernel runs this shape in: the requested one, else exact f32 when only
+    that is compiled (bf16 -> fp32 never loses accuracy); None when neither is (per-step loop)."""
+    _lib.precision_code(precision)
+    if _lib.sampler_supported(width, n_hidden, xdim, ydim, mode, precision):
+        return precision
+    if precision == "bf16" and _lib.sampler_supported(width, n_hidden, xdim, ydim, mode, "fp32"):
+        return "fp32"
+    return None
+
+
 class BaseClassDiffusionModel:
     """models/diffusion.py:14-58."""
 
@@ -46,17 +68,20 @@ class BaseClassDiffusionModel:
         self.xdim = xdim
         self.ydim = ydim
         self.sde = None
+        self.precision = default_precision()  # "bf16" | "fp32": arithmetic of the sampler's network GEMMs
 
     def __call__(self, *args, **kwargs):
         return self.forward(*args, **kwargs)
 
     # ----------------------------------------------------------------- sampling API
-    def forward(self, y, num_samples=2000, num_steps=200, mean=0, std=1):
+    def forward(self, y, num_samples=2000, num_steps=200, mean=0, std=1, precision=None):
         """Posterior samples for one observation y (ydim,): np.ndarray (num_samples, xdim) float32
         (models/diffusion.py:27-46). Under torch.distributed with world_size > 1 the chains are
-        sharded over the ranks and every rank returns all num_samples (parallel.sample_sharded)."""
+        sharded over the ranks and every rank returns all num_samples (parallel.sample_sharded).
+        `precision` overrides self.precision for this call."""
         from . import parallel
-        x = parallel.sample_sharded(self, y, num_samples, num_steps, mean, std)
+        x = parallel.sample_sharded(self, y, num_samples, num_steps, mean, std, precision=precision)
+        _lib.device_status(x.device)  # asynchronous kernel failures surface here, not as silent NaNs
         return x.cpu().numpy()
 
     def _exec_device(self, y):
@@ -75,10 +100,11 @@ class BaseClassDiffusionModel:
         return ys.reshape(-1, self.ydim).contiguous()
 
     def sample_device(self, y, num_samples, num_steps=200, mean=0, std=1, seed=None, chain_offset=0,
-                      noise=None):
+                      noise=None, precision=None):
         """Device-resident samples (n_y, num_samples, xdim) for ys (n_y, ydim) -- no host copy.
         `chain_offset` selects a shard of a larger run; `noise` injects standard normals
-        (num_steps + 1, n_y, num_samples, xdim) (slot 0 -> x0) in place of the internal RNG."""
+        (num_steps + 1, n_y, num_samples, xdim) (slot 0 -> x0) in place of the internal RNG;
+        `precision` ("bf16" | "fp32") overrides self.precision."""
         raise NotImplementedError
 
     def _prepare(self, y, num_samples, num_steps, nets):
@@ -141,16 +167,28 @@ class CDE(BaseClassDiffusionModel):
         self.sde = sdes.PluginReverseSDE(sdes.VariancePreservingSDE(), score_net, T=1, debias=True)
 
     def sample_device(self, y, num_samples, num_steps=200, mean=0, std=1, seed=None, chain_offset=0,
-                      noise=None):
+                      noise=None, precision=None):
         net = self.sde.a
         dev, ys, sde, out = self._prepare(y, num_samples, num_steps, [net])
         handle = net.dmip_handle(dev, self.xdim)
         seed = _draw_seed() if seed is None else seed
+        prec = _fused_precision(precision or self.precision, _lib.DMIP_SAMPLER_CDE, handle.width, handle.n_hidden,
+                                self.xdim, self.ydim)
         if noise is not None:
             noise = noise.to(device=dev, dtype=torch.float32).contiguous()
             if tuple(noise.shape) != (int(num_steps) + 1, ys.shape[0], int(num_samples), self.xdim):
                 raise ValueError("noise must have shape (num_steps+1, n_y, num_samples, xdim)")
-        _lib.em_sample(handle, sde, ys, num_samples, chain_offset, num_steps, mean, std, seed, out, noise)
+        if prec is None:
+            if noise is not None:
+                raise ValueError("noise injection needs a fused CDE kernel for this shape")
+            base = self.sde.base_sde
+
+            def drift(x, y, tvec):
+                return base.g(tvec, x) * self.sde.a(x, y, tvec) - base.f(tvec, x)
+
+            return _em_device_loop(self, ys, int(num_samples), int(num_steps), mean, std, seed, chain_offset,
+                                   drift, self.xdim, self.xdim)
+        _lib.em_sample(handle, sde, ys, num_samples, chain_offset, num_steps, mean, std, seed, out, noise, prec)
         return out
 
     def train_epoch(self, optimizer, loss_fn, epoch_data_loader):
@@ -171,31 +209,46 @@ class CDE(BaseClassDiffusionModel):
         return self._train_loop(optimizer, epoch_data_loader, batch_loss)
 
 
+_LOOP_STREAM = 1 << 62  # RNG stream ids of the per-step loop (disjoint from the fused kernels' y indices)
+
+
+def _loop_normals(seed, chain_offset, stream_id, n, d, dev):
+    """(n, d) normals of the kernels' chain-keyed generator for chains [chain_offset, chain_offset + n)."""
+    out = torch.empty(n, 2 * ((d + 1) // 2), device=dev, dtype=torch.float32)
+    _lib.rng_normals(seed, chain_offset, stream_id, n, (d + 1) // 2, out)
+    return out[:, :d]
+
+
 def _em_device_loop(model, ys, num_samples, num_steps, mean, std, seed, chain_offset, drift, zdim,
                     keep, y_resample=None):
     """Reverse-SDE EM loop on device tensors for shapes without a compiled fused sampler: the
-    network evaluations are dmip_mlp_forward launches, the update follows
-    models/diffusion.py:40-42 (same rounding order as the fused kernel)."""
+    network evaluations are dmip_mlp_forward launches (model precision), the update follows
+    models/diffusion.py:40-42 (same rounding order as the fused kernel). Noise comes from the
+    kernels' counter-keyed generator, keyed by (seed, global chain index, stream = (y index, step)),
+    so a shard of a run draws exactly the chains of the full run (bit-identical union)."""
     dev = ys.device
     base = model.sde.base_sde
     T = float(model.sde.T)
     n_y = ys.shape[0]
-    gen = torch.Generator(device=dev)
-    gen.manual_seed((seed + 7919 * int(chain_offset)) & 0x7FFFFFFFFFFFFFFF)
     outs = []
     ts = torch.linspace(0, 1, num_steps + 1) * T
     delta = T / num_steps
+    off = int(chain_offset)
     with torch.no_grad():
         for k in range(n_y):
             y = ys[k]
-            x = torch.randn(num_samples, zdim, device=dev, generator=gen) * std + mean
+            sid = _LOOP_STREAM + (k << 40)
+            x = _loop_normals(seed, off, sid, num_samples, zdim, dev) * std + mean
             for i in range(num_steps):
                 tau = (T - ts[i]).item()
                 tvec = torch.full((num_samples, 1), tau, device=dev)
-                z_in = x if y_resample is None else y_resample(x, y, tau, gen)
+                eps_y = None
+                if y_resample is not None:
+                    eps_y = _loop_normals(seed, off, sid + (1 << 39) + i, num_samples, model.ydim, dev)
+                z_in = x if y_resample is None else y_resample(x, y, tau, eps_y)
                 mu = drift(z_in, y, tvec)
                 sigma = base.g(tvec, z_in)
-                xi = torch.randn(z_in.shape, device=dev, generator=gen)
+                xi = _loop_normals(seed, off, sid + 1 + i, num_samples, z_in.shape[1], dev)
                 z = z_in + delta * mu + delta ** 0.5 * sigma * xi
                 x = z[:, :keep] if keep < z.shape[1] else z
             outs.append(x[:, :keep])
@@ -216,35 +269,38 @@ class CDiffE(BaseClassDiffusionModel):
         score_net = MLP(xdim + ydim + 1, xdim + ydim, hidden_layers, nn.Tanh()).to(device)
         self.sde = sdes.PluginReverseSDE(sdes.VariancePreservingSDE(), score_net, T=1, debias=True)
 
-    def forward(self, y, num_samples=2000, num_steps=200, mean=0, std=1, corrector_steps=0, snr=0.16):
+    def forward(self, y, num_samples=2000, num_steps=200, mean=0, std=1, corrector_steps=0, snr=0.16,
+                precision=None):
         """As BaseClassDiffusionModel.forward; `corrector_steps` > 0 adds Langevin corrector steps
         before every predictor step (predictor-corrector sampling, BASELINE config 3; see
         dmip_em_sample_cdiffe in include/dmip.h for the definition)."""
         from . import parallel
         x = parallel.sample_sharded(self, y, num_samples, num_steps, mean, std,
-                                    corrector_steps=corrector_steps, snr=snr)
+                                    corrector_steps=corrector_steps, snr=snr, precision=precision)
+        _lib.device_status(x.device)
         return x.cpu().numpy()
 
     def sample_device(self, y, num_samples, num_steps=200, mean=0, std=1, seed=None, chain_offset=0,
-                      noise=None, corrector_steps=0, snr=0.16):
+                      noise=None, corrector_steps=0, snr=0.16, precision=None):
         if noise is not None:
             raise ValueError("noise injection is only implemented for the fused CDE sampler")
         net = self.sde.a
         dev, ys, sde, out = self._prepare(y, num_samples, num_steps, [net])
         seed = _draw_seed() if seed is None else seed
         handle = net.dmip_handle(dev, self.xdim)
-        if _lib.sampler_supported(handle.width, handle.n_hidden, self.xdim, self.ydim, _lib.DMIP_SAMPLER_CDIFFE):
+        prec = _fused_precision(precision or self.precision, _lib.DMIP_SAMPLER_CDIFFE, handle.width,
+                                handle.n_hidden, self.xdim, self.ydim)
+        if prec is not None:
             _lib.em_sample_cdiffe(handle, sde, ys, num_samples, chain_offset, num_steps, mean, std, seed, out,
-                                  corrector_steps, snr)
+                                  corrector_steps, snr, prec)
             return out
         if corrector_steps:
             raise ValueError("the predictor-corrector sampler needs a compiled fused CDiffE kernel for this shape")
         base = self.sde.base_sde
         xd = self.xdim
 
-        def y_resample(x, y, tau, gen):
+        def y_resample(x, y, tau, eps):
             tt = torch.full((x.shape[0], 1), tau, device=x.device)
-            eps = torch.randn(x.shape[0], self.ydim, device=x.device, generator=gen)
             y_t = base.mean_weight(tt) * y + base.var(tt) ** 0.5 * eps
             return torch.cat([x[:, :xd], y_t], dim=1)
 
@@ -280,7 +336,7 @@ class PosteriorDiffusionEstimator(BaseClassDiffusionModel):
         self.loss_fn = PosteriorLoss
 
     def sample_device(self, y, num_samples, num_steps=200, mean=0, std=1, seed=None, chain_offset=0,
-                      noise=None):
+                      noise=None, precision=None):
         if noise is not None:
             raise ValueError("noise injection is only implemented for the fused CDE sampler")
         score = self.sde.a
@@ -288,10 +344,13 @@ class PosteriorDiffusionEstimator(BaseClassDiffusionModel):
         seed = _draw_seed() if seed is None else seed
         prior = score.prior_net.dmip_handle(dev, self.xdim)
         lik = score.likelihood_net.dmip_handle(dev, self.xdim)
-        if (prior.width, prior.n_hidden) == (lik.width, lik.n_hidden) and _lib.sampler_supported(
-                lik.width, lik.n_hidden, self.xdim, self.ydim, _lib.DMIP_SAMPLER_POSTERIOR):
+        prec = None
+        if (prior.width, prior.n_hidden) == (lik.width, lik.n_hidden):
+            prec = _fused_precision(precision or self.precision, _lib.DMIP_SAMPLER_POSTERIOR, lik.width,
+                                    lik.n_hidden, self.xdim, self.ydim)
+        if prec is not None:
             _lib.em_sample_posterior(prior, lik, sde, ys, num_samples, chain_offset, num_steps, mean, std, seed,
-                                     out)
+                                     out, prec)
             return out
         base = self.sde.base_sde
 
@@ -360,7 +419,9 @@ class DPS(BaseClassDiffusionModel):
         m.sde.a.prior_net.to(next(pn.parameters()).device)
         return m
 
-    def sample_device(self, y, num_samples, num_steps=200, mean=0, std=1, seed=None, chain_offset=0, noise=None):
+    def sample_device(self, y, num_samples, num_steps=200, mean=0, std=1, seed=None, chain_offset=0, noise=None,
+                      precision=None):
+        """Exact f32 always (dmip_dps_sample); `precision` is accepted for API symmetry."""
         if noise is not None:
             raise ValueError("noise injection is only implemented for the fused CDE sampler")
         from .problems import surrogate_handle

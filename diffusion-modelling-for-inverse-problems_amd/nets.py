@@ -7,8 +7,9 @@ hidden layer apply tanh twice: the reference stores its activation module a seco
 and the next Linear and shifts the numbering.
 
 Evaluation on a HIP device with autograd off goes to the fused MFMA kernel
-(libdmip dmip_mlp_forward); the weights are packed once per parameter snapshot. Autograd (the
-training losses) uses the eager module chain.
+(libdmip dmip_mlp_forward) -- in exact f32 by default (`dmip_precision = "fp32"`, the reference's own
+arithmetic, e.g. for the evaluate drivers' score MSE), or with bf16 operands (`"bf16"`); the weights
+are packed once per parameter snapshot. Autograd (the training losses) uses the eager module chain.
 """
 import collections
 
@@ -34,6 +35,7 @@ class _TanhChainMLP(nn.Sequential):
         super().__init__(collections.OrderedDict(mods))
         self.act = activation
         self._dmip = None
+        self.dmip_precision = "fp32"  # arithmetic of the HIP forward (dmip_mlp_forward): "fp32" or "bf16"
 
     # -------------------------------------------------------------- packed HIP weights
     def linear_layers(self):
@@ -72,7 +74,7 @@ class _TanhChainMLP(nn.Sequential):
             y_stride = yc.shape[1] if yc.shape[0] == n and n != 1 else 0
             yc = yc.contiguous()
         out = torch.empty(n, self.output_dim, device=dev, dtype=torch.float32)
-        _lib.mlp_forward(h, xc, yc, tt, out, y_stride, t_stride)
+        _lib.mlp_forward(h, xc, yc, tt, out, y_stride, t_stride, getattr(self, "dmip_precision", "fp32"))
         return out
 
 

@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define DMIP_ABI_VERSION 4
+#define DMIP_ABI_VERSION 5
 
 typedef enum {
   DMIP_OK = 0,
@@ -37,9 +37,14 @@ typedef enum { DMIP_INPUT_X_Y_T = 0, DMIP_INPUT_X_T = 1 } dmip_input_layout;
  * time as `self.act` (nets.py:26). DMIP_ACT_TANH is the single-tanh chain. */
 typedef enum { DMIP_ACT_TANH_TWICE_FIRST = 0, DMIP_ACT_TANH = 1 } dmip_act;
 
-/* Arithmetic of the network GEMMs: bf16 MFMA operands with fp32 accumulation (layer 1 takes its
- * inputs as split hi+lo bf16, i.e. ~fp32); the chain state and the SDE update are always fp32. */
-typedef enum { DMIP_PREC_BF16 = 0 } dmip_precision;
+/* Arithmetic of the network GEMMs; the chain state, the schedule and the SDE update are fp32 in both.
+ *   DMIP_PREC_BF16  bf16 MFMA operands, fp32 accumulation (layer 1 takes its inputs as split hi+lo
+ *                   bf16, i.e. ~fp32); tanh by exp2 + rcp. The throughput mode (BASELINE headline).
+ *   DMIP_PREC_F32   exact f32: every product and sum in f32 (v_mfma_f32_16x16x4_f32, an fmaf chain),
+ *                   libm-accurate tanh -- the reference's own arithmetic (nets.py:32-35 in fp32).
+ *                   The parity mode; ~1/6 of the bf16 throughput. Same RNG stream per chain as bf16,
+ *                   so the two modes are comparable chain by chain. */
+typedef enum { DMIP_PREC_BF16 = 0, DMIP_PREC_F32 = 1 } dmip_precision;
 
 /* VariancePreservingSDE (sdes.py:9-19): beta(t) = beta_min + (beta_max - beta_min) t. */
 typedef struct {
@@ -251,8 +256,18 @@ int dmip_em_sample_stamps(const dmip_mlp* net, const dmip_vpsde* sde, const floa
 
 const char* dmip_last_error(void);
 int dmip_abi_version(void);
-/* Non-zero when this build has a kernel for the given sampler (dmip_sampler_mode) and shape. */
+
+/* Synchronise `stream` and report asynchronous kernel failures of its device since the last call:
+ * DMIP_OK, or DMIP_ERR_HIP with dmip_last_error() naming the failure (the status is then cleared).
+ * Today the only such failure is the balanced sampler's hand-over timeout (a consumer wave gave up
+ * waiting for the wave that ran the first part of its tile; those chains are written as NaN).
+ * The Python layer calls it after every host-facing sampling call (model(y, ...)). */
+int dmip_device_status(void* stream);
+/* Non-zero when this build has a kernel for the given sampler (dmip_sampler_mode) and shape in bf16
+ * (dmip_sampler_supported) or exact f32 (dmip_sampler_supported_f32: widths 64/128/256/512, 1-3
+ * hidden layers, xdim 2 or 3; CDiffE for (xdim, ydim) = (2, 2) and (3, 23)). */
 int dmip_sampler_supported(int mode, int width, int n_hidden, int xdim, int ydim);
+int dmip_sampler_supported_f32(int mode, int width, int n_hidden, int xdim, int ydim);
 
 #ifdef __cplusplus
 }

@@ -24,9 +24,9 @@ step() {  # step <name> <seconds> <cmd...>
   esac
 }
 
-step pytest_gpu 600 python -m pytest tests -m gpu -q -p no:cacheprovider -rf
+step pytest_gpu 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread -p no:cacheprovider -rf
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-step bench 600 python bench.py --steps 5 --warmup 2
+step bench 600 python -u bench.py --steps 10 --warmup 3
 cd /tmp && mkdir -p prof && cd - > /dev/null
 step rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
   python bench.py --steps 3 --warmup 1 --no-cpu-baseline

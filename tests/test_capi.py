@@ -32,7 +32,7 @@ def test_exports_every_declared_symbol(lib, dmip):
 
 
 def test_abi_version(lib, dmip):
-    assert lib.dmip_abi_version() == dmip._lib.ABI_VERSION == 4
+    assert lib.dmip_abi_version() == dmip._lib.ABI_VERSION == 5
 
 
 def test_supported_shapes(lib, dmip):
@@ -45,6 +45,22 @@ def test_supported_shapes(lib, dmip):
     assert sup(256, 3, 2, 2, P) and sup(64, 2, 3, 23, P) and not sup(512, 3, 3, 23, P)
     assert sup(256, 3, 3, 23, C) and sup(128, 3, 2, 2, C)
     assert not sup(256, 3, 3, 5, C)  # CDiffE feeds y_t through layer 1: compiled ydim only
+    # exact f32: every mode at widths 64..512 and 1..3 hidden layers (the reference configs' [512]*3)
+    for mode in (0, P, C):
+        assert sup(512, 3, 3, 23, mode, "fp32") and sup(64, 2, 2, 2, mode, "fp32") and sup(256, 1, 3, 23, mode, "fp32")
+    assert not sup(96, 3, 3, 23, 0, "fp32") and not sup(256, 4, 3, 23, 0, "fp32") and not sup(256, 3, 3, 5, C, "fp32")
+    with pytest.raises(ValueError):
+        sup(256, 3, 3, 23, 0, "fp16")
+
+
+def test_precision_rejected_before_launch(lib, dmip):
+    L = dmip._lib
+    sde = L.vpsde(0.1, 20.0, 1.0)
+    # unknown precision code: INVALID before any device work (no handle needed to reach the check)
+    rc = lib.dmip_mlp_forward(None, None, None, 0, None, 0, 4, None, 7, None)
+    assert rc == L.DMIP_ERR_INVALID
+    rc = lib.dmip_em_sample(None, ctypes.byref(sde), None, 1, 2, 2, 10, 0, 10, 0.0, 1.0, 1, 7, None, None, None)
+    assert rc == L.DMIP_ERR_INVALID
 
 
 def test_create_rejects_bad_arguments(lib, dmip):

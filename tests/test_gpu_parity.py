@@ -614,3 +614,23 @@ def test_balanced_schedule_other_samplers(dmip, cls):
     for lo in (0, 40000, n - 500):
         part = m.sample_device(y, 500, S, seed=3, chain_offset=lo)[0]
         assert torch.equal(full[lo:lo + 500], part), lo
+
+
+def test_handover_timeout_is_reported_not_silent(dmip, golden, monkeypatch):
+    """Test hook DMIP_DEBUG_NO_HANDOVER=1: the balanced schedule's producers never publish their split
+    tiles and the consumers give up after a short spin bound. The affected chains come out NaN and the
+    device status turns the failure into a RuntimeError (never silently wrong chains); the next clean
+    run reports nothing."""
+    m = _cde(dmip, "scat", golden("ckpt_scat.npz"), "")
+    y = torch.from_numpy(golden("data_scat.npz")["y_test"][0]).to(DEV)
+    monkeypatch.setenv("DMIP_DEBUG_NO_HANDOVER", "1")
+    x = m.sample_device(y, 100000, 8, seed=1)  # > one round: split tiles exist
+    with pytest.raises(RuntimeError, match="hand-over"):
+        dmip._lib.device_status(x.device)
+    assert torch.isnan(x).any() and torch.isfinite(x).any()
+    with pytest.raises(RuntimeError, match="hand-over"):
+        m(y, num_samples=100000, num_steps=8)
+    monkeypatch.delenv("DMIP_DEBUG_NO_HANDOVER")
+    x = m.sample_device(y, 100000, 8, seed=1)
+    dmip._lib.device_status(x.device)
+    assert torch.isfinite(x).all()
