@@ -305,7 +305,8 @@ __global__ void __launch_bounds__(Shape<W>::NW * 64, 1) f32_sampler_kernel(F32Sa
       v[C::NV0 - 1] = cf.tau;
 
       // a(x) at this step's time and y_t: output rows 0..D-1 of every chain, on all its lanes
-      auto score = [&](const float (&vin)[C::NV0], float (&a)[D]) {
+      // always inlined: an outlined call would put the activation arrays on the scratch stack
+      auto score = [&](const float (&vin)[C::NV0], float (&a)[D]) __attribute__((always_inline)) {
         f32x4 out[1];
         float b0[C::K1Q0];
         l1_operand<C::NV0, C::K1Q0>(vin, g, b0);
