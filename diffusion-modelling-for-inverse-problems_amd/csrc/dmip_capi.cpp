@@ -17,9 +17,11 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <new>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "../../include/dmip.h"
@@ -113,6 +115,32 @@ int upload(T** dst, const std::vector<T>& src) {
 }
 
 }  // namespace
+
+namespace dmip {
+
+int resident_slots_impl(const void* fn, int nthreads, hipStream_t st) {
+  static std::mutex mu;
+  static std::map<std::tuple<const void*, int, int>, int> cache;
+  const int dev = stream_device(st);
+  const auto key = std::make_tuple(fn, nthreads, dev);
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+  }
+  int n_cu = 256, per_cu = 1, cur = dev;
+  (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+  (void)hipGetDevice(&cur);
+  if (cur != dev) (void)hipSetDevice(dev);  // the occupancy query is for the current device
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, nthreads, 0) != hipSuccess || per_cu < 1) per_cu = 1;
+  if (cur != dev) (void)hipSetDevice(cur);
+  const int slots = (n_cu > 0 ? n_cu : 256) * per_cu;
+  std::lock_guard<std::mutex> lk(mu);
+  cache[key] = slots;
+  return slots;
+}
+
+}  // namespace dmip
 
 struct dmip_mlp {
   int in_dim = 0, out_dim = 0, n_hidden = 0, width = 0, act_mode = 0, layout = 0, xdim = 0;
@@ -719,13 +747,8 @@ int dmip_loss_grad(int in_dim, int out_dim, int n_hidden, const int* widths, int
   p.icb[1] = cfg->ic_b[1];
   // one workgroup per CU (LDS-bound; one wave per SIMD), 16-sample tiles strided over the waves
   int n_cu = 256;
-  {
-    int dev = 0;
-    hipDeviceProp_t prop;
-    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess &&
-        prop.multiProcessorCount > 0)
-      n_cu = prop.multiProcessorCount;
-  }
+  (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dmip::stream_device(st));
+  if (n_cu < 1) n_cu = 256;
   const int64_t tiles = (batch + 15) / 16;
   const int64_t per_wg = dmip::train_waves_per_wg();
   int n_wg = (int)std::min<int64_t>((int64_t)n_cu, (tiles + per_wg - 1) / per_wg);
@@ -778,13 +801,10 @@ int surrogate_check(const dmip_surrogate* s, int64_t n) {
   return DMIP_OK;
 }
 
-int surrogate_n_wg(int64_t rows) {
+int surrogate_n_wg(int64_t rows, hipStream_t st) {
   int n_cu = 256;
-  int dev = 0;
-  hipDeviceProp_t prop;
-  if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess &&
-      prop.multiProcessorCount > 0)
-    n_cu = prop.multiProcessorCount;
+  (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dmip::stream_device(st));
+  if (n_cu < 1) n_cu = 256;
   const int64_t per = dmip::surrogate_rows_per_wg();
   return (int)std::max<int64_t>(1, std::min<int64_t>(n_cu, (rows + per - 1) / per));
 }
@@ -883,7 +903,7 @@ int dmip_surrogate_forward(const dmip_surrogate* s, const float* x_dev, int64_t 
   p.x = x_dev;
   p.n = n;
   p.f_out = f_out_dev;
-  hipError_t e = dmip::launch_surrogate_eval(p, 0, surrogate_n_wg(n), (hipStream_t)stream);
+  hipError_t e = dmip::launch_surrogate_eval(p, 0, surrogate_n_wg(n, (hipStream_t)stream), (hipStream_t)stream);
   return e == hipSuccess ? DMIP_OK : hip_fail(e, "surrogate_forward launch");
 }
 
@@ -902,7 +922,7 @@ int dmip_log_posterior(const dmip_surrogate* s, const dmip_scat_noise* noise, co
   p.n = n;
   p.e_out = e_out_dev;
   p.g_out = grad_out_dev;
-  hipError_t e = dmip::launch_surrogate_eval(p, grad_out_dev ? 2 : 1, surrogate_n_wg(n), (hipStream_t)stream);
+  hipError_t e = dmip::launch_surrogate_eval(p, grad_out_dev ? 2 : 1, surrogate_n_wg(n, (hipStream_t)stream), (hipStream_t)stream);
   return e == hipSuccess ? DMIP_OK : hip_fail(e, "log_posterior launch");
 }
 

@@ -3,7 +3,6 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
-#include <atomic>
 
 namespace dmip {
 
@@ -18,24 +17,15 @@ inline int stream_device(hipStream_t st) {
   return dev;
 }
 
-// number of workgroups of `kern` the stream's device holds at once (CUs x occupancy), cached per
-// device and kernel instantiation (thread-safe: a racing first query computes the same value)
+// number of workgroups of kernel `fn` the stream's device holds at once (CUs x occupancy), cached per
+// (kernel address, block size, device). Keyed by the kernel's ADDRESS: every sampler instantiation
+// has the same function type, and a type-keyed cache once handed one kernel's slot count to all of
+// them -- a grid larger than the resident set breaks the balanced schedule's co-residency.
+int resident_slots_impl(const void* fn, int nthreads, hipStream_t st);
+
 template <typename Kern>
 int resident_slots(Kern kern, int nthreads, hipStream_t st) {
-  static std::atomic<int> cache[kMaxDevices];
-  const int dev = stream_device(st);
-  const int di = dev >= 0 && dev < kMaxDevices ? dev : 0;
-  const int v = cache[di].load(std::memory_order_relaxed);
-  if (v > 0) return v;
-  int n_cu = 256, per_cu = 1, cur = dev;
-  (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
-  (void)hipGetDevice(&cur);
-  if (cur != dev) (void)hipSetDevice(dev);  // the occupancy query is for the current device
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, nthreads, 0) != hipSuccess || per_cu < 1) per_cu = 1;
-  if (cur != dev) (void)hipSetDevice(cur);
-  const int slots = (n_cu > 0 ? n_cu : 256) * per_cu;
-  cache[di].store(slots, std::memory_order_relaxed);
-  return slots;
+  return resident_slots_impl(reinterpret_cast<const void*>(kern), nthreads, st);
 }
 
 // Sampler modes (dmip_kernels.hip em_sampler_kernel)
