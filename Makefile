@@ -37,7 +37,30 @@ $(CSRC)/dmip_capi.o: $(CSRC)/dmip_capi.cpp $(HDRS)
 $(PKG)/libdmip.so: $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(OBJS) -o $@
 
-clean:
-	rm -f $(OBJS) $(PKG)/libdmip.so
+# microbenchmarks (scripts/ubench): built here, never committed
+UBENCH := scripts/ubench/valu_mix scripts/ubench/valu_rates
+ubench: $(UBENCH)
+scripts/ubench/%: scripts/ubench/%.hip
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 $< -o $@
 
-.PHONY: all clean
+# Host-only AddressSanitizer build of the C-ABI layer (argument validation, packing, handle
+# management): dmip_capi.cpp instrumented on the host side only (-Xarch_host), linked with the same
+# kernel objects, driven by tests/asan/capi_args.cpp through the calls that need no GPU.
+# dmip_capi.cpp has no device code: it compiles as plain host C++ against the HIP runtime headers.
+ASAN_DIR := build/asan
+HOSTCXX ?= /opt/rocm/lib/llvm/bin/clang++
+ASANFLAGS := -O1 -g -std=c++17 -fPIC -fsanitize=address -fno-omit-frame-pointer
+asan: $(ASAN_DIR)/capi_args
+$(ASAN_DIR)/dmip_capi_asan.o: $(CSRC)/dmip_capi.cpp $(HDRS)
+	@mkdir -p $(ASAN_DIR)
+	$(HOSTCXX) -x c++ -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include $(ASANFLAGS) -c $< -o $@
+$(ASAN_DIR)/libdmip_asan.so: $(filter-out $(CSRC)/dmip_capi.o,$(OBJS)) $(ASAN_DIR)/dmip_capi_asan.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -fsanitize=address $^ -o $@
+$(ASAN_DIR)/capi_args: tests/asan/capi_args.cpp $(ASAN_DIR)/libdmip_asan.so include/dmip.h
+	$(HOSTCXX) $(ASANFLAGS) $< -L$(ASAN_DIR) -ldmip_asan -Wl,-rpath,$(abspath $(ASAN_DIR)) -lpthread -o $@
+
+clean:
+	rm -f $(OBJS) $(PKG)/libdmip.so $(UBENCH)
+	rm -rf $(ASAN_DIR)
+
+.PHONY: all clean ubench asan

@@ -1,11 +1,11 @@
 """Training losses with the reference's API (losses.py:7-386).
 
 DSM, ScoreFPE (exact divergence + the total time-derivative of the score by autograd), the
-conditional ScoreFPE, DSM_PDE, PINN and Posterior losses. Round-1 status: these are PyTorch-ROCm
-autograd graphs (the reference's own arithmetic on the device), checked against the reference's
-values and parameter gradients (tests/golden/pinn_linear.npz). The fused HIP PINN/ScoreFPE
-training kernel (forward-mode jets through the MFMA net + hand-written backward) is the next row of
-SURVEY.md §8f (F1); it will slot in behind these same classes.
+conditional ScoreFPE, DSM_PDE, PINN and Posterior losses as PyTorch autograd graphs (the reference's
+own arithmetic, on any device), checked against the reference's values and parameter gradients
+(tests/golden/pinn_linear.npz). On a HIP device, CDE.train_epoch replaces the loss + backward of
+the supported (network, loss) pairs with the fused HIP loss-and-gradient kernel (csrc/dmip_train.hip,
+training.py); these classes stay the API and the reference for every other case.
 """
 import torch
 from torch import nn
@@ -65,14 +65,16 @@ class ScoreFPELoss(nn.Module):
         self.metric = metric
 
     def forward(self, s, x_t, t, beta, divergence_method='exact'):
-        assert s.shape == x_t.shape, 's and x_t need to have the same shape, but {} and {} was given, repsectively.'.format(s.shape, x_t.shape)
+        if s.shape != x_t.shape:
+            raise ValueError(f"score shape {tuple(s.shape)} differs from x_t shape {tuple(x_t.shape)}")
         n = x_t.shape[0]
         if divergence_method == 'exact':
             div = divergence(s, x_t)
         elif divergence_method in ['hutchinson', 'approx', 'approximate']:
             div = div_estimator(s, x_t)
         else:
-            raise ValueError('No valid value for divergence method specified. Need to be one of "exact","hutchinson","approx" or "approximate", but {} was given'.format(divergence_method))
+            raise ValueError(f"unknown divergence method {divergence_method!r} "
+                             "(one of 'exact', 'hutchinson', 'approx', 'approximate')")
         ds_dt = batch_gradient(s, t)
         potential = div + torch.sum(s ** 2, dim=1).view(-1, 1) + (x_t[:, None, :] @ s[:, :, None]).view(-1, 1)
         grad_x = torch.autograd.grad(potential, x_t, grad_outputs=torch.ones_like(div), retain_graph=True)[0]
@@ -81,7 +83,7 @@ class ScoreFPELoss(nn.Module):
             return torch.mean(torch.abs(r), dim=1).view(n, 1)
         if self.metric == 'L2':
             return torch.mean(r ** 2, dim=1).view(n, 1)
-        raise ValueError('No valid metric specified. Metric should be one of "L1" or "L2" but was {}'.format(self.metric))
+        raise ValueError(f"metric must be 'L1' or 'L2', got {self.metric!r}")
 
 
 class ConditionalScoreFPELoss(nn.Module):
@@ -100,7 +102,7 @@ class ConditionalScoreFPELoss(nn.Module):
             return torch.sum(r ** 2, dim=1)
         if self.metric == 'L1':
             return torch.sum(torch.abs(r), dim=1)
-        raise ValueError('No valid metric specified. Metric should be one of "L1" or "L2" but was {}'.format(self.metric))
+        raise ValueError(f"metric must be 'L1' or 'L2', got {self.metric!r}")
 
 
 def _score_and_cond(model, x, y, diffused_samples, t, g):

@@ -165,7 +165,8 @@ int dmip_loss_grad_supported(int in_dim, int out_dim, int n_hidden, const int* w
  * outside points dropped). Replaces: the np.histogramdd calls of the evaluate drivers
  * (main_diffusion_scatterometry.py:71-74).
  *   x_dev      [n_hist][n][d] fp32;  d in 1..3
- *   counts_dev [n_hist][nbins^d] uint32, accumulated (zero it first) */
+ *   counts_dev [n_hist][nbins^d] 32-bit counters, accumulated (zero it first); uint32 in the kernel --
+ *              an int32 buffer (what the Python layer allocates) holds the same bits for counts < 2^31 */
 int dmip_histogram(const float* x_dev, int64_t n, int d, int nbins, double lo, double hi, int n_hist,
                    uint32_t* counts_dev, void* stream);
 
