@@ -33,7 +33,7 @@ EXPORTED = (
     "dmip_em_sample_stamps", "dmip_em_sample_posterior", "dmip_em_sample_cdiffe", "dmip_loss_grad",
     "dmip_loss_grad_supported", "dmip_histogram", "dmip_surrogate_create", "dmip_surrogate_destroy",
     "dmip_surrogate_forward", "dmip_log_posterior", "dmip_mh_sample", "dmip_dps_sample", "dmip_device_status",
-    "dmip_sampler_supported_f32",
+    "dmip_sampler_supported_f32", "dmip_posterior_loss_grad",
 )
 DMIP_DPS_NLL, DMIP_DPS_NORM = 0, 1
 
@@ -67,6 +67,11 @@ def _declare(lib):
     lib.dmip_sampler_supported.argtypes = [_i32, _i32, _i32, _i32, _i32]
     lib.dmip_sampler_supported_f32.argtypes = [_i32, _i32, _i32, _i32, _i32]
     lib.dmip_device_status.argtypes = [_c_void_p]
+    _pp = ctypes.POINTER(_c_void_p)
+    lib.dmip_posterior_loss_grad.argtypes = [_i32, _i32, _i32, ctypes.POINTER(_i32), _pp, _pp, _pp, _pp, _c_void_p,
+                                             ctypes.POINTER(DmipScatNoise), _f32, ctypes.POINTER(DmipVpsde),
+                                             _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _c_void_p, _c_void_p,
+                                             _c_void_p, _c_void_p, _c_void_p]
     lib.dmip_mlp_create.argtypes = [_i32, _i32, _i32, ctypes.POINTER(_i32), _i32, _i32, _i32,
                                     ctypes.POINTER(_c_void_p), ctypes.POINTER(_c_void_p),
                                     ctypes.POINTER(_c_void_p)]
@@ -105,7 +110,7 @@ def _declare(lib):
     lib.dmip_dps_sample.argtypes = [_c_void_p, _c_void_p, ctypes.POINTER(DmipScatNoise), ctypes.POINTER(DmipVpsde),
                                     _c_void_p, _i32, _i64, _i64, _i32, _f32, _f32, _u64, _i32, _f32, _c_void_p,
                                     _c_void_p]
-    for name in ("dmip_device_status", "dmip_sampler_supported_f32", "dmip_dps_sample", "dmip_mlp_create", "dmip_mlp_destroy", "dmip_mlp_forward", "dmip_em_sample",
+    for name in ("dmip_posterior_loss_grad", "dmip_device_status", "dmip_sampler_supported_f32", "dmip_dps_sample", "dmip_mlp_create", "dmip_mlp_destroy", "dmip_mlp_forward", "dmip_em_sample",
                  "dmip_rng_words", "dmip_rng_normals", "dmip_schedule", "dmip_sampler_supported",
                  "dmip_em_sample_stamps", "dmip_em_sample_posterior", "dmip_em_sample_cdiffe",
                  "dmip_loss_grad", "dmip_loss_grad_supported", "dmip_histogram", "dmip_surrogate_create",
@@ -331,3 +336,19 @@ def dps_sample(prior, surrogate, noise, sde, y, n_chains, chain_offset, num_step
                                 int(n_chains), int(chain_offset), int(num_steps), float(mean), float(std),
                                 ctypes.c_uint64(int(seed) & 0xFFFFFFFFFFFFFFFF), int(mode), float(zeta), ptr(out),
                                 stream_of(y.device)))
+
+
+def posterior_loss_grad(prior_layers, lik_layers, surrogate, noise, lam, sde, x, y, t, eps, grad_prior, grad_lik,
+                        loss_out, target_out=None):
+    """dmip_posterior_loss_grad (A18): layers = [(weight, bias)] device fp32 tensors of the prior (MLP2) and
+    likelihood (MLP) networks; writes the flat reference-order gradients, loss_out[3] and optionally the
+    likelihood target."""
+    calls["posterior_loss_grad"] = calls.get("posterior_loss_grad", 0) + 1
+    L = len(prior_layers) - 1
+    widths = (_i32 * L)(*[int(prior_layers[i][0].shape[0]) for i in range(L)])
+    arr = lambda ts: (_c_void_p * (L + 1))(*[v.data_ptr() for v in ts])
+    check(lib().dmip_posterior_loss_grad(
+        int(x.shape[1]), int(y.shape[1]), L, widths, arr([w for w, _ in prior_layers]), arr([b for _, b in prior_layers]),
+        arr([w for w, _ in lik_layers]), arr([b for _, b in lik_layers]), surrogate.h, ctypes.byref(noise),
+        float(lam), ctypes.byref(sde), ptr(x), ptr(y), ptr(t), ptr(eps), int(x.shape[0]), ptr(grad_prior),
+        ptr(grad_lik), ptr(loss_out), ptr(target_out), stream_of(x.device)))

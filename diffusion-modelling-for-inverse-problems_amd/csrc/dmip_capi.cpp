@@ -1000,6 +1000,258 @@ int dmip_dps_sample(const dmip_mlp* prior, const dmip_surrogate* fwd, const dmip
   return e == hipSuccess ? DMIP_OK : hip_fail(e, "dps_sample launch");
 }
 
+}  // extern "C"
+
+// ---- A18: PosteriorLoss value + parameter gradients (GEMM-composed exact-f32 step, dmip_gemm.hip)
+namespace {
+
+struct MlpDims {
+  int L;                      // hidden layers; linear layers 0..L
+  std::vector<int> in, out;   // per linear layer
+};
+
+// one network's forward over the batch: layer inputs [B][in+1] (ones column last), hidden outputs
+// with their activation derivatives, output [B][out]
+struct MlpTape {
+  std::vector<float*> h;      // h[l]: input matrix of layer l, [B][in_l + 1]; h[0] is the caller's
+  std::vector<float*> d;      // d[l]: act'(z_l) of hidden layer l, [B][out_l]
+  float* out = nullptr;       // [B][out_L]
+};
+
+hipError_t mlp_forward_f32(const MlpDims& dm, const float* const* W, const float* const* b, MlpTape& tp, int64_t B,
+                           hipStream_t st) {
+  for (int l = 0; l <= dm.L; ++l) {
+    dmip::GemmParams g{};
+    g.a = tp.h[l];
+    g.lda = dm.in[l] + 1;
+    g.b = W[l];
+    g.ldb = dm.in[l];
+    g.m = B;
+    g.n = dm.out[l];
+    g.k = dm.in[l];
+    g.bias = b[l];
+    if (l < dm.L) {
+      g.c = tp.h[l + 1];
+      g.ldc = dm.out[l] + 1;
+      g.epi = l == 0 ? dmip::GEMM_EPI_BIAS_TANH2 : dmip::GEMM_EPI_BIAS_TANH;
+      g.aux_out = tp.d[l];
+      g.ldaux = dm.out[l];
+    } else {
+      g.c = tp.out;
+      g.ldc = dm.out[l];
+      g.epi = dmip::GEMM_EPI_BIAS;
+    }
+    hipError_t e = dmip::launch_gemm_f32(g, false, true, 1, st);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+// reverse pass from the output adjoint `adj` [B][out_L]: with grads != null, [dW_l | db_l] into the
+// flat reference-order gradient buffer; with in_grad != null, d/d(input) [B][in_0] (no parameter grads)
+hipError_t mlp_backward_f32(const MlpDims& dm, const float* const* W, const MlpTape& tp, const float* adj, int64_t B,
+                            float* delta_a, float* delta_b, float* grads, float* in_grad, float* part, int splits,
+                            hipStream_t st) {
+  std::vector<size_t> off(dm.L + 2, 0);
+  for (int l = 0; l <= dm.L; ++l) off[l + 1] = off[l] + (size_t)dm.out[l] * dm.in[l] + dm.out[l];
+  const float* dl = adj;  // adjoint of layer l's output, [B][out_l]
+  float* bufs[2] = {delta_a, delta_b};
+  for (int l = dm.L; l >= 0; --l) {
+    hipError_t e;
+    if (grads) {
+      dmip::GemmParams g{};
+      g.a = dl;
+      g.lda = dm.out[l];
+      g.b = tp.h[l];
+      g.ldb = dm.in[l] + 1;
+      g.m = dm.out[l];
+      g.n = dm.in[l] + 1;
+      g.k = B;
+      g.c = grads + off[l];
+      g.ldc = dm.in[l];
+      g.epi = dmip::GEMM_EPI_WGRAD;
+      g.bias_out = grads + off[l] + (size_t)dm.out[l] * dm.in[l];
+      g.part = part;
+      if ((e = dmip::launch_gemm_f32(g, true, false, splits, st)) != hipSuccess) return e;
+    }
+    if (l == 0 && !in_grad) break;
+    dmip::GemmParams g{};
+    g.a = dl;
+    g.lda = dm.out[l];
+    g.b = W[l];
+    g.ldb = dm.in[l];
+    g.m = B;
+    g.n = dm.in[l];
+    g.k = dm.out[l];
+    if (l > 0) {
+      float* nxt = bufs[l & 1];
+      g.c = nxt;
+      g.ldc = dm.in[l];
+      g.epi = dmip::GEMM_EPI_MUL_AUX;
+      g.aux_in = tp.d[l - 1];
+      g.ldaux = dm.in[l];
+      if ((e = dmip::launch_gemm_f32(g, false, false, 1, st)) != hipSuccess) return e;
+      dl = nxt;
+    } else {
+      g.c = in_grad;
+      g.ldc = dm.in[0];
+      g.epi = dmip::GEMM_EPI_NONE;
+      if ((e = dmip::launch_gemm_f32(g, false, false, 1, st)) != hipSuccess) return e;
+    }
+  }
+  return hipSuccess;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dmip_posterior_loss_grad(int xdim, int ydim, int n_hidden, const int* widths, const float* const* prior_w,
+                             const float* const* prior_b, const float* const* lik_w, const float* const* lik_b,
+                             const dmip_surrogate* fwd, const dmip_scat_noise* noise, float lam, const dmip_vpsde* sde,
+                             const float* x_dev, const float* y_dev, const float* t_dev, const float* eps_dev,
+                             int64_t batch, float* grad_prior_dev, float* grad_lik_dev, float* loss_out_dev,
+                             float* target_out_dev, void* stream) {
+  if (!widths || !prior_w || !prior_b || !lik_w || !lik_b || !fwd || !noise || !sde || !x_dev || !y_dev || !t_dev ||
+      !eps_dev || !grad_prior_dev || !grad_lik_dev || !loss_out_dev)
+    return fail(DMIP_ERR_INVALID, "null argument");
+  if (xdim != dmip::kSurXdim || ydim != dmip::kSurYdim)
+    return fail(DMIP_ERR_UNSUPPORTED, "PosteriorLoss: the scatterometry surrogate's shapes (xdim 3, ydim 23)");
+  if (n_hidden < 1 || n_hidden > 8) return fail(DMIP_ERR_UNSUPPORTED, "n_hidden must be in [1, 8]");
+  for (int i = 0; i < n_hidden; ++i)
+    if (widths[i] < 1 || widths[i] > 4096) return fail(DMIP_ERR_INVALID, "hidden widths must be in [1, 4096]");
+  for (int i = 0; i <= n_hidden; ++i)
+    if (!prior_w[i] || !prior_b[i] || !lik_w[i] || !lik_b[i]) return fail(DMIP_ERR_INVALID, "null layer pointer");
+  if (batch < 1) return fail(DMIP_ERR_INVALID, "batch must be >= 1");
+  if (!(noise->b > 0.0f) || !(noise->a >= 0.0f)) return fail(DMIP_ERR_INVALID, "noise model needs b > 0, a >= 0");
+  if (!(sde->beta_min > 0.0)) return fail(DMIP_ERR_INVALID, "beta_min must be > 0");
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t B = batch;
+  MlpDims dp, dl;  // prior MLP2 (x, t) and likelihood MLP (x, y, t)
+  dp.L = dl.L = n_hidden;
+  for (int l = 0; l <= n_hidden; ++l) {
+    const int in_w = l == 0 ? 0 : widths[l - 1], out_w = l == n_hidden ? xdim : widths[l];
+    dp.in.push_back(l == 0 ? xdim + 1 : in_w);
+    dl.in.push_back(l == 0 ? xdim + ydim + 1 : in_w);
+    dp.out.push_back(out_w);
+    dl.out.push_back(out_w);
+  }
+  int wmax = xdim + ydim + 2;
+  for (int i = 0; i < n_hidden; ++i) wmax = std::max(wmax, widths[i] + 1);
+  const int splits = (int)std::max<int64_t>(1, std::min<int64_t>(64, B / 2048));
+  // scratch (one allocation, carved in 256-byte aligned pieces)
+  std::vector<std::pair<float**, size_t>> plan;
+  auto need = [&](float** p, size_t n) { plan.emplace_back(p, n); };
+  MlpTape tp, tl;
+  tp.h.assign(n_hidden + 1, nullptr);
+  tl.h.assign(n_hidden + 1, nullptr);
+  tp.d.assign(n_hidden, nullptr);
+  tl.d.assign(n_hidden, nullptr);
+  for (int l = 0; l <= n_hidden; ++l) {
+    need(&tp.h[l], (size_t)B * (dp.in[l] + 1));
+    need(&tl.h[l], (size_t)B * (dl.in[l] + 1));
+  }
+  for (int l = 0; l < n_hidden; ++l) {
+    need(&tp.d[l], (size_t)B * widths[l]);
+    need(&tl.d[l], (size_t)B * widths[l]);
+  }
+  float *sp = nullptr, *sl = nullptr, *alpha = nullptr, *stdv = nullptr, *xt = nullptr, *x0 = nullptr, *u = nullptr,
+        *jtu = nullptr, *tgt = nullptr, *ap = nullptr, *al = nullptr, *rows = nullptr, *da = nullptr, *db = nullptr,
+        *part = nullptr;
+  need(&sp, (size_t)B * xdim);
+  need(&sl, (size_t)B * xdim);
+  need(&alpha, B);
+  need(&stdv, B);
+  need(&xt, (size_t)B * xdim);
+  need(&x0, (size_t)B * xdim);
+  need(&u, (size_t)B * xdim);
+  need(&jtu, (size_t)B * (xdim + 1));
+  need(&tgt, (size_t)B * xdim);
+  need(&ap, (size_t)B * xdim);
+  need(&al, (size_t)B * xdim);
+  need(&rows, (size_t)B * 2);
+  need(&da, (size_t)B * wmax);
+  need(&db, (size_t)B * wmax);
+  need(&part, (size_t)splits * (size_t)wmax * (size_t)wmax);
+  size_t total = 0;
+  for (auto& q : plan) total += (q.second * sizeof(float) + 255) / 256 * 256;
+  char* scratch = nullptr;
+  hipError_t e = hipMallocAsync((void**)&scratch, total, st);
+  if (e != hipSuccess) return fail(DMIP_ERR_ALLOC, std::string("hipMallocAsync: ") + hipGetErrorString(e));
+  {
+    size_t o = 0;
+    for (auto& q : plan) {
+      *q.first = (float*)(scratch + o);
+      o += (q.second * sizeof(float) + 255) / 256 * 256;
+    }
+  }
+  tp.out = sp;
+  tl.out = sl;
+  dmip::PosteriorParams pp{};
+  pp.batch = B;
+  pp.xdim = xdim;
+  pp.ydim = ydim;
+  pp.bmin = (float)sde->beta_min;
+  pp.bdiff = (float)(sde->beta_max - sde->beta_min);
+  pp.lam = lam;
+  pp.x = x_dev;
+  pp.y = y_dev;
+  pp.t = t_dev;
+  pp.eps = eps_dev;
+  pp.alpha = alpha;
+  pp.stdv = stdv;
+  pp.x_t = xt;
+  pp.prior_in = tp.h[0];
+  pp.lik_in = tl.h[0];
+  pp.s_prior = sp;
+  pp.s_lik = sl;
+  pp.x0 = x0;
+  pp.u = u;
+  pp.jtu = jtu;
+  pp.target = target_out_dev ? target_out_dev : tgt;
+  pp.adj_prior = ap;
+  pp.adj_lik = al;
+  pp.rows = rows;
+  pp.loss_out = loss_out_dev;
+  dmip::SurrogateParams sq{};
+  surrogate_params(fwd, sq);
+  sq.a = noise->a;
+  sq.b2 = (float)((double)noise->b * (double)noise->b);
+  sq.x = x0;
+  sq.y = y_dev;
+  sq.y_stride = ydim;
+  sq.n = B;
+  sq.g_out = u;
+  auto run = [&]() -> hipError_t {
+    hipError_t r;
+    for (int l = 1; l <= n_hidden; ++l) {
+      if ((r = dmip::launch_ones_column(tp.h[l], B, dp.in[l] + 1, st)) != hipSuccess) return r;
+      if ((r = dmip::launch_ones_column(tl.h[l], B, dl.in[l] + 1, st)) != hipSuccess) return r;
+    }
+    if ((r = dmip::launch_posterior_stage(pp, 0, st)) != hipSuccess) return r;  // x_t, network inputs
+    if ((r = mlp_forward_f32(dp, prior_w, prior_b, tp, B, st)) != hipSuccess) return r;
+    if ((r = mlp_forward_f32(dl, lik_w, lik_b, tl, B, st)) != hipSuccess) return r;
+    if ((r = dmip::launch_posterior_stage(pp, 1, st)) != hipSuccess) return r;  // Tweedie x0
+    if ((r = dmip::launch_surrogate_eval(sq, 3, surrogate_n_wg(B, st), st)) != hipSuccess) return r;  // u = J_F^T v
+    // J_s^T u: the prior's reverse pass to its input, no parameter gradients
+    if ((r = mlp_backward_f32(dp, prior_w, tp, u, B, da, db, nullptr, jtu, part, splits, st)) != hipSuccess) return r;
+    if ((r = dmip::launch_posterior_stage(pp, 2, st)) != hipSuccess) return r;  // target, adjoints, rows
+    if ((r = mlp_backward_f32(dp, prior_w, tp, ap, B, da, db, grad_prior_dev, nullptr, part, splits, st)) != hipSuccess)
+      return r;
+    if ((r = mlp_backward_f32(dl, lik_w, tl, al, B, da, db, grad_lik_dev, nullptr, part, splits, st)) != hipSuccess)
+      return r;
+    return dmip::launch_posterior_stage(pp, 3, st);  // loss reduction
+  };
+  e = run();
+  (void)hipFreeAsync(scratch, st);
+  if (e != hipSuccess) return hip_fail(e, "posterior_loss_grad launch");
+  return DMIP_OK;
+}
+
+}  // extern "C"
+
+extern "C" {
+
 int dmip_rng_words(uint64_t seed, int64_t chain_offset, uint64_t stream_id, int64_t n_chains, int n_words,
                    uint32_t* out_dev, void* stream) {
   if (!out_dev || n_chains < 0 || n_words < 0) return fail(DMIP_ERR_INVALID, "bad argument");

@@ -1,0 +1,296 @@
+// Exact-f32 training engine on gfx950: one tiled MFMA GEMM (v_mfma_f32_16x16x4_f32, an fmaf chain)
+// with fused epilogues, plus the elementwise stages of the PosteriorLoss step (A18). A network's
+// training step over a batch is GEMM-shaped work and runs as GEMMs:
+//   forward   Z_l = H_{l-1} W_l^T + b_l, H_l = act(Z_l), act'(Z_l) kept      (epilogue BIAS_TANH[2])
+//   backward  D_{l-1} = (D_l W_l) * act'(Z_{l-1})                            (epilogue MUL_AUX)
+//   gradients [dW_l | db_l] = D_l^T [H_{l-1} | 1]                              (split-K over the batch,
+//             fixed-order reduction: deterministic)
+// Activations are stored row-major [B][ld] with ld = width + 1 and the last column set to 1, so one
+// GEMM yields a layer's weight AND bias gradient.
+// Reference: nets.py:17-57 (the MLP chain, double tanh on layer 1), losses.py:293-386 (PosteriorLoss),
+// models/diffusion.py:204-229 (its training loop).
+#include "dmip_device.h"
+#include "dmip_internal.h"
+
+namespace dmip {
+namespace gemm {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int BM = 64, BN = 64, KB = 16, PAD = 4;
+constexpr int NT = 256;  // 4 waves: 2 x 2 wave tiles of 32 x 32 (2 x 2 MFMA tiles of 16 x 16 each)
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// epilogue of one output element (m, n) from the accumulated value v
+__device__ __forceinline__ void epilogue(const GemmParams& p, long long m, int n, float v) {
+  switch (p.epi) {
+    case GEMM_EPI_NONE:
+      p.c[m * p.ldc + n] = v;
+      break;
+    case GEMM_EPI_BIAS:
+      p.c[m * p.ldc + n] = v + p.bias[n];
+      break;
+    case GEMM_EPI_BIAS_TANH: {
+      const float h = tanhf(v + p.bias[n]);
+      p.c[m * p.ldc + n] = h;
+      p.aux_out[m * p.ldaux + n] = 1.0f - h * h;
+      break;
+    }
+    case GEMM_EPI_BIAS_TANH2: {  // the reference's first layer applies tanh twice (nets.py:21-26)
+      const float t1 = tanhf(v + p.bias[n]);
+      const float t2 = tanhf(t1);
+      p.c[m * p.ldc + n] = t2;
+      p.aux_out[m * p.ldaux + n] = (1.0f - t2 * t2) * (1.0f - t1 * t1);
+      break;
+    }
+    case GEMM_EPI_MUL_AUX:
+      p.c[m * p.ldc + n] = v * p.aux_in[m * p.ldaux + n];
+      break;
+    case GEMM_EPI_WGRAD:  // [dW | db]: column N-1 is the bias gradient
+      if (n < p.n - 1) p.c[m * p.ldc + n] = v;
+      else p.bias_out[m] = v;
+      break;
+    default:
+      break;
+  }
+}
+
+// C (M x N) = A (M x K) B (K x N) with A(m, k) = TA ? A[k lda + m] : A[m lda + k] and
+// B(k, n) = TB ? B[n ldb + k] : B[k ldb + n]. grid.z > 1: split-K partials (raw sums) into p.part.
+template <bool TA, bool TB>
+__global__ void __launch_bounds__(NT) gemm_f32_kernel(GemmParams p) {
+  __shared__ float As[2][KB][BM + PAD];
+  __shared__ float Bs[2][KB][BN + PAD];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int i = lane & 15, g = lane >> 4;
+  const long long m0 = (long long)blockIdx.y * BM;
+  const int n0 = blockIdx.x * BN;
+  const int wm = (w >> 1) * 32, wn = (w & 1) * 32;
+  // this split's k range
+  const long long kchunk = ((p.k + gridDim.z - 1) / gridDim.z + KB - 1) / KB * KB;
+  const long long k_lo = (long long)blockIdx.z * kchunk;
+  const long long k_hi = k_lo + kchunk < p.k ? k_lo + kchunk : p.k;
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+
+  // global -> registers for one KB slice (4 elements of A and of B per thread)
+  float ra[4], rb[4];
+  auto load = [&](long long k0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = tid * 4 + q;  // element of the 64 x 16 slice
+      int mm, kk;
+      if (TA) { kk = e / BM; mm = e % BM; } else { mm = e / KB; kk = e % KB; }
+      const long long m = m0 + mm, k = k0 + kk;
+      ra[q] = (m < p.m && k < k_hi) ? (TA ? p.a[k * p.lda + m] : p.a[m * p.lda + k]) : 0.0f;
+      int nn, kb;
+      if (TB) { nn = e / KB; kb = e % KB; } else { kb = e / BN; nn = e % BN; }
+      const long long n = n0 + nn, kq = k0 + kb;
+      rb[q] = (n < p.n && kq < k_hi) ? (TB ? p.b[n * p.ldb + kq] : p.b[kq * p.ldb + n]) : 0.0f;
+    }
+  };
+  auto store = [&](int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = tid * 4 + q;
+      int mm, kk;
+      if (TA) { kk = e / BM; mm = e % BM; } else { mm = e / KB; kk = e % KB; }
+      As[buf][kk][mm] = ra[q];
+      int nn, kb;
+      if (TB) { nn = e / KB; kb = e % KB; } else { kb = e / BN; nn = e % BN; }
+      Bs[buf][kb][nn] = rb[q];
+    }
+  };
+
+  int buf = 0;
+  if (k_lo < k_hi) {
+    load(k_lo);
+    store(0);
+  }
+  __syncthreads();
+  for (long long k0 = k_lo; k0 < k_hi; k0 += KB) {
+    const bool more = k0 + KB < k_hi;
+    if (more) load(k0 + KB);  // global loads of the next slice in flight during the MFMAs
+#pragma unroll
+    for (int ks = 0; ks < KB / 4; ++ks) {
+      float av[2], bv[2];
+#pragma unroll
+      for (int a = 0; a < 2; ++a) av[a] = As[buf][ks * 4 + g][wm + a * 16 + i];
+#pragma unroll
+      for (int b = 0; b < 2; ++b) bv[b] = Bs[buf][ks * 4 + g][wn + b * 16 + i];
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] = mfma4(av[a], bv[b], acc[a][b]);
+    }
+    if (more) store(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+
+  // lane (g, j = i) of MFMA tile (a, b) holds rows 4g + r of column j
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const long long m = m0 + wm + a * 16 + 4 * g + r;
+        const int n = n0 + wn + b * 16 + i;
+        if (m < p.m && n < p.n) {
+          if (gridDim.z > 1) p.part[((long long)blockIdx.z * p.m + m) * p.n + n] = acc[a][b][r];
+          else epilogue(p, m, n, acc[a][b][r]);
+        }
+      }
+}
+
+// split-K: sum the partials in split order (deterministic), then the epilogue
+__global__ void gemm_reduce_kernel(GemmParams p, int splits) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= p.m * p.n) return;
+  float s = 0.0f;
+  for (int z = 0; z < splits; ++z) s += p.part[(long long)z * p.m * p.n + e];
+  epilogue(p, e / p.n, (int)(e % p.n), s);
+}
+
+// ---------------------------------------------------------------- PosteriorLoss elementwise stages
+// prep: alpha, std at t (sdes.py:24-28 order), x_t = eps std + alpha x (sdes.py:37-49), the two
+// network input matrices [x_t, t, 1] and [x_t, y, t, 1] (nets.py:33,54 plus the ones column)
+__global__ void posterior_prep_kernel(PosteriorParams p) {
+  const long long b = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= p.batch) return;
+  const float t = p.t[b];
+  const float al = vp_mean_weight(t, p.bmin, p.bdiff);
+  const float sd = vp_std(t, p.bmin, p.bdiff);
+  p.alpha[b] = al;
+  p.stdv[b] = sd;
+  const int D = p.xdim, M = p.ydim;
+  float* pin = p.prior_in + b * (D + 2);
+  float* lin = p.lik_in + b * (D + M + 2);
+  for (int k = 0; k < D; ++k) {
+    const float xt = __fadd_rn(__fmul_rn(p.eps[b * D + k], sd), __fmul_rn(al, p.x[b * D + k]));
+    p.x_t[b * D + k] = xt;
+    pin[k] = xt;
+    lin[k] = xt;
+  }
+  for (int k = 0; k < M; ++k) lin[D + k] = p.y[b * M + k];
+  pin[D] = t;
+  pin[D + 1] = 1.0f;
+  lin[D + M] = t;
+  lin[D + M + 1] = 1.0f;
+}
+
+// x_0 = 1 / alpha * (x_t + std^2 s_prior)   (losses.py:379, the reference's operation order)
+__global__ void posterior_x0_kernel(PosteriorParams p) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= p.batch * p.xdim) return;
+  const long long b = e / p.xdim;
+  const float sd = p.stdv[b];
+  const float inv = __fdiv_rn(1.0f, p.alpha[b]);
+  p.x0[e] = __fmul_rn(inv, __fadd_rn(p.x_t[e], __fmul_rn(__fmul_rn(sd, sd), p.s_prior[e])));
+}
+
+// target = u + std^2 J_s^T u (losses.py:366 with the three VJPs / VHPs combined by linearity),
+// the per-row losses (losses.py:376,381) and the output adjoints of both networks
+__global__ void posterior_target_kernel(PosteriorParams p) {
+  const long long b = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= p.batch) return;
+  const int D = p.xdim;
+  const float sd = p.stdv[b], al = p.alpha[b];
+  const float inv_b = 1.0f / (float)p.batch;
+  float prior = 0.0f, lik = 0.0f;
+  for (int k = 0; k < D; ++k) {
+    const long long e = b * D + k;
+    const float tgt = p.u[e] + sd * sd * p.jtu[b * (D + 1) + k];  // jtu: input gradient over [x_t, t]
+    p.target[e] = tgt;
+    const float rp = p.s_prior[e] * sd + p.eps[e];  // DSMLoss residual s std + eps (losses.py:42-52)
+    const float rl = al * p.s_lik[e] - tgt;
+    prior += rp * rp;
+    lik += rl * rl;
+    p.adj_prior[e] = rp * sd * inv_b;                 // d mean(0.5 |rp|^2) / d s_prior
+    p.adj_lik[e] = 2.0f * p.lam * al * rl * inv_b;    // d mean(lam |rl|^2) / d s_lik
+  }
+  p.rows[b * 2 + 0] = 0.5f * prior;
+  p.rows[b * 2 + 1] = lik;
+}
+
+// loss, PriorLoss, LikelihoodLoss: one workgroup, fixed-order tree (deterministic), f64 sums
+__global__ void posterior_loss_reduce_kernel(PosteriorParams p) {
+  __shared__ double sp[256], sl[256];
+  double a = 0.0, c = 0.0;
+  for (long long b = threadIdx.x; b < p.batch; b += 256) {
+    a += p.rows[b * 2 + 0];
+    c += p.rows[b * 2 + 1];
+  }
+  sp[threadIdx.x] = a;
+  sl[threadIdx.x] = c;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) {
+      sp[threadIdx.x] += sp[threadIdx.x + s];
+      sl[threadIdx.x] += sl[threadIdx.x + s];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const double n = (double)p.batch;
+    p.loss_out[1] = (float)(sp[0] / n);
+    p.loss_out[2] = (float)((double)p.lam * sl[0] / n);
+    p.loss_out[0] = (float)(sp[0] / n + (double)p.lam * sl[0] / n);
+  }
+}
+
+// the ones column of an activation matrix [B][ld] (column ld - 1)
+__global__ void ones_column_kernel(float* h, long long rows, int ld) {
+  const long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < rows) h[r * ld + ld - 1] = 1.0f;
+}
+
+}  // namespace gemm
+
+// ----------------------------------------------------------------------------------- launches
+hipError_t launch_gemm_f32(const GemmParams& p_in, bool ta, bool tb, int splits, hipStream_t st) {
+  GemmParams p = p_in;
+  if (p.m <= 0 || p.n <= 0) return hipSuccess;
+  if (splits < 1) splits = 1;
+  const dim3 grid((unsigned)((p.n + gemm::BN - 1) / gemm::BN), (unsigned)((p.m + gemm::BM - 1) / gemm::BM),
+                  (unsigned)splits);
+  if (splits > 1 && !p.part) return hipErrorInvalidValue;
+#define G(TA_, TB_) \
+  if (ta == TA_ && tb == TB_) hipLaunchKernelGGL((gemm::gemm_f32_kernel<TA_, TB_>), grid, dim3(gemm::NT), 0, st, p);
+  G(false, false) G(false, true) G(true, false) G(true, true)
+#undef G
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || splits == 1) return e;
+  const long long n = p.m * p.n;
+  hipLaunchKernelGGL(gemm::gemm_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, p, splits);
+  return hipGetLastError();
+}
+
+hipError_t launch_ones_column(float* h, long long rows, int ld, hipStream_t st) {
+  hipLaunchKernelGGL(gemm::ones_column_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, st, h, rows, ld);
+  return hipGetLastError();
+}
+
+hipError_t launch_posterior_stage(const PosteriorParams& p, int stage, hipStream_t st) {
+  const unsigned rows = (unsigned)((p.batch + 255) / 256);
+  switch (stage) {
+    case 0: hipLaunchKernelGGL(gemm::posterior_prep_kernel, dim3(rows), dim3(256), 0, st, p); break;
+    case 1:
+      hipLaunchKernelGGL(gemm::posterior_x0_kernel, dim3((unsigned)((p.batch * p.xdim + 255) / 256)), dim3(256), 0,
+                         st, p);
+      break;
+    case 2: hipLaunchKernelGGL(gemm::posterior_target_kernel, dim3(rows), dim3(256), 0, st, p); break;
+    default: hipLaunchKernelGGL(gemm::posterior_loss_reduce_kernel, dim3(1), dim3(256), 0, st, p); break;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace dmip

@@ -224,6 +224,60 @@ bool f32_sampler_supported(int mode, int width, int n_hidden, int xdim, int ydim
 hipError_t launch_f32_forward(const F32ForwardParams& p, int width, int ot, hipStream_t st, bool* supported);
 hipError_t launch_f32_l1_prep(const F32L1PrepParams& p, int n_y, hipStream_t st);
 
+// ---- exact-f32 training engine (dmip_gemm.hip): MFMA GEMM with fused epilogues
+enum {
+  GEMM_EPI_NONE = 0,      // C = acc
+  GEMM_EPI_BIAS = 1,      // C = acc + bias[n]
+  GEMM_EPI_BIAS_TANH = 2, // C = tanh(acc + bias[n]), aux_out = 1 - C^2
+  GEMM_EPI_BIAS_TANH2 = 3,// C = tanh(tanh(acc + bias[n])), aux_out = its derivative
+  GEMM_EPI_MUL_AUX = 4,   // C = acc * aux_in
+  GEMM_EPI_WGRAD = 5      // columns < n-1 -> C ([dW]), column n-1 -> bias_out[m] ([db])
+};
+
+struct GemmParams {
+  const float* a;
+  const float* b;
+  float* c;
+  long long m, n, k;
+  long long lda, ldb, ldc;
+  int epi;
+  const float* bias;
+  const float* aux_in;    // MUL_AUX: [m][ldaux]
+  float* aux_out;         // TANH epilogues: [m][ldaux]
+  long long ldaux;
+  float* bias_out;        // WGRAD: [m]
+  float* part;            // split-K partials [splits][m][n]
+};
+
+struct PosteriorParams {
+  long long batch;
+  int xdim, ydim;
+  float bmin, bdiff, lam;
+  const float* x;         // [B][xdim]
+  const float* y;         // [B][ydim]
+  const float* t;         // [B]
+  const float* eps;       // [B][xdim]
+  float* alpha;           // [B]
+  float* stdv;            // [B]
+  float* x_t;             // [B][xdim]
+  float* prior_in;        // [B][xdim + 2]: x_t, t, 1
+  float* lik_in;          // [B][xdim + ydim + 2]: x_t, y, t, 1
+  const float* s_prior;   // [B][xdim]
+  const float* s_lik;     // [B][xdim]
+  float* x0;              // [B][xdim]
+  const float* u;         // [B][xdim]: J_F^T v (surrogate reverse pass)
+  const float* jtu;       // [B][xdim + 1]: the prior's input gradient for the adjoint u
+  float* target;          // [B][xdim]
+  float* adj_prior;       // [B][xdim]
+  float* adj_lik;         // [B][xdim]
+  float* rows;            // [B][2]: per-row prior DSM and likelihood terms
+  float* loss_out;        // [3]: loss, PriorLoss, LikelihoodLoss
+};
+
+hipError_t launch_gemm_f32(const GemmParams& p, bool ta, bool tb, int splits, hipStream_t st);
+hipError_t launch_ones_column(float* h, long long rows, int ld, hipStream_t st);
+hipError_t launch_posterior_stage(const PosteriorParams& p, int stage, hipStream_t st);
+
 hipError_t launch_histogram(const float* x, long long n, int d, int nbins, double lo, double hi, int n_hist,
                             unsigned int* counts, hipStream_t st);
 

@@ -285,6 +285,31 @@ __device__ __forceinline__ float energy(const f32x4 (&f)[2], const float* y, con
   return 0.5f * slog + 0.5f * ssq + lam * bd;
 }
 
+// v = v2 + a^2 (v3 - v1) with v1 = f / pref, v2 = (y - f) / pref, v3 = (y - f)^2 f / pref: the
+// combination of PosteriorLoss.likelihood_target's three VJP vectors (losses.py:353-356,366) -- the
+// target is linear in them, so one reverse pass through the surrogate gives their weighted sum.
+__device__ __forceinline__ void posterior_target_v(const f32x4 (&f)[2], const float* y, float a, float b2, int g,
+                                                   f32x4 (&v)[2]) {
+  const float a2 = a * a;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 16 * t + 4 * g + r;
+      float vk = 0.0f;
+      if (row < YD) {
+        const float fk = f[t][r];
+        const float af = a * fk;
+        const float pref = af * af + b2;
+        const float res = y[row] - fk;
+        const float v1 = fk / pref, v2 = res / pref, v3 = res * res * fk / pref;
+        vk = v2 + a2 * (v3 - v1);
+      }
+      v[t][r] = vk;
+    }
+  }
+}
+
 __device__ __forceinline__ float boundary_grad(float xd, float lam) {
   return (xd > 1.0f ? lam : 0.0f) - (xd < -1.0f ? lam : 0.0f);
 }
@@ -296,10 +321,11 @@ __device__ __forceinline__ Plan make_plan(const SurrogateParams& p) {
 }
 
 // ------------------------------------------------------------------------- evaluation kernel
-// MODE 0: f = F(x); 1: E(x, y); 2: E and dE/dx. Rows strided over the grid, 16 per wave.
+// MODE 0: f = F(x); 1: E(x, y); 2: E and dE/dx; 3: J_F^T v with PosteriorLoss's target vector v
+// (posterior_target_v, into g_out). Rows strided over the grid, 16 per wave.
 template <int MODE>
 __global__ void __launch_bounds__(NW * 64, 1) surrogate_eval_kernel(SurrogateParams p) {
-  constexpr bool GRAD = MODE == 2;
+  constexpr bool GRAD = MODE >= 2;
   constexpr int RING_OFF = GRAD ? RING_OFF_GRAD : RING_OFF_FWD;
   __shared__ __attribute__((aligned(16))) char lds[RING_OFF + R * CHUNK];
   const int lane = threadIdx.x & 63;
@@ -330,6 +356,16 @@ __global__ void __launch_bounds__(NW * 64, 1) surrogate_eval_kernel(SurrogatePar
             const int k = 16 * t + 4 * g + r;
             if (k < YD) p.f_out[row * YD + k] = f[t][r];
           }
+      }
+    } else if constexpr (MODE == 3) {
+      const float* y = p.y + (p.y_stride ? rr * p.y_stride : 0);
+      f32x4 v[2];
+      posterior_target_v(f, y, p.a, p.b2, g, v);
+      float gx[XD];
+      eng.backward(v, m, gx);
+      if (valid && g == 0) {
+#pragma unroll
+        for (int d = 0; d < XD; ++d) p.g_out[row * XD + d] = gx[d];
       }
     } else {
       const float* y = p.y + (p.y_stride ? rr * p.y_stride : 0);
@@ -640,6 +676,7 @@ hipError_t launch_surrogate_eval(const SurrogateParams& p, int mode, int n_wg, h
   switch (mode) {
     case 0: hipLaunchKernelGGL(sg::surrogate_eval_kernel<0>, grid, block, 0, st, p); break;
     case 1: hipLaunchKernelGGL(sg::surrogate_eval_kernel<1>, grid, block, 0, st, p); break;
+    case 3: hipLaunchKernelGGL(sg::surrogate_eval_kernel<3>, grid, block, 0, st, p); break;
     default: hipLaunchKernelGGL(sg::surrogate_eval_kernel<2>, grid, block, 0, st, p); break;
   }
   return hipGetLastError();

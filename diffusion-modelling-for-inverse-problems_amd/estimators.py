@@ -361,8 +361,19 @@ class PosteriorDiffusionEstimator(BaseClassDiffusionModel):
                                drift, self.xdim, self.xdim)
 
     def train_epoch(self, optimizer, loss_fn, epoch_data_loader):
+        """models/diffusion.py:204-229. On a HIP device with PosteriorLoss on the scatterometry surrogate,
+        each batch's loss and both networks' gradients come from dmip_posterior_loss_grad (exact f32,
+        training.posterior_loss_grad); otherwise the autograd graph of losses.PosteriorLoss."""
+        from .training import posterior_fused_ok, posterior_loss_grad
+        fused = posterior_fused_ok(self, loss_fn)
+
         def batch_loss(x, y):
-            return loss_fn(self.sde, x, y, self.sample_t(x))
+            t = self.sample_t(x)
+            if fused:
+                eps = torch.randn_like(x)  # base_sde.sample's draw (sdes.py:37-49)
+                optimizer.zero_grad()
+                return _FusedStep(*posterior_loss_grad(self, loss_fn, x, y, t, eps))
+            return loss_fn(self.sde, x, y, t)
         return self._train_loop(optimizer, epoch_data_loader, batch_loss)
 
 

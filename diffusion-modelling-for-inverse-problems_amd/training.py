@@ -159,3 +159,52 @@ def train_scatterometry(model, optimizer, loss_fn, forward_model_params, save_di
     os.makedirs(save_dir, exist_ok=True)
     torch.save(model.sde.a.state_dict(), os.path.join(save_dir, 'diffusion.pt'))
     return model
+
+
+# ------------------------------------------------------------------ A18: PosteriorLoss on the device
+def posterior_fused_ok(model, loss_fn):
+    """True when PosteriorDiffusionEstimator.train_epoch can take dmip_posterior_loss_grad: a PosteriorLoss on
+    the scatterometry surrogate, both networks fp32 on a HIP device with equal hidden layers."""
+    from .losses import PosteriorLoss
+    from .problems import surrogate_handle
+    if os.environ.get("DMIP_TRAIN_FUSED", "1") == "0" or not isinstance(loss_fn, PosteriorLoss):
+        return False
+    prior, lik = model.sde.a.prior_net, model.sde.a.likelihood_net
+    p0 = prior.linear_layers()[0][0]
+    if not p0.is_cuda or p0.dtype != torch.float32 or (model.xdim, model.ydim) != (3, 23):
+        return False
+    if [int(w.shape[0]) for w, _ in prior.linear_layers()] != [int(w.shape[0]) for w, _ in lik.linear_layers()]:
+        return False
+    return loss_fn.forward_model is not None and surrogate_handle(loss_fn.forward_model, p0.device) is not None
+
+
+def posterior_loss_grad(model, loss_fn, x, y, t, eps, want_target=False):
+    """One fused PosteriorLoss evaluation (dmip_posterior_loss_grad): gradients written into both networks'
+    .grad (set, not accumulated); returns (loss, info[, target]) like the reference loss object."""
+    from .problems import surrogate_handle
+    prior, lik = model.sde.a.prior_net, model.sde.a.likelihood_net
+    pl = [(w.detach(), b.detach()) for w, b in prior.linear_layers()]
+    ll = [(w.detach(), b.detach()) for w, b in lik.linear_layers()]
+    dev = pl[0][0].device
+    f32 = dict(device=dev, dtype=torch.float32)
+    x = x.detach().to(**f32).contiguous()
+    y = y.detach().to(**f32).contiguous()
+    t = t.detach().to(**f32).reshape(-1).contiguous()
+    eps = eps.detach().to(**f32).contiguous()
+    pp, lp = list(prior.parameters()), list(lik.parameters())
+    gp = torch.empty(sum(p.numel() for p in pp), **f32)
+    gl = torch.empty(sum(p.numel() for p in lp), **f32)
+    out = torch.empty(3, **f32)
+    tgt = torch.empty_like(x) if want_target else None
+    base = model.sde.base_sde
+    sur = surrogate_handle(loss_fn.forward_model, dev)
+    _lib.posterior_loss_grad(pl, ll, sur, _lib.scat_noise(loss_fn.a, loss_fn.b, 0.0), loss_fn.lam,
+                             _lib.vpsde(base.beta_min, base.beta_max, 1.0), x, y, t, eps, gp, gl, out, tgt)
+    for params, flat in ((pp, gp), (lp, gl)):
+        off = 0
+        for p in params:
+            n = p.numel()
+            p.grad = flat[off:off + n].view_as(p).clone()
+            off += n
+    info = {'PriorLoss': out[1], 'LikelihoodLoss': out[2]}
+    return (out[0], info, tgt) if want_target else (out[0], info)

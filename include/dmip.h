@@ -237,6 +237,31 @@ int dmip_dps_sample(const dmip_mlp* prior, const dmip_surrogate* fwd, const dmip
                     int num_steps, float mean, float stdv, uint64_t seed, int mode, float zeta, float* x_out_dev,
                     void* stream);
 
+/* ---- PosteriorLoss training step ------------------------------------------ */
+/* Loss value, components and the parameter gradients of PosteriorLoss(forward_model, a, b, lam)(sde, x,
+ * y, t) + loss.backward() (losses.py:293-386) as PosteriorDiffusionEstimator.train_epoch drives it
+ * (models/diffusion.py:204-229), with the forward diffusion x_t = eps std(t) + mean_weight(t) x in the
+ * step (sdes.py:37-49; eps caller-drawn, the reference's randn_like). Exact f32 throughout: the two
+ * networks' forward and reverse passes as MFMA GEMMs with fused tanh / derivative epilogues, the
+ * likelihood target (I + std^2 J_s^T) J_F^T (v2 + a^2 (v3 - v1)) -- the reference's three VJPs and three
+ * vector-Hessian products, which it takes without create_graph (constants for the gradients), combined
+ * by linearity -- through the fused surrogate reverse pass, deterministic split-K reductions.
+ *   xdim, ydim          3, 23 (the scatterometry surrogate)
+ *   n_hidden, widths    hidden layers of both networks (any widths, equal for the two networks)
+ *   prior_w/b, lik_w/b  device fp32 parameters (nn.Linear layout, n_hidden + 1 layers) of the
+ *                       MLP2 prior (x, t) and the MLP likelihood (x, y, t) networks
+ *   fwd, noise, lam     the surrogate handle, its noise model (a, b), the likelihood-loss weight
+ *   x, y, t, eps        [batch][3], [batch][23], [batch], [batch][3]
+ *   grad_prior / grad_lik   [n_params] each, written in the reference parameter order
+ *   loss_out            [3]: loss, PriorLoss, LikelihoodLoss (the reference's returned dict)
+ *   target_out          optional [batch][3]: the likelihood target (NULL: not returned) */
+int dmip_posterior_loss_grad(int xdim, int ydim, int n_hidden, const int* widths, const float* const* prior_w,
+                             const float* const* prior_b, const float* const* lik_w, const float* const* lik_b,
+                             const dmip_surrogate* fwd, const dmip_scat_noise* noise, float lam, const dmip_vpsde* sde,
+                             const float* x_dev, const float* y_dev, const float* t_dev, const float* eps_dev,
+                             int64_t batch, float* grad_prior_dev, float* grad_lik_dev, float* loss_out_dev,
+                             float* target_out_dev, void* stream);
+
 /* Test hooks for the parity suite (integer RNG stream, normals, schedule). */
 int dmip_rng_words(uint64_t seed, int64_t chain_offset, uint64_t stream_id, int64_t n_chains, int n_words,
                    uint32_t* out_dev, void* stream);

@@ -707,3 +707,87 @@ def dps_sample(prior_params, sur_params, y, num_samples, num_steps, seed, zeta=1
         xe = em_step(x, (g * s.astype(F32)).astype(F32), tau[i], delta, beta_min, beta_max, xi)
         x = (xe - (lam[:, None] * gt).astype(F32)).astype(F32)
     return x
+
+
+# ------------------------------------------------------------------------------------------
+# A18  PosteriorLoss -- losses.py:293-386, driven by PosteriorDiffusionEstimator.train_epoch
+#      (models/diffusion.py:204-229). Test infrastructure (the checker of the fused HIP path).
+# ------------------------------------------------------------------------------------------
+
+def _mlp_tape(params, inp):
+    """Forward of the reference MLP chain (double tanh on layer 1) in float64, keeping what the
+    reverse pass needs: per layer its input and the activation derivative."""
+    W = [np.asarray(p[0], np.float64) for p in params]
+    b = [np.asarray(p[1], np.float64) for p in params]
+    h = np.asarray(inp, np.float64)
+    tape = []
+    for li in range(len(W)):
+        z = h @ W[li].T + b[li]
+        if li == len(W) - 1:
+            tape.append((h, None))
+            h = z
+        elif li == 0:
+            t1 = np.tanh(z)
+            t2 = np.tanh(t1)
+            tape.append((h, (1 - t2 * t2) * (1 - t1 * t1)))
+            h = t2
+        else:
+            t = np.tanh(z)
+            tape.append((h, 1 - t * t))
+            h = t
+    return h, tape, W
+
+
+def _mlp_backprop(tape, W, adj):
+    """Reverse pass from the output adjoint adj (n, out): per-layer (dW, db) and d/d(input)."""
+    grads = [None] * len(W)
+    d = np.asarray(adj, np.float64)
+    for li in range(len(W) - 1, -1, -1):
+        h_in, dact = tape[li]
+        grads[li] = (d.T @ h_in, d.sum(0))
+        d = d @ W[li]
+        if li > 0:
+            d = d * tape[li - 1][1]
+    return grads, d
+
+
+def posterior_loss_grad(prior_params, lik_params, sur_params, x, y, t, eps, a=0.2, b=0.01, lam=0.01,
+                        beta_min=BETA_MIN, beta_max=BETA_MAX):
+    """PosteriorLoss(forward_model, a, b, lam)(sde, x, y, t) and loss.backward(), float64.
+
+    The reference's likelihood target takes every autograd.grad without create_graph (losses.py:
+    358-365): it is a constant for the parameter gradients, which therefore come from the prior's DSM
+    term (losses.py:376) and the likelihood net's regression term (losses.py:381) only. By linearity
+    the three VJPs and three vector-Hessian (input-Jacobian) products collapse to
+        target = (I + std^2 J_s^T) J_F^T (v2 + a^2 (v3 - v1)),
+    J_s = d s_prior / d x_t, J_F = dF/dx0 at x0 = (x_t + std^2 s_prior) / alpha (losses.py:379-380).
+    Returns (loss, {'PriorLoss', 'LikelihoodLoss'}, grads_prior [(dW, db)], grads_lik, target)."""
+    x = np.asarray(x, np.float64)
+    n, d = x.shape
+    t = np.asarray(t, np.float64).reshape(-1, 1)
+    eps = np.asarray(eps, np.float64)
+    y = np.asarray(y, np.float64)
+    bmin, bdiff = np.float64(beta_min), np.float64(beta_max - beta_min)
+    alpha = np.exp(-0.25 * t * t * bdiff - 0.5 * t * bmin)
+    std = np.sqrt(1.0 - np.exp(-0.5 * t * t * bdiff - t * bmin))
+    x_t = eps * std + alpha * x
+    s_p, tape_p, Wp = _mlp_tape(prior_params, np.concatenate([x_t, t], 1))
+    s_l, tape_l, Wl = _mlp_tape(lik_params, np.concatenate([x_t, y, t], 1))
+    x0 = (x_t + std ** 2 * s_p) / alpha
+    f, pre = surrogate_forward(sur_params, x0, keep=True)
+    pref = (a * f) ** 2 + b ** 2
+    v1, v2, v3 = f / pref, (y - f) / pref, (y - f) ** 2 * f / pref
+    u = v2 + a * a * (v3 - v1)
+    for i in range(len(sur_params) - 1, -1, -1):
+        u = u @ np.asarray(sur_params[i][0], np.float64)
+        if i > 0:
+            u = u * (pre[i - 1] > 0)
+    _, jtu = _mlp_backprop(tape_p, Wp, u)  # J_s^T u: the input gradient of the prior at x_t
+    target = u + std ** 2 * jtu[:, :d]
+    prior_rows = 0.5 * ((s_p * std + eps) ** 2).sum(1)
+    lik_rows = ((alpha * s_l - target) ** 2).sum(1)
+    loss = float(np.mean(prior_rows + lam * lik_rows))
+    gp, _ = _mlp_backprop(tape_p, Wp, (s_p * std + eps) * std / n)
+    gl, _ = _mlp_backprop(tape_l, Wl, 2.0 * lam * alpha * (alpha * s_l - target) / n)
+    info = {"PriorLoss": float(prior_rows.mean()), "LikelihoodLoss": float(lam * lik_rows.mean())}
+    return loss, info, gp, gl, target

@@ -21,11 +21,14 @@ Fixtures (SURVEY.md §8c "Golden fixtures"):
   G9 ckpt_prior_scat.npz   a scatterometry prior score network MLP2 [256]*3 (the PosteriorDiffusionEstimator's
                            prior) trained with the reference's DSMLoss on inverse_cdf_prior samples (the
                            prior half of PosteriorLoss, losses.py:373-377; uniform t) -- for the DPS sampler
+  G10 posterior_loss.npz   PosteriorLoss (losses.py:293-386) value, components, likelihood target and every
+                           parameter gradient of both networks (prior = G9 checkpoint, likelihood seeded,
+                           surrogate = G7) on 256 rows with captured eps and t
   G8 surrogate_io.npz      surrogate forward, get_log_posterior and its autograd input gradient
                            (energy_grad) on 256 seeded rows; anneal_to_energy (random-walk MH) with
                            its captured draws (64 chains x 50 steps) and a 4000-chain x 1000-step run
 
-Usage:  python tests/golden/make_golden.py [--what all|schedule|mlp|data|train|traj|samples|pinn]
+Usage:  python tests/golden/make_golden.py [--what all|schedule|mlp|data|train|traj|samples|pinn|posterior_loss]
 """
 import argparse
 import os
@@ -402,6 +405,55 @@ def train_prior(R, minutes):
              train_log=np.array(log, dtype=np.float64))
 
 
+# ---------------------------------------------------------------------------------------- G10
+def gen_posterior_loss(R):
+    """PosteriorLoss.forward + backward (losses.py:348-386) exactly as PosteriorDiffusionEstimator.train_epoch
+    drives it (models/diffusion.py:204-229): loss_fn(model.sde, x, y, t) with t requiring grad."""
+    import torch
+    from torch import nn
+    torch.set_num_threads(os.cpu_count())
+    torch.manual_seed(41)
+    post = R.diffusion.PosteriorDiffusionEstimator(3, 23, [256] * 3)
+    load_state(post.sde.a.prior_net, os.path.join(OUT, "ckpt_prior_scat.npz"))
+    zs = np.load(os.path.join(OUT, "surrogate.npz"))
+    fm = nn.Sequential(nn.Linear(3, 256), nn.ReLU(), nn.Linear(256, 256), nn.ReLU(), nn.Linear(256, 256), nn.ReLU(),
+                       nn.Linear(256, 23))
+    fm.load_state_dict({k: torch.from_numpy(zs[k.replace(".", "_")]) for k in fm.state_dict().keys()})
+    for prm in fm.parameters():
+        prm.requires_grad = False
+    a, b, lam = 0.2, 0.01, 0.01  # load_forward_model params; config_scatterometry.yml lam
+    lf = R.losses.PosteriorLoss(fm, a, b, lam=lam)
+    B = 256
+    g = torch.Generator().manual_seed(10)
+    x = torch.rand(B, 3, generator=g) * 2 - 1
+    ys = torch.from_numpy(np.load(os.path.join(OUT, "data_scat.npz"))["y_test"])
+    y = ys[torch.arange(B) % ys.shape[0]]
+    t = (1e-4 + torch.rand(B, 1, generator=g) * (1 - 1e-4)).requires_grad_(True)
+    torch.manual_seed(77)
+    eps = torch.randn(B, 3)
+    torch.manual_seed(77)  # base_sde.sample's randn_like(x) is the first draw in forward
+    loss, info = lf(post.sde, x, y, t)
+    loss.backward()
+    out = {"x": x.numpy(), "y": y.numpy(), "t": t.detach().numpy(), "eps": eps.numpy(), "a": a, "b": b, "lam": lam,
+           "loss": float(loss), "PriorLoss": float(info["PriorLoss"]), "LikelihoodLoss": float(info["LikelihoodLoss"])}
+    for tag, net in (("prior", post.sde.a.prior_net), ("lik", post.sde.a.likelihood_net)):
+        out.update(state_to_npz_dict(net.state_dict(), f"{tag}_"))
+        for k, prm in net.named_parameters():
+            out[f"{tag}_grad_{k.replace('.', '_')}"] = prm.grad.numpy().copy()
+    # intermediates on the same inputs (a fresh graph): x_t, both scores, x0 and the likelihood target
+    sde = post.sde.base_sde
+    x_t = eps * sde.var(t) ** 0.5 + sde.mean_weight(t) * x
+    std = sde.var(t) ** 0.5
+    s_p = post.sde.a.prior_net(x_t, t)
+    s_l = post.sde.a.likelihood_net(x_t, y, t)
+    x_0 = 1 / sde.mean_weight(t) * (x_t + std ** 2 * s_p)
+    T = lf.likelihood_target(x_0, y, x_t, s_p, std)
+    out.update({"x_t": x_t.detach().numpy(), "s_prior": s_p.detach().numpy(), "s_lik": s_l.detach().numpy(),
+                "x_0": x_0.detach().numpy(), "target": T.detach().numpy()})
+    np.savez(os.path.join(OUT, "posterior_loss.npz"), **out)
+    print("G10 loss", float(loss), {k: float(v) for k, v in info.items()})
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--what", default="all")
@@ -427,6 +479,8 @@ def main():
         gen_pinn(R)
     if w in ("all", "samples"):
         gen_samples(R)
+    if w in ("all", "posterior_loss"):
+        gen_posterior_loss(R)
     if w in ("all", "surrogate"):
         gen_surrogate(R)
     if w in ("all", "prior"):

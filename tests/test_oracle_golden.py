@@ -175,3 +175,21 @@ def test_mh_oracle_replays_reference_trajectories(golden):
     np.testing.assert_allclose(ed, z["mh_ediff"], rtol=1e-4, atol=1e-3)
     # some proposals were accepted and some rejected
     assert 0 < np.mean(np.any(x != z["mh_x0"], axis=1)) <= 1
+
+
+def test_posterior_loss_oracle_matches_reference(golden):
+    """oracle.posterior_loss_grad (float64, the likelihood target by linearity of the reference's
+    detached VJPs / VHPs) against the reference's PosteriorLoss forward + backward (G10)."""
+    z = golden("posterior_loss.npz")
+    sur = O.surrogate_params_from_npz(golden("surrogate.npz"))
+    pp, pl = O.mlp_params_from_state(z, "prior_"), O.mlp_params_from_state(z, "lik_")
+    loss, info, gp, gl, T = O.posterior_loss_grad(pp, pl, sur, z["x"], z["y"], z["t"], z["eps"],
+                                                  float(z["a"]), float(z["b"]), float(z["lam"]))
+    assert abs(loss - float(z["loss"])) < 1e-5 * abs(float(z["loss"]))
+    assert abs(info["PriorLoss"] - float(z["PriorLoss"])) < 1e-5 * float(z["PriorLoss"])
+    assert abs(info["LikelihoodLoss"] - float(z["LikelihoodLoss"])) < 1e-5 * float(z["LikelihoodLoss"])
+    assert np.abs(T - z["target"]).max() < 2e-4 * np.abs(z["target"]).max()
+    for tag, grads in (("prior", gp), ("lik", gl)):
+        for i, (dW, db) in zip([0, 3, 5, 7], grads):
+            for got, ref in ((dW, z[f"{tag}_grad_{i}_weight"]), (db, z[f"{tag}_grad_{i}_bias"])):
+                assert np.abs(got - ref).max() < 2e-5 * np.abs(ref).max()
