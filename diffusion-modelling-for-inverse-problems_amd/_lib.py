@@ -33,7 +33,7 @@ EXPORTED = (
     "dmip_em_sample_stamps", "dmip_em_sample_posterior", "dmip_em_sample_cdiffe", "dmip_loss_grad",
     "dmip_loss_grad_supported", "dmip_histogram", "dmip_surrogate_create", "dmip_surrogate_destroy",
     "dmip_surrogate_forward", "dmip_log_posterior", "dmip_mh_sample", "dmip_dps_sample", "dmip_device_status",
-    "dmip_sampler_supported_f32", "dmip_posterior_loss_grad",
+    "dmip_sampler_supported_f32", "dmip_posterior_loss_grad", "dmip_loss_grad_f32",
 )
 DMIP_DPS_NLL, DMIP_DPS_NORM = 0, 1
 
@@ -67,6 +67,10 @@ def _declare(lib):
     lib.dmip_sampler_supported.argtypes = [_i32, _i32, _i32, _i32, _i32]
     lib.dmip_sampler_supported_f32.argtypes = [_i32, _i32, _i32, _i32, _i32]
     lib.dmip_device_status.argtypes = [_c_void_p]
+    lib.dmip_loss_grad_f32.argtypes = [_i32, _i32, _i32, ctypes.POINTER(_i32), _i32, ctypes.POINTER(_c_void_p),
+                                       ctypes.POINTER(_c_void_p), ctypes.POINTER(DmipVpsde), ctypes.POINTER(DmipLossCfg),
+                                       _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _c_void_p,
+                                       _c_void_p, _c_void_p]
     _pp = ctypes.POINTER(_c_void_p)
     lib.dmip_posterior_loss_grad.argtypes = [_i32, _i32, _i32, ctypes.POINTER(_i32), _pp, _pp, _pp, _pp, _c_void_p,
                                              ctypes.POINTER(DmipScatNoise), _f32, ctypes.POINTER(DmipVpsde),
@@ -110,7 +114,7 @@ def _declare(lib):
     lib.dmip_dps_sample.argtypes = [_c_void_p, _c_void_p, ctypes.POINTER(DmipScatNoise), ctypes.POINTER(DmipVpsde),
                                     _c_void_p, _i32, _i64, _i64, _i32, _f32, _f32, _u64, _i32, _f32, _c_void_p,
                                     _c_void_p]
-    for name in ("dmip_posterior_loss_grad", "dmip_device_status", "dmip_sampler_supported_f32", "dmip_dps_sample", "dmip_mlp_create", "dmip_mlp_destroy", "dmip_mlp_forward", "dmip_em_sample",
+    for name in ("dmip_loss_grad_f32", "dmip_posterior_loss_grad", "dmip_device_status", "dmip_sampler_supported_f32", "dmip_dps_sample", "dmip_mlp_create", "dmip_mlp_destroy", "dmip_mlp_forward", "dmip_em_sample",
                  "dmip_rng_words", "dmip_rng_normals", "dmip_schedule", "dmip_sampler_supported",
                  "dmip_em_sample_stamps", "dmip_em_sample_posterior", "dmip_em_sample_cdiffe",
                  "dmip_loss_grad", "dmip_loss_grad_supported", "dmip_histogram", "dmip_surrogate_create",
@@ -268,6 +272,18 @@ def loss_grad(layers, in_dim, out_dim, xdim, sde, cfg, x, y, t, eps, grad_out, l
     check(lib().dmip_loss_grad(in_dim, out_dim, L, widths, xdim, wp, bp, ctypes.byref(sde), ctypes.byref(cfg),
                                ptr(x), ptr(y), ptr(t), ptr(eps), int(x.shape[0]), ptr(grad_out), ptr(loss_out),
                                stream_of(x.device)))
+
+
+def loss_grad_f32(layers, in_dim, out_dim, xdim, sde, cfg, x, y, t, eps, grad_out, loss_out, ic_target=None):
+    """dmip_loss_grad_f32: the exact-f32 stacked-jet training step at any width."""
+    calls["loss_grad_f32"] = calls.get("loss_grad_f32", 0) + 1
+    L = len(layers) - 1
+    widths = (_i32 * L)(*[int(layers[i][0].shape[0]) for i in range(L)])
+    wp = (_c_void_p * (L + 1))(*[w.data_ptr() for w, _ in layers])
+    bp = (_c_void_p * (L + 1))(*[b.data_ptr() for _, b in layers])
+    check(lib().dmip_loss_grad_f32(in_dim, out_dim, L, widths, xdim, wp, bp, ctypes.byref(sde), ctypes.byref(cfg),
+                                   ptr(x), ptr(y), ptr(t), ptr(eps), ptr(ic_target), int(x.shape[0]), ptr(grad_out),
+                                   ptr(loss_out), stream_of(x.device)))
 
 
 def histogram(x, nbins, lo, hi, counts):

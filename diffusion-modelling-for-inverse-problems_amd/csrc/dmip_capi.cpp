@@ -767,6 +767,97 @@ int dmip_loss_grad(int in_dim, int out_dim, int n_hidden, const int* widths, int
   return DMIP_OK;
 }
 
+int dmip_loss_grad_f32(int in_dim, int out_dim, int n_hidden, const int* widths, int xdim,
+                       const float* const* weights_dev, const float* const* biases_dev, const dmip_vpsde* sde,
+                       const dmip_loss_cfg* cfg, const float* x_dev, const float* y_dev, const float* t_dev,
+                       const float* eps_dev, const float* ic_target_dev, int64_t batch, float* grad_out_dev,
+                       float* loss_out_dev, void* stream) {
+  if (!widths || !weights_dev || !biases_dev || !sde || !cfg || !x_dev || !y_dev || !t_dev || !eps_dev ||
+      !grad_out_dev || !loss_out_dev)
+    return fail(DMIP_ERR_INVALID, "null argument");
+  if (n_hidden < 1 || n_hidden > dmip::kJetsMaxLayers - 1) return fail(DMIP_ERR_UNSUPPORTED, "n_hidden must be in [1, 8]");
+  if (xdim < 1 || xdim > 4 || out_dim != xdim)
+    return fail(DMIP_ERR_UNSUPPORTED, "f32 training: CDE networks (out_dim == xdim) with xdim in [1, 4]");
+  const int ydim = in_dim - xdim - 1;
+  if (ydim < 0) return fail(DMIP_ERR_INVALID, "in_dim must be xdim + ydim + 1");
+  for (int i = 0; i < n_hidden; ++i)
+    if (widths[i] < 1 || widths[i] > 4096) return fail(DMIP_ERR_INVALID, "hidden widths must be in [1, 4096]");
+  for (int i = 0; i <= n_hidden; ++i)
+    if (!weights_dev[i] || !biases_dev[i]) return fail(DMIP_ERR_INVALID, "null layer pointer");
+  if (batch < 1) return fail(DMIP_ERR_INVALID, "batch must be >= 1");
+  if (cfg->kind < DMIP_LOSS_DSM || cfg->kind > DMIP_LOSS_PINN2) return fail(DMIP_ERR_INVALID, "unknown loss kind");
+  const bool has_pde = cfg->kind != DMIP_LOSS_DSM;
+  const bool has_ic = cfg->kind == DMIP_LOSS_PINN || cfg->kind == DMIP_LOSS_PINN2;
+  if (has_pde && cfg->pde != DMIP_PDE_FPE && cfg->pde != DMIP_PDE_CFPE)
+    return fail(DMIP_ERR_INVALID, "pde must be DMIP_PDE_FPE or DMIP_PDE_CFPE for this loss");
+  if (has_ic && !ic_target_dev && (xdim != 2 || ydim != 2))
+    return fail(DMIP_ERR_INVALID, "initial-condition target required (the built-in one is the linear problem's, 2-D)");
+  if (!(sde->beta_min > 0.0)) return fail(DMIP_ERR_INVALID, "beta_min must be > 0");
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t B = batch;
+  dmip::JetsParams p{};
+  p.batch = B;
+  p.xdim = xdim;
+  p.ydim = ydim;
+  p.out_dim = out_dim;
+  p.bmin = (float)sde->beta_min;
+  p.bdiff = (float)(sde->beta_max - sde->beta_min);
+  p.lam = cfg->lam;
+  p.lam2 = cfg->lam2;
+  p.has_dsm = cfg->kind != DMIP_LOSS_PINN2;
+  p.pde = has_pde ? cfg->pde : 0;
+  p.pde_l1 = cfg->pde_metric == DMIP_METRIC_L1;
+  p.ic_l1 = cfg->ic_metric == DMIP_METRIC_L1;
+  for (int i = 0; i < 4; ++i) p.icA[i] = cfg->ic_A[i], p.icS[i] = cfg->ic_Sinv[i];
+  p.icb[0] = cfg->ic_b[0];
+  p.icb[1] = cfg->ic_b[1];
+  p.x = x_dev;
+  p.y = y_dev;
+  p.t = t_dev;
+  p.eps = eps_dev;
+  p.ic_target = ic_target_dev;
+  const bool fpe = has_pde && cfg->pde == DMIP_PDE_FPE;
+  p.blk_v = has_pde ? 1 : -1;
+  p.blk_c = has_ic ? (has_pde ? 2 : 1) : -1;
+  p.n_bwd = 1 + (has_pde ? 1 : 0) + (has_ic ? 1 : 0);
+  p.blk_e = p.n_bwd;
+  p.n_e = fpe ? xdim : 0;
+  p.n_pair = fpe ? xdim * (xdim + 1) / 2 : 0;
+  p.n_streams = p.n_bwd + p.n_e + p.n_pair;
+  int wmax = in_dim + 1;
+  for (int i = 0; i < n_hidden; ++i) wmax = std::max(wmax, widths[i] + 1);
+  p.splits = (int)std::max<int64_t>(1, std::min<int64_t>(64, (int64_t)p.n_bwd * B / 4096));
+  const int64_t nS = p.n_streams, nb = p.n_bwd;
+  std::vector<std::pair<float**, size_t>> plan;
+  for (int l = 0; l <= n_hidden; ++l) plan.emplace_back(&p.h[l], (size_t)nS * B * ((l == 0 ? in_dim : widths[l - 1]) + 1));
+  for (int l = 0; l < n_hidden; ++l) plan.emplace_back(&p.aux[l], (size_t)3 * B * widths[l]);
+  plan.emplace_back(&p.scal, (size_t)B * 8);
+  plan.emplace_back(&p.x_t, (size_t)B * xdim);
+  plan.emplace_back(&p.z, (size_t)nS * B * wmax);
+  plan.emplace_back(&p.a_out, (size_t)nS * B * out_dim);
+  plan.emplace_back(&p.zbar, (size_t)nb * B * out_dim);
+  plan.emplace_back(&p.zbar_a, (size_t)nb * B * wmax);
+  plan.emplace_back(&p.zbar_b, (size_t)nb * B * wmax);
+  plan.emplace_back(&p.hbar, (size_t)nb * B * wmax);
+  plan.emplace_back(&p.rows, (size_t)B * 3);
+  plan.emplace_back(&p.part, (size_t)p.splits * wmax * wmax);
+  size_t total = 0;
+  for (auto& q : plan) total += (q.second * sizeof(float) + 255) / 256 * 256;
+  char* scratch = nullptr;
+  hipError_t e = hipMallocAsync((void**)&scratch, total, st);
+  if (e != hipSuccess) return fail(DMIP_ERR_ALLOC, std::string("hipMallocAsync: ") + hipGetErrorString(e));
+  size_t o = 0;
+  for (auto& q : plan) {
+    *q.first = (float*)(scratch + o);
+    o += (q.second * sizeof(float) + 255) / 256 * 256;
+  }
+  p.loss_out = loss_out_dev;
+  e = dmip::launch_jets_loss_grad(p, n_hidden, widths, weights_dev, biases_dev, grad_out_dev, st);
+  (void)hipFreeAsync(scratch, st);
+  if (e != hipSuccess) return hip_fail(e, "loss_grad_f32 launch");
+  return DMIP_OK;
+}
+
 int dmip_histogram(const float* x_dev, int64_t n, int d, int nbins, double lo, double hi, int n_hist,
                    uint32_t* counts_dev, void* stream) {
   if (!x_dev || !counts_dev) return fail(DMIP_ERR_INVALID, "null argument");

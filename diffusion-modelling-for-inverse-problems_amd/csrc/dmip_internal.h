@@ -274,6 +274,41 @@ struct PosteriorParams {
   float* loss_out;        // [3]: loss, PriorLoss, LikelihoodLoss
 };
 
+// ---- exact-f32 score-matching losses at any width (dmip_jets.hip): stacked jet streams
+constexpr int kJetsMaxLayers = 9;
+
+struct JetsParams {
+  long long batch;
+  int xdim, ydim, out_dim;
+  float bmin, bdiff, lam, lam2;
+  int has_dsm, pde, pde_l1, ic_l1;      // pde: 0 none, 1 ScoreFPE, 2 conditional ScoreFPE
+  float icA[4], icb[2], icS[4];         // linear-problem IC target (used when ic_target is null)
+  const float* x;                       // [B][xdim]
+  const float* y;                       // [B][ydim]
+  const float* t;                       // [B]
+  const float* eps;                     // [B][xdim]
+  const float* ic_target;               // [B][xdim] or null
+  // stream blocks (B rows each): P = 0, then V, C, the first-order E_a and the second-order pairs
+  int n_streams, n_bwd, blk_v, blk_c, blk_e, n_e, n_pair;
+  float* scal;                          // [B][8]: alpha, std, beta, g, g'
+  float* x_t;                           // [B][xdim]
+  float* h[kJetsMaxLayers];             // layer inputs [n_streams B][in_l + 1]
+  float* aux[kJetsMaxLayers];           // hidden layer l: [3][B][width_l] (d1, d2 z_V, d1 of C)
+  float* z;                             // [n_streams B][max width] pre-activations
+  float* a_out;                         // [n_streams B][out_dim]
+  float* zbar;                          // [n_bwd][B][out_dim] output adjoints
+  float* zbar_a;                        // [n_bwd B][max width] hidden adjoints (ping-pong)
+  float* zbar_b;
+  float* hbar;                          // [n_bwd B][max width]
+  float* rows;                          // [B][3]: DSM, PDE, IC per row
+  float* loss_out;                      // [4]: loss, PDE-Loss, Initial Condition, DSM
+  float* part;                          // split-K partials
+  int splits;
+};
+
+hipError_t launch_jets_loss_grad(const JetsParams& p, int n_hidden, const int* widths, const float* const* W,
+                                 const float* const* b, float* grads, hipStream_t st);
+
 hipError_t launch_gemm_f32(const GemmParams& p, bool ta, bool tb, int splits, hipStream_t st);
 hipError_t launch_ones_column(float* h, long long rows, int ld, hipStream_t st);
 hipError_t launch_posterior_stage(const PosteriorParams& p, int stage, hipStream_t st);

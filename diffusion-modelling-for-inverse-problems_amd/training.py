@@ -1,11 +1,16 @@
-"""Fused training step on the HIP device (libdmip dmip_loss_grad).
+"""Fused training step on the HIP device (§8a A6, A13-A18).
 
-`fused_loss_grad(model, loss_fn, x, y, t, eps)` computes the loss value, its components and the
+`fused_loss_grad(model, loss_fn, cfg, x, y, t, eps)` computes the loss value, its components and the
 parameter gradients of DSMLoss / DSM_PDELoss / PINNLoss / PINNLoss2 (losses.py:42-290 with the
-ScoreFPE or conditional ScoreFPE residual) in one persistent kernel + one reduction, writing the
-gradients into the parameters' `.grad` (set, not accumulated). It is what CDE.train_epoch runs on a
-HIP device when `fused_config` accepts the network and loss; everything else (other networks, the
-Posterior loss, CPU tensors) takes the autograd path of losses.py.
+ScoreFPE or conditional ScoreFPE residual), writing the gradients into the parameters' `.grad` (set,
+not accumulated). Two device paths:
+  * "fp32" (default): dmip_loss_grad_f32 -- exact f32 at any width (the reference configs' [512]*3
+    included) and any initial-condition target (the linear problem's analytic score, the
+    scatterometry -energy_grad, ...): forward-mode jets as stacked-stream MFMA GEMMs;
+  * "bf16": dmip_loss_grad -- the persistent bf16-MFMA kernel of BASELINE config 5 (the linear
+    problem's width-64 CDE with its analytic IC target), selected with $DMIP_TRAIN_PRECISION=bf16.
+It is what CDE.train_epoch runs on a HIP device when `fused_config` accepts the network and loss;
+everything else (CDiffE's joint training, CPU tensors) takes the autograd path of losses.py.
 """
 import os
 
@@ -20,8 +25,20 @@ def _metric(m):
     return _lib.DMIP_METRIC_L1 if m == 'L1' else _lib.DMIP_METRIC_L2
 
 
+def train_precision():
+    return os.environ.get("DMIP_TRAIN_PRECISION", "fp32")
+
+
+def _linear_ic(loss_fn):
+    prob = getattr(loss_fn.initial_condition, "__self__", None)
+    if isinstance(prob, LinearForwardProblem) and \
+            getattr(loss_fn.initial_condition, "__func__", None) is LinearForwardProblem.score_posterior:
+        return prob
+    return None
+
+
 def fused_config(model, loss_fn):
-    """dmip_loss_cfg for (model, loss_fn), or None when the fused kernel does not cover them."""
+    """dmip_loss_cfg for (model, loss_fn), or None when no fused path covers them."""
     if os.environ.get("DMIP_TRAIN_FUSED", "1") == "0":
         return None
     net = model.sde.a
@@ -31,10 +48,7 @@ def fused_config(model, loss_fn):
     p0 = layers[0][0]
     if not p0.is_cuda or p0.dtype != torch.float32:
         return None
-    widths = [int(w.shape[0]) for w, _ in layers[:-1]]
-    if not _lib.loss_grad_supported(net.input_dim, net.output_dim, widths, model.xdim):
-        return None
-    if net.output_dim != model.xdim:  # CDE only (CDiffE trains on the joint z)
+    if net.output_dim != model.xdim or model.xdim > 4 or len(layers) - 1 > 8:  # CDE only (CDiffE trains on z)
         return None
     cfg = _lib.DmipLossCfg()
     if type(loss_fn) is DSMLoss:
@@ -48,21 +62,22 @@ def fused_config(model, loss_fn):
     cfg.pde_metric = _metric(loss_fn.pde_loss.metric)
     cfg.lam = float(loss_fn.lam)
     if cfg.kind in (_lib.DMIP_LOSS_PINN, _lib.DMIP_LOSS_PINN2):
-        prob = getattr(loss_fn.initial_condition, "__self__", None)
-        if not isinstance(prob, LinearForwardProblem) or \
-                getattr(loss_fn.initial_condition, "__func__", None) is not LinearForwardProblem.score_posterior:
-            return None  # the kernel's IC target is the linear problem's analytic posterior score
         cfg.ic_metric = _metric(loss_fn.ic_metric)
         cfg.lam2 = float(loss_fn.lam2)
-        cfg.ic_A[:] = [float(v) for v in prob.A.reshape(-1)]
-        cfg.ic_b[:] = [float(v) for v in prob.b.reshape(-1)]
-        cfg.ic_Sinv[:] = [float(v) for v in prob.Sigma_inv.reshape(-1)]
+        prob = _linear_ic(loss_fn)
+        if prob is not None:
+            cfg.ic_A[:] = [float(v) for v in prob.A.reshape(-1)]
+            cfg.ic_b[:] = [float(v) for v in prob.b.reshape(-1)]
+            cfg.ic_Sinv[:] = [float(v) for v in prob.Sigma_inv.reshape(-1)]
+        elif not callable(loss_fn.initial_condition):
+            return None
     return cfg
 
 
-def fused_loss_grad(model, loss_fn, cfg, x, y, t, eps):
+def fused_loss_grad(model, loss_fn, cfg, x, y, t, eps, precision=None):
     """One fused loss + gradient evaluation. Returns (loss, info) like the reference loss objects:
-    a 0-d tensor and {component name: 0-d tensor}."""
+    a 0-d tensor and {component name: 0-d tensor}. precision: "fp32" (dmip_loss_grad_f32, default) or
+    "bf16" (dmip_loss_grad, where compiled: the linear problem's width-64 CDE, analytic IC)."""
     net = model.sde.a
     layers = [(w.detach(), b.detach()) for w, b in net.linear_layers()]
     dev = layers[0][0].device
@@ -75,8 +90,22 @@ def fused_loss_grad(model, loss_fn, cfg, x, y, t, eps):
     flat = torch.empty(sum(p.numel() for p in params), **f32)
     out = torch.empty(4, **f32)
     base = model.sde.base_sde
-    _lib.loss_grad(layers, net.input_dim, net.output_dim, model.xdim, _lib.vpsde(base.beta_min, base.beta_max, 1.0),
-                   cfg, x, y, t, eps, flat, out)
+    sde = _lib.vpsde(base.beta_min, base.beta_max, 1.0)
+    has_ic = cfg.kind in (_lib.DMIP_LOSS_PINN, _lib.DMIP_LOSS_PINN2)
+    precision = precision or train_precision()
+    widths = [int(w.shape[0]) for w, _ in layers[:-1]]
+    bf16_ok = _lib.loss_grad_supported(net.input_dim, net.output_dim, widths, model.xdim) and \
+        (not has_ic or _linear_ic(loss_fn) is not None)
+    if precision == "bf16" and bf16_ok:
+        _lib.loss_grad(layers, net.input_dim, net.output_dim, model.xdim, sde, cfg, x, y, t, eps, flat, out)
+    else:
+        ic = None
+        if has_ic and _linear_ic(loss_fn) is None:
+            # the reference's initial_condition(x, y) is a constant target (losses.py:223-226)
+            with torch.enable_grad():
+                ic = loss_fn.initial_condition(x, y)
+            ic = ic.detach().to(**f32)[:, :model.xdim].contiguous()
+        _lib.loss_grad_f32(layers, net.input_dim, net.output_dim, model.xdim, sde, cfg, x, y, t, eps, flat, out, ic)
     off = 0
     for p in params:
         p.grad = flat[off:off + p.numel()].view_as(p)

@@ -156,6 +156,19 @@ int dmip_loss_grad(int in_dim, int out_dim, int n_hidden, const int* widths, int
                    const dmip_loss_cfg* cfg, const float* x_dev, const float* y_dev, const float* t_dev,
                    const float* eps_dev, int64_t batch, float* grad_out_dev, float* loss_out_dev, void* stream);
 
+/* The same losses, gradients and outputs in exact f32 at any network shape (hidden widths up to 4096,
+ * 1-8 hidden layers, xdim <= 4; the reference configs' [512]*3 included): forward-mode jets as
+ * stacked streams through MFMA GEMMs with fused epilogues (dmip_jets.hip), reverse pass through the
+ * primal, time-tangent and initial-condition streams, deterministic split-K reductions.
+ *   ic_target_dev  [batch][xdim] initial-condition target score_posterior(x, y) (PINNLoss's
+ *                  initial_condition, e.g. the scatterometry -energy_grad, main_diffusion_scatterometry.py:
+ *                  142-145), or NULL for the linear problem's analytic target from cfg (xdim = ydim = 2) */
+int dmip_loss_grad_f32(int in_dim, int out_dim, int n_hidden, const int* widths, int xdim,
+                       const float* const* weights_dev, const float* const* biases_dev, const dmip_vpsde* sde,
+                       const dmip_loss_cfg* cfg, const float* x_dev, const float* y_dev, const float* t_dev,
+                       const float* eps_dev, const float* ic_target_dev, int64_t batch, float* grad_out_dev,
+                       float* loss_out_dev, void* stream);
+
 /* Non-zero when dmip_loss_grad has a kernel for this network shape. */
 int dmip_loss_grad_supported(int in_dim, int out_dim, int n_hidden, const int* widths, int xdim);
 

@@ -371,7 +371,7 @@ def _vp_terms(t, beta_min=BETA_MIN, beta_max=BETA_MAX):
 
 
 def loss_grad(params, x, y, t, eps, kind="pinn", pde="FPE", pde_metric="L1", ic_metric="L2", lam=1.0,
-              lam2=1.0, ic_A=None, ic_b=None, ic_Sinv=None, beta_min=BETA_MIN, beta_max=BETA_MAX):
+              lam2=1.0, ic_A=None, ic_b=None, ic_Sinv=None, beta_min=BETA_MIN, beta_max=BETA_MAX, ic_target=None):
     """Loss value, components and parameter gradients of the CDE training losses for one batch,
     with the reference's semantics (models/diffusion.py:80-89 -> losses.py):
       kind 'dsm'     DSMLoss(a/g, std, eps).mean()                        (losses.py:42-52)
@@ -380,7 +380,8 @@ def loss_grad(params, x, y, t, eps, kind="pinn", pde="FPE", pde_metric="L1", ic_
       kind 'pinn2'   PINNLoss2: mean(IC + lam PDE)                         (losses.py:245-290)
     PDE 'FPE' = ScoreFPELoss (exact divergence; ds/dt the total derivative through x_t(t) and g(t);
     grad_x detached), 'cFPE' = ConditionalScoreFPELoss. IC = lam2 * metric(a(x, y, 0)/g(0) - ic(x, y))
-    with ic the linear problem's analytic posterior score (linear_problem.py:61-65).
+    with ic the linear problem's analytic posterior score (linear_problem.py:61-65), or the given
+    ic_target (n, d) (e.g. the scatterometry -energy_grad, main_diffusion_scatterometry.py:142-145).
     Network: nets.py:17-35 with the double tanh on layer 1. Returns (loss, comps, grads) where
     grads = [(dW, db), ...] per linear layer."""
     P = [(np.asarray(W, np.float64), np.asarray(b, np.float64)) for W, b in params]
@@ -525,10 +526,13 @@ def loss_grad(params, x, y, t, eps, kind="pinn", pde="FPE", pde_metric="L1", ic_
         aC, _, _, cache_C = forward(u_C, [e])  # dummy tangent (zero direction)
         g0 = np.sqrt(beta_min)
         s0 = aC / g0
-        A = np.asarray(ic_A, np.float64)
-        bb = np.asarray(ic_b, np.float64)
-        S = np.asarray(ic_Sinv, np.float64)
-        ic = -x + ((y - (x @ A.T + bb)) @ S.T) @ A
+        if ic_target is not None:
+            ic = np.asarray(ic_target, np.float64)
+        else:
+            A = np.asarray(ic_A, np.float64)
+            bb = np.asarray(ic_b, np.float64)
+            S = np.asarray(ic_Sinv, np.float64)
+            ic = -x + ((y - (x @ A.T + bb)) @ S.T) @ A
         dlt = s0[:, :d] - ic
         if ic_metric == "L2":
             rows = lam2 * np.mean(dlt * dlt, axis=1)
@@ -749,6 +753,17 @@ def _mlp_backprop(tape, W, adj):
         if li > 0:
             d = d * tape[li - 1][1]
     return grads, d
+
+
+def reference_weights(dims, seed):
+    """nn.Linear-range weights from a numpy seed (tests/golden/make_golden.py reference_weights, G11)."""
+    g = np.random.default_rng(seed)
+    out = []
+    for i in range(len(dims) - 1):
+        bd = 1.0 / np.sqrt(dims[i])
+        out.append((g.uniform(-bd, bd, (dims[i + 1], dims[i])).astype(F32),
+                    g.uniform(-bd, bd, dims[i + 1]).astype(F32)))
+    return out
 
 
 def posterior_loss_grad(prior_params, lik_params, sur_params, x, y, t, eps, a=0.2, b=0.01, lam=0.01,

@@ -24,6 +24,10 @@ Fixtures (SURVEY.md §8c "Golden fixtures"):
   G10 posterior_loss.npz   PosteriorLoss (losses.py:293-386) value, components, likelihood target and every
                            parameter gradient of both networks (prior = G9 checkpoint, likelihood seeded,
                            surrogate = G7) on 256 rows with captured eps and t
+  G11 pinn_ref_configs.npz PINNLoss value, components and every parameter gradient at the reference configs'
+                           hidden_layers [512]*3 for both problems (config_linear.yml / config_scatterometry.yml
+                           loss settings; the scatterometry IC target -energy_grad(get_log_posterior),
+                           main_diffusion_scatterometry.py:142-145); weights from a numpy seed (reference_weights)
   G8 surrogate_io.npz      surrogate forward, get_log_posterior and its autograd input gradient
                            (energy_grad) on 256 seeded rows; anneal_to_energy (random-walk MH) with
                            its captured draws (64 chains x 50 steps) and a 4000-chain x 1000-step run
@@ -454,6 +458,72 @@ def gen_posterior_loss(R):
     print("G10 loss", float(loss), {k: float(v) for k, v in info.items()})
 
 
+# ---------------------------------------------------------------------------------------- G11
+def reference_weights(dims, seed):
+    """Layer weights in nn.Linear's default range U(+-1/sqrt(fan_in)) from a numpy seed, so the tests can
+    rebuild the same network without storing it (float32)."""
+    g = np.random.default_rng(seed)
+    out = []
+    for i in range(len(dims) - 1):
+        bd = 1.0 / np.sqrt(dims[i])
+        out.append((g.uniform(-bd, bd, (dims[i + 1], dims[i])).astype(np.float32),
+                    g.uniform(-bd, bd, dims[i + 1]).astype(np.float32)))
+    return out
+
+
+def gen_pinn_ref_configs(R):
+    """PINNLoss forward + backward at hidden_layers [512]*3 (config_linear.yml:11-16,21 and
+    config_scatterometry.yml:10-19), as CDE.train_epoch calls it (models/diffusion.py:80-89)."""
+    import torch
+    from torch import nn
+    torch.set_num_threads(os.cpu_count())
+    out = {}
+    zs = np.load(os.path.join(OUT, "surrogate.npz"))
+    fm = nn.Sequential(nn.Linear(3, 256), nn.ReLU(), nn.Linear(256, 256), nn.ReLU(), nn.Linear(256, 256), nn.ReLU(),
+                       nn.Linear(256, 23))
+    fm.load_state_dict({k: torch.from_numpy(zs[k.replace(".", "_")]) for k in fm.state_dict().keys()})
+    for prm in fm.parameters():
+        prm.requires_grad = False
+    f = R.linear_problem.LinearForwardProblem()
+    a_s, b_s, lbd = 0.2, 0.01, 1000.0
+    for tag, (xd, yd, seed) in {"lin": (2, 2, 511), "scat": (3, 23, 512)}.items():
+        m = R.diffusion.CDE(xd, yd, [512] * 3)
+        lin = [l for l in m.sde.a if isinstance(l, nn.Linear)]
+        for l, (W, bb) in zip(lin, reference_weights([xd + yd + 1, 512, 512, 512, xd], seed)):
+            l.weight.data.copy_(torch.from_numpy(W))
+            l.bias.data.copy_(torch.from_numpy(bb))
+        g = torch.Generator().manual_seed(seed)
+        B = 128
+        if tag == "lin":
+            x = torch.randn(B, 2, generator=g)
+            y = (x @ f.A.T + f.b) + 0.3 * torch.randn(B, 2, generator=g)
+            lf = R.losses.PINNLoss(f.score_posterior, lam=1e-3, lam2=0.1, pde_loss="FPE", ic_metric="L2",
+                                   pde_metric="L1")
+        else:
+            x = torch.rand(B, 3, generator=g) * 2 - 1
+            ys = torch.from_numpy(np.load(os.path.join(OUT, "data_scat.npz"))["y_test"])
+            y = ys[torch.arange(B) % ys.shape[0]]
+            sp = lambda xx, yy: -R.snf.energy_grad(xx, lambda v: R.scat.get_log_posterior(v, fm, a_s, b_s, yy, lbd))[0]
+            lf = R.losses.PINNLoss(sp, lam=0.01, lam2=0.001, pde_loss="FPE", ic_metric="L2", pde_metric="L1")
+            out["scat_ic_target"] = sp(x.clone(), y).detach().numpy()
+        t = (1e-4 + torch.rand(B, 1, generator=g) * (1 - 1e-4)).requires_grad_(True)
+        eps = torch.randn(B, xd, generator=g)
+        sde = m.sde.base_sde
+        std = sde.var(t) ** 0.5
+        x_t = eps * std + sde.mean_weight(t) * x
+        gg = sde.g(t, x_t)
+        loss, info = lf(m.sde, x, y, x_t, t, eps, std, gg)
+        loss.backward()
+        out.update({f"{tag}_x": x.detach().numpy(), f"{tag}_y": y.numpy(), f"{tag}_t": t.detach().numpy(),
+                    f"{tag}_eps": eps.numpy(), f"{tag}_seed": seed, f"{tag}_loss": float(loss)})
+        for k, v in info.items():
+            out[f"{tag}_{k.replace(' ', '_').replace('-', '_')}"] = float(v)
+        for k, prm in m.sde.a.named_parameters():
+            out[f"{tag}_grad_{k.replace('.', '_')}"] = prm.grad.numpy().copy()
+        print("G11", tag, float(loss), {k: float(v) for k, v in info.items()})
+    np.savez(os.path.join(OUT, "pinn_ref_configs.npz"), **out)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--what", default="all")
@@ -481,6 +551,8 @@ def main():
         gen_samples(R)
     if w in ("all", "posterior_loss"):
         gen_posterior_loss(R)
+    if w in ("all", "pinn_ref"):
+        gen_pinn_ref_configs(R)
     if w in ("all", "surrogate"):
         gen_surrogate(R)
     if w in ("all", "prior"):

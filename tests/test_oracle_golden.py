@@ -193,3 +193,23 @@ def test_posterior_loss_oracle_matches_reference(golden):
         for i, (dW, db) in zip([0, 3, 5, 7], grads):
             for got, ref in ((dW, z[f"{tag}_grad_{i}_weight"]), (db, z[f"{tag}_grad_{i}_bias"])):
                 assert np.abs(got - ref).max() < 2e-5 * np.abs(ref).max()
+
+
+@pytest.mark.parametrize("tag", ["lin", "scat"])
+def test_loss_grad_oracle_matches_reference_at_reference_width(golden, tag):
+    """oracle.loss_grad against the reference PINNLoss at hidden_layers [512]*3 with the configs' loss
+    settings (G11); the scatterometry IC target is the reference's own -energy_grad values."""
+    z = golden("pinn_ref_configs.npz")
+    xd, yd = (2, 2) if tag == "lin" else (3, 23)
+    params = O.reference_weights([xd + yd + 1, 512, 512, 512, xd], int(z[f"{tag}_seed"]))
+    kw = dict(kind="pinn", pde="FPE", pde_metric="L1", ic_metric="L2")
+    if tag == "lin":
+        kw.update(lam=1e-3, lam2=0.1, ic_A=[[1, 0.5], [0, 1]], ic_b=[0.3, 0.5], ic_Sinv=np.eye(2) / 0.3)
+    else:
+        kw.update(lam=0.01, lam2=0.001, ic_target=z["scat_ic_target"])
+    loss, comps, grads = O.loss_grad(params, z[f"{tag}_x"], z[f"{tag}_y"], z[f"{tag}_t"], z[f"{tag}_eps"], **kw)
+    assert abs(loss - float(z[f"{tag}_loss"])) < 1e-4 * abs(float(z[f"{tag}_loss"]))
+    assert abs(comps["PDE"] - float(z[f"{tag}_PDE_Loss"])) < 1e-3 * abs(float(z[f"{tag}_PDE_Loss"]))
+    for li, (dW, db) in zip([0, 3, 5, 7], grads):
+        for got, ref in ((dW, z[f"{tag}_grad_{li}_weight"]), (db, z[f"{tag}_grad_{li}_bias"])):
+            assert np.linalg.norm(got - ref) < 1e-3 * np.linalg.norm(ref), (li, np.linalg.norm(got - ref) / np.linalg.norm(ref))
