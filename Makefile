@@ -5,7 +5,7 @@ HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-parameter
 F32OBJS := $(CSRC)/dmip_f32.o $(CSRC)/dmip_f32_cde.o $(CSRC)/dmip_f32_post.o $(CSRC)/dmip_f32_cdiffe.o
-OBJS := $(CSRC)/dmip_kernels.o $(CSRC)/dmip_train.o $(CSRC)/dmip_eval.o $(CSRC)/dmip_surrogate.o $(CSRC)/dmip_gemm.o $(CSRC)/dmip_jets.o $(F32OBJS) $(CSRC)/dmip_capi.o
+OBJS := $(CSRC)/dmip_kernels.o $(CSRC)/dmip_train.o $(CSRC)/dmip_eval.o $(CSRC)/dmip_surrogate.o $(CSRC)/dmip_gemm.o $(CSRC)/dmip_jets.o $(CSRC)/dmip_step.o $(F32OBJS) $(CSRC)/dmip_capi.o
 HDRS := $(CSRC)/dmip_device.h $(CSRC)/dmip_internal.h include/dmip.h
 
 all: $(PKG)/libdmip.so
@@ -28,6 +28,9 @@ $(CSRC)/dmip_gemm.o: $(CSRC)/dmip_gemm.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(CSRC)/dmip_jets.o: $(CSRC)/dmip_jets.hip $(HDRS)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(CSRC)/dmip_step.o: $(CSRC)/dmip_step.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 # exact-f32 parity engine: one header, four translation units compiled in parallel

@@ -33,7 +33,8 @@ EXPORTED = (
     "dmip_em_sample_stamps", "dmip_em_sample_posterior", "dmip_em_sample_cdiffe", "dmip_loss_grad",
     "dmip_loss_grad_supported", "dmip_histogram", "dmip_surrogate_create", "dmip_surrogate_destroy",
     "dmip_surrogate_forward", "dmip_log_posterior", "dmip_mh_sample", "dmip_dps_sample", "dmip_device_status",
-    "dmip_sampler_supported_f32", "dmip_posterior_loss_grad", "dmip_loss_grad_f32",
+    "dmip_sampler_supported_f32", "dmip_posterior_loss_grad", "dmip_loss_grad_f32", "dmip_train_draws",
+    "dmip_adam_step",
 )
 DMIP_DPS_NLL, DMIP_DPS_NORM = 0, 1
 
@@ -67,6 +68,11 @@ def _declare(lib):
     lib.dmip_sampler_supported.argtypes = [_i32, _i32, _i32, _i32, _i32]
     lib.dmip_sampler_supported_f32.argtypes = [_i32, _i32, _i32, _i32, _i32]
     lib.dmip_device_status.argtypes = [_c_void_p]
+    lib.dmip_train_draws.argtypes = [_u64, _u64, _i64, _i32, _i32, ctypes.POINTER(DmipVpsde), ctypes.c_double, _f32,
+                                     _c_void_p, _c_void_p, _c_void_p]
+    lib.dmip_adam_step.argtypes = [_i32, ctypes.POINTER(_c_void_p), ctypes.POINTER(_c_void_p), ctypes.POINTER(_c_void_p),
+                                   ctypes.POINTER(_c_void_p), ctypes.POINTER(_i64), ctypes.c_double, ctypes.c_double,
+                                   ctypes.c_double, ctypes.c_double, _i64, _c_void_p]
     lib.dmip_loss_grad_f32.argtypes = [_i32, _i32, _i32, ctypes.POINTER(_i32), _i32, ctypes.POINTER(_c_void_p),
                                        ctypes.POINTER(_c_void_p), ctypes.POINTER(DmipVpsde), ctypes.POINTER(DmipLossCfg),
                                        _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _c_void_p,
@@ -114,7 +120,7 @@ def _declare(lib):
     lib.dmip_dps_sample.argtypes = [_c_void_p, _c_void_p, ctypes.POINTER(DmipScatNoise), ctypes.POINTER(DmipVpsde),
                                     _c_void_p, _i32, _i64, _i64, _i32, _f32, _f32, _u64, _i32, _f32, _c_void_p,
                                     _c_void_p]
-    for name in ("dmip_loss_grad_f32", "dmip_posterior_loss_grad", "dmip_device_status", "dmip_sampler_supported_f32", "dmip_dps_sample", "dmip_mlp_create", "dmip_mlp_destroy", "dmip_mlp_forward", "dmip_em_sample",
+    for name in ("dmip_train_draws", "dmip_adam_step", "dmip_loss_grad_f32", "dmip_posterior_loss_grad", "dmip_device_status", "dmip_sampler_supported_f32", "dmip_dps_sample", "dmip_mlp_create", "dmip_mlp_destroy", "dmip_mlp_forward", "dmip_em_sample",
                  "dmip_rng_words", "dmip_rng_normals", "dmip_schedule", "dmip_sampler_supported",
                  "dmip_em_sample_stamps", "dmip_em_sample_posterior", "dmip_em_sample_cdiffe",
                  "dmip_loss_grad", "dmip_loss_grad_supported", "dmip_histogram", "dmip_surrogate_create",

@@ -858,6 +858,68 @@ int dmip_loss_grad_f32(int in_dim, int out_dim, int n_hidden, const int* widths,
   return DMIP_OK;
 }
 
+int dmip_train_draws(uint64_t seed, uint64_t stream_id, int64_t batch, int xdim, int debias, const dmip_vpsde* sde,
+                     double t_epsilon, float t_add, float* t_out_dev, float* eps_out_dev, void* stream) {
+  if (!sde || !t_out_dev || !eps_out_dev) return fail(DMIP_ERR_INVALID, "null argument");
+  if (batch < 0 || xdim < 1 || xdim > 4) return fail(DMIP_ERR_INVALID, "batch >= 0 and xdim in [1, 4]");
+  if (!(sde->T > 0.0) || !(sde->beta_min > 0.0)) return fail(DMIP_ERR_INVALID, "bad SDE parameters");
+  if (batch == 0) return DMIP_OK;
+  dmip::TrainDrawsParams p{};
+  p.batch = batch;
+  p.xdim = xdim;
+  p.debias = debias ? 1 : 0;
+  p.seed = seed;
+  p.stream_id = stream_id;
+  p.t_add = t_add;
+  p.T = (float)sde->T;
+  const double a = sde->beta_max - sde->beta_min, b = sde->beta_min, te = t_epsilon;
+  const double B_te = 0.5 * a * te * te + b * te;
+  const double r_te = (b + a * te) / (1.0 - std::exp(-B_te));
+  const double A_te = std::log(std::expm1(B_te));
+  const double B_T = 0.5 * a * sde->T * sde->T + b * sde->T;
+  p.a = (float)a;
+  p.b = (float)b;
+  p.te = (float)te;
+  p.r_te = (float)r_te;
+  p.A_te = (float)A_te;
+  p.Z = (float)(te * r_te + std::log(std::expm1(B_T)) - A_te);
+  p.t = t_out_dev;
+  p.eps = eps_out_dev;
+  hipError_t e = dmip::launch_train_draws(p, (hipStream_t)stream);
+  return e == hipSuccess ? DMIP_OK : hip_fail(e, "train_draws launch");
+}
+
+int dmip_adam_step(int n_tensors, float* const* params, const float* const* grads, float* const* exp_avg,
+                   float* const* exp_avg_sq, const int64_t* numel, double lr, double beta1, double beta2, double eps,
+                   int64_t step, void* stream) {
+  if (!params || !grads || !exp_avg || !exp_avg_sq || !numel) return fail(DMIP_ERR_INVALID, "null argument");
+  if (n_tensors < 1 || n_tensors > dmip::kAdamMaxTensors)
+    return fail(DMIP_ERR_UNSUPPORTED, "n_tensors must be in [1, 16]");
+  if (step < 1) return fail(DMIP_ERR_INVALID, "step must be >= 1 (torch increments before the update)");
+  dmip::AdamParams p{};
+  p.n = n_tensors;
+  p.off[0] = 0;
+  for (int k = 0; k < n_tensors; ++k) {
+    if (!params[k] || !grads[k] || !exp_avg[k] || !exp_avg_sq[k] || numel[k] < 0)
+      return fail(DMIP_ERR_INVALID, "null tensor or negative size");
+    p.param[k] = params[k];
+    p.grad[k] = grads[k];
+    p.m[k] = exp_avg[k];
+    p.v[k] = exp_avg_sq[k];
+    p.off[k + 1] = p.off[k] + numel[k];
+  }
+  // torch.optim.Adam's scalars, in Python double like torch computes them
+  const double bc1 = 1.0 - std::pow(beta1, (double)step), bc2 = 1.0 - std::pow(beta2, (double)step);
+  p.step_size = (float)(lr / bc1);
+  p.bc2_sqrt = (float)std::sqrt(bc2);
+  p.w1 = (float)(1.0 - beta1);
+  p.beta2 = (float)beta2;
+  p.w2 = (float)(1.0 - beta2);
+  p.eps = (float)eps;
+  hipError_t e = dmip::launch_adam(p, (hipStream_t)stream);
+  return e == hipSuccess ? DMIP_OK : hip_fail(e, "adam launch");
+}
+
 int dmip_histogram(const float* x_dev, int64_t n, int d, int nbins, double lo, double hi, int n_hist,
                    uint32_t* counts_dev, void* stream) {
   if (!x_dev || !counts_dev) return fail(DMIP_ERR_INVALID, "null argument");

@@ -310,6 +310,34 @@ hipError_t launch_jets_loss_grad(const JetsParams& p, int n_hidden, const int* w
                                  const float* const* b, float* grads, hipStream_t st);
 
 hipError_t launch_gemm_f32(const GemmParams& p, bool ta, bool tb, int splits, hipStream_t st);
+
+// ---- device-side rest of a training step (dmip_step.hip)
+struct TrainDrawsParams {
+  long long batch;
+  int xdim, debias;
+  unsigned long long seed, stream_id;
+  float t_add, T;
+  float a, b, te, r_te, A_te, Z;  // sample_vp_truncated_q constants (sdes.py), host-computed in f64
+  float* t;                       // [B]
+  float* eps;                     // [B][xdim]
+};
+
+constexpr int kAdamMaxTensors = 16;
+
+struct AdamParams {
+  int n;
+  float* param[kAdamMaxTensors];
+  const float* grad[kAdamMaxTensors];
+  float* m[kAdamMaxTensors];
+  float* v[kAdamMaxTensors];
+  long long off[kAdamMaxTensors + 1];  // prefix sums of the tensors' sizes
+  // torch's scalars, each rounded from Python double as torch passes them: lerp weight 1 - beta1,
+  // beta2, addcmul value 1 - beta2, eps, lr / bias_correction1, sqrt(bias_correction2)
+  float w1, beta2, w2, eps, step_size, bc2_sqrt;
+};
+
+hipError_t launch_train_draws(const TrainDrawsParams& p, hipStream_t st);
+hipError_t launch_adam(const AdamParams& p, hipStream_t st);
 hipError_t launch_ones_column(float* h, long long rows, int ld, hipStream_t st);
 hipError_t launch_posterior_stage(const PosteriorParams& p, int stage, hipStream_t st);
 

@@ -38,8 +38,8 @@ device = 'cuda' if torch.cuda.is_available() else 'cpu'
 class _FusedStep:
     """A batch whose loss and parameter gradients came from the fused kernel (training.py)."""
 
-    def __init__(self, loss, info):
-        self.loss, self.info = loss, info
+    def __init__(self, loss, info, stepped=False):
+        self.loss, self.info, self.stepped = loss, info, stepped  # stepped: the optimizer update ran too
 
 
 def _draw_seed():
@@ -153,7 +153,8 @@ class BaseClassDiffusionModel:
                 loss = self._accumulate(logger_info, k, out)
                 optimizer.zero_grad()
                 loss.backward()
-            optimizer.step()
+            if not (isinstance(out, _FusedStep) and out.stepped):
+                optimizer.step()
             mean_loss = mean_loss * k / (k + 1) + loss / (k + 1)
         return mean_loss, logger_info
 
@@ -192,10 +193,16 @@ class CDE(BaseClassDiffusionModel):
         return out
 
     def train_epoch(self, optimizer, loss_fn, epoch_data_loader):
-        from .training import fused_config, fused_loss_grad
+        from .training import DeviceTrainStep, _plain_adam, device_step_enabled, fused_config, fused_loss_grad, \
+            loss_info
         cfg = fused_config(self, loss_fn)
+        # $DMIP_TRAIN_DEVICE_STEP=1: t, eps and Adam on the device too (training.DeviceTrainStep)
+        dstep = DeviceTrainStep(self, loss_fn, optimizer) \
+            if cfg is not None and device_step_enabled() and _plain_adam(optimizer) is not None else None
 
         def batch_loss(x, y):
+            if dstep is not None:
+                return _FusedStep(*loss_info(cfg.kind, dstep(x, y)), stepped=True)
             t = self.sample_t(x)
             if cfg is not None:
                 # same draws as base_sde.sample (sdes.py:37-49): eps = randn_like(x)

@@ -169,6 +169,21 @@ int dmip_loss_grad_f32(int in_dim, int out_dim, int n_hidden, const int* widths,
                        const float* eps_dev, const float* ic_target_dev, int64_t batch, float* grad_out_dev,
                        float* loss_out_dev, void* stream);
 
+/* The rest of a training step on the device (dmip_step.hip), so a whole step is a few launches:
+ * dmip_train_draws  the batch's diffusion times t (BaseClassDiffusionModel.sample_t, models/diffusion.py:
+ *                   48-58: debias = the truncated beta/var inverse-CDF sampler (sdes.py sample_vp_truncated_q
+ *                   restated), else uniform; + t_add with the t > T correction) and the forward-diffusion
+ *                   noise eps [batch][xdim] (sdes.py:37-49), from the chain-keyed generator
+ *                   (seed, sample index, stream_id)
+ * dmip_adam_step    torch.optim.Adam's update (amsgrad off, no weight decay; step = the step count after
+ *                   the increment) on the optimizer's own exp_avg / exp_avg_sq tensors, all parameter
+ *                   tensors (<= 16) in one launch */
+int dmip_train_draws(uint64_t seed, uint64_t stream_id, int64_t batch, int xdim, int debias, const dmip_vpsde* sde,
+                     double t_epsilon, float t_add, float* t_out_dev, float* eps_out_dev, void* stream);
+int dmip_adam_step(int n_tensors, float* const* params, const float* const* grads, float* const* exp_avg,
+                   float* const* exp_avg_sq, const int64_t* numel, double lr, double beta1, double beta2, double eps,
+                   int64_t step, void* stream);
+
 /* Non-zero when dmip_loss_grad has a kernel for this network shape. */
 int dmip_loss_grad_supported(int in_dim, int out_dim, int n_hidden, const int* widths, int xdim);
 

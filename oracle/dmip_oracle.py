@@ -225,6 +225,44 @@ def rng_uniform_words(seed, chain_ids, n_words, stream=0):
 
 
 # ------------------------------------------------------------------------------------------
+# Training-time draws -- models/diffusion.py:48-58 (sample_t), sdes.py:37-57 (sample, sample_debiasing_t)
+# ------------------------------------------------------------------------------------------
+def vp_truncated_q(u, beta_min=0.1, beta_max=20.0, t_epsilon=1e-3, T=1.0):
+    """Inverse CDF of q(t) ~ beta(t)/var(t) above t_epsilon, flat below (sdes.py:51-57 calls
+    sdeflow-light's sample_vp_truncated_q, which the reference does not vendor: restated from its
+    math in float64, parity unpinned). With B(t) = int_0^t beta: CDF(t) = t r(t_eps) below t_eps, and
+    t_eps r(t_eps) + log(e^B(t) - 1) - log(e^B(t_eps) - 1) above; normalised by its value at T."""
+    u = np.asarray(u, np.float64)
+    a, b, te = beta_max - beta_min, beta_min, t_epsilon
+    B = lambda t: 0.5 * a * t * t + b * t
+    r_te = (b + a * te) / (1.0 - np.exp(-B(te)))
+    A_te = np.log(np.expm1(B(te)))
+    Z = te * r_te + np.log(np.expm1(B(T))) - A_te
+    v = Z * u + A_te - te * r_te
+    Bu = np.where(v > 30, v, np.log1p(np.exp(np.minimum(v, 30))))
+    hi = (-b + np.sqrt(b * b + 2.0 * a * Bu)) / a
+    return np.where(u <= te * r_te / Z, Z / r_te * u, hi)
+
+
+def train_draws(seed, stream_id, batch, xdim, debias=True, beta_min=0.1, beta_max=20.0, t_epsilon=1e-3, T=1.0,
+                t_add=1e-4):
+    """dmip_train_draws restated: sample index b, generator (seed, b, stream_id); the first word gives
+    u = (w >> 8) 2^-24 and t = sample_t's draw (models/diffusion.py:50-57: q(u) + t_add, minus t_add
+    again above T; or t_add + u T, set to T - t_add above T); then two Box-Muller pairs give eps
+    (base_sde.sample's randn_like, sdes.py:41), the first xdim of them kept. Returns (t[batch], eps)."""
+    s = rng_init(seed, np.arange(batch, dtype=np.uint64), stream_id)
+    u = (rng_next(s) >> np.uint32(8)).astype(np.float64) * 2.0 ** -24
+    if debias:
+        t = vp_truncated_q(u, beta_min, beta_max, t_epsilon, T) + t_add
+        t = np.where(t > T, t - t_add, t)
+    else:
+        t = t_add + u * T
+        t = np.where(t > T, T - t_add, t)
+    eps = rng_normals(s, 4)[:, :xdim]
+    return t, eps
+
+
+# ------------------------------------------------------------------------------------------
 # A2/A8  Euler-Maruyama reverse-SDE loop -- models/diffusion.py:27-46, sdes.py:77-87
 # ------------------------------------------------------------------------------------------
 

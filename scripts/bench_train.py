@@ -1,9 +1,14 @@
-"""BASELINE config 5: PINNLoss training step of the linear CDE ([64]*3, batch 65,536) on one MI355X.
+"""BASELINE config 5: PINNLoss training step of the linear CDE ([64]*3, batch 65,536) on one MI355X,
+plus the exact-f32 engine at the reference configs' hidden_layers [512]*3.
 
-Times (HIP events on the launching stream) the fused loss+gradient kernel (dmip_loss_grad), the whole
-fused train step (sample_t + randn + kernel + Adam), the same step through torch autograd on the GPU
-(DMIP_TRAIN_FUSED=0), and the torch autograd step on the host CPU on a bounded batch. Prints one
-JSON line. Algorithmic flops per sample: 16.94 F, F = 17,280 (SURVEY.md §8a A14, W = 64).
+For each (width, precision) it times with HIP events on the launching stream:
+  * ms_loss_grad   the fused loss + gradient launch sequence alone (dmip_loss_grad / _f32),
+  * ms_device_step the whole step on the device (training.DeviceTrainStep: dmip_train_draws ->
+                   loss + gradients -> dmip_adam_step, no host synchronisation),
+  * ms_epoch_step  CDE.train_epoch's step (host t / eps draws, torch Adam, the reference's per-batch
+                   loss.item()), host-timed,
+and once, the same step through torch autograd on the GPU and on the host CPU (bounded batch).
+Algorithmic flops per sample: 16.94 F, F = 2 (5 W + 2 W^2 + 2 W). One JSON line.
     python scripts/bench_train.py [--batch 65536] [--steps 20] [--cpu-batch 4096]"""
 import argparse
 import importlib
@@ -12,11 +17,12 @@ import os
 import sys
 import time
 
-import numpy as np
 import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+
+PEAK = {"bf16": 2500.0, "fp32": 157.3}  # dense TFLOP/s (MI355X_MICROARCH.md)
 
 
 def main():
@@ -33,14 +39,9 @@ def main():
     torch.manual_seed(0)
     prob = pkg.LinearForwardProblem()
     lf = pkg.PINNLoss(prob.score_posterior, lam=1e-3, lam2=0.1, pde_loss="FPE", ic_metric="L2", pde_metric="L1")
-    m = pkg.CDE(2, 2, [64] * 3)
     B = a.batch
     x = torch.randn(B, 2, device=dev)
     y = x @ prob.A.to(dev).T + prob.b.to(dev) + 0.3 * torch.randn(B, 2, device=dev)
-    t = m.sample_t(x).detach()
-    eps = torch.randn_like(x)
-    cfg = tr.fused_config(m, lf)
-    assert cfg is not None
     st = torch.cuda.current_stream()
 
     def timed(fn, k):
@@ -53,25 +54,46 @@ def main():
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) / k
 
-    kern = lambda: tr.fused_loss_grad(m, lf, cfg, x, y, t, eps)
-    for _ in range(a.warmup):
-        kern()
-    ms_kernel = timed(kern, a.steps)
-
-    opt = torch.optim.Adam(m.sde.a.parameters(), lr=1e-4)
-
     def loader():
         yield x, y
-    step = lambda: m.train_epoch(opt, lf, loader)
-    for _ in range(a.warmup):
-        step()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
-    torch.cuda.synchronize()
-    ms_step = (time.perf_counter() - t0) * 1e3 / a.steps
 
+    rows = {}
+    for width, prec in ((64, "bf16"), (64, "fp32"), (512, "fp32")):
+        os.environ["DMIP_TRAIN_PRECISION"] = prec
+        m = pkg.CDE(2, 2, [width] * 3)
+        cfg = tr.fused_config(m, lf)
+        assert cfg is not None
+        t = m.sample_t(x).detach()
+        eps = torch.randn_like(x)
+        kern = lambda: tr.fused_loss_grad(m, lf, cfg, x, y, t, eps, precision=prec)
+        for _ in range(a.warmup):
+            kern()
+        ms_kernel = timed(kern, a.steps)
+        opt = torch.optim.Adam(m.sde.a.parameters(), lr=1e-4)
+        dstep = tr.DeviceTrainStep(m, lf, opt, precision=prec)
+        run = lambda: dstep(x, y)
+        for _ in range(a.warmup):
+            run()
+        ms_dev = timed(run, a.steps)
+        step = lambda: m.train_epoch(opt, lf, loader)
+        for _ in range(a.warmup):
+            step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            step()
+        torch.cuda.synchronize()
+        ms_epoch = (time.perf_counter() - t0) * 1e3 / a.steps
+        F = 2 * (5 * width + 2 * width * width + width * 2)
+        tf = 16.94 * F * B / (ms_kernel * 1e-3) / 1e12
+        rows[f"w{width}_{prec}"] = {"ms_loss_grad": ms_kernel, "ms_device_step": ms_dev, "ms_epoch_step": ms_epoch,
+                                    "device_step_samples_per_s": B / (ms_dev * 1e-3),
+                                    "loss_grad_tflops": tf, "frac_of_dense_peak": tf / PEAK[prec]}
+    os.environ.pop("DMIP_TRAIN_PRECISION", None)
+
+    m = pkg.CDE(2, 2, [64] * 3)
+    opt = torch.optim.Adam(m.sde.a.parameters(), lr=1e-4)
+    step = lambda: m.train_epoch(opt, lf, loader)
     os.environ["DMIP_TRAIN_FUSED"] = "0"
     for _ in range(2):
         step()
@@ -82,7 +104,6 @@ def main():
         step()
     torch.cuda.synchronize()
     ms_autograd = (time.perf_counter() - t0) * 1e3 / k_ag
-    os.environ["DMIP_TRAIN_FUSED"] = "1"
 
     cpu = None
     if not a.no_cpu:
@@ -100,21 +121,21 @@ def main():
             mc.train_epoch(optc, lf, loader_c)
         s = (time.perf_counter() - t0) / n_c
         cpu = {"value": a.cpu_batch / s, "unit": "samples/s", "cores": torch.get_num_threads(), "kind": "port",
-               "sample": f"torch autograd PINNLoss step on the host CPU, batch {a.cpu_batch}, {n_c} steps"}
+               "sample": f"torch autograd PINNLoss step ([64]*3) on the host CPU, batch {a.cpu_batch}, {n_c} steps"}
+    os.environ.pop("DMIP_TRAIN_FUSED", None)
 
-    F = 2 * (5 * 64 + 2 * 64 * 64 + 64 * 2)
-    flops = 16.94 * F * B
-    tflops = flops / (ms_kernel * 1e-3) / 1e12
+    head = rows["w64_bf16"]
     print(json.dumps({
         "metric": "PINNLoss train-step samples/sec (linear CDE [64]*3, BASELINE configs[4])",
-        "value": B / (ms_step * 1e-3), "unit": "samples/s", "n_gpus": 1, "steps": a.steps,
-        "ms_per_step": ms_step, "ms_loss_grad_kernel": ms_kernel, "ms_per_step_torch_autograd_gpu": ms_autograd,
+        "value": head["device_step_samples_per_s"], "unit": "samples/s", "n_gpus": 1, "steps": a.steps,
+        "ms_per_step": head["ms_device_step"], "ms_per_step_torch_autograd_gpu": ms_autograd,
         "higher_is_better": True, "dtype": "bf16 (split-bf16 primal streams)", "data": "synthetic",
-        "config": {"workload": "PINNLoss(FPE, L1; IC L2, lam 1e-3, lam2 0.1) train step", "batch": B,
-                   "hidden_layers": [64, 64, 64]},
-        "roofline": {"bound": "mfma", "achieved": tflops, "peak": 2500.0, "unit": "TFLOP/s",
-                     "frac": tflops / 2500.0, "flops_per_step": flops,
-                     "note": "algorithmic 16.94 F per sample (SURVEY A14); the kernel is latency-bound at this size"},
+        "config": {"workload": "PINNLoss(FPE, L1; IC L2, lam 1e-3, lam2 0.1) train step: draws + loss/grad + Adam",
+                   "batch": B, "hidden_layers": [64, 64, 64]},
+        "roofline": {"bound": "mfma", "achieved": head["loss_grad_tflops"], "peak": PEAK["bf16"], "unit": "TFLOP/s",
+                     "frac": head["frac_of_dense_peak"], "traffic": None,
+                     "note": "algorithmic 16.94 F per sample (SURVEY A14) over the loss+grad launches"},
+        "per_config": rows,
         "cpu_baseline": cpu,
     }))
 
