@@ -56,6 +56,21 @@ float bf2f(uint16_t b) {
   return f;
 }
 
+// fp16 images of the hidden and output layers (the engine's v_mfma_f32_32x32x16_f16 operands):
+// round to nearest even, subnormals kept, |v| <= 65504 (trained and random-init weights are far inside)
+uint16_t f2h(float f) {
+  const _Float16 h = (_Float16)f;
+  uint16_t u;
+  std::memcpy(&u, &h, 2);
+  return u;
+}
+
+float h2f(uint16_t u) {
+  _Float16 h;
+  std::memcpy(&h, &u, 2);
+  return (float)h;
+}
+
 // f32 A-fragment images for v_mfma_f32_16x16x4_f32 (dmip_surrogate.hip): k-step (q, r) of output
 // tile o, lane l = i + 16 g, holds M[16 o + i][16 q + 4 g + r]; stored [o][q][lane][r] (one float4
 // per lane per q). M(row, col) returns 0 outside the matrix.
@@ -275,9 +290,9 @@ int dmip_mlp_create(int in_dim, int out_dim, int n_hidden, const int* widths, in
   net->xdim = xdim;
   const int T = W / 32, KS = W / 16, L = n_hidden;
 
-  // ---- hidden W x W layers. Input in r-form (after a single tanh): A = bf16(-2c W),
+  // ---- hidden W x W layers (fp16 images). Input in r-form (after a single tanh): A = fp16(-2c W),
   // init = c b - 0.5 sum_k A. Input in t-form (the first W x W layer: layer 1's double tanh is
-  // emitted as the value itself, dmip_device.h act_t_twice): A = bf16(c W), init = c b.
+  // emitted as the value itself, dmip_device.h act_t_twice_pk_f16): A = fp16(c W), init = c b.
   std::vector<uint16_t> hid((size_t)(L - 1) * T * KS * 512);
   std::vector<float> bh((size_t)(L - 1) * T * 32);
   for (int li = 0; li < L - 1; ++li) {
@@ -289,9 +304,10 @@ int dmip_mlp_create(int in_dim, int out_dim, int n_hidden, const int* widths, in
     for (int r = 0; r < W; ++r) {
       double acc = 0.0;
       for (int k = 0; k < W; ++k) {
-        const uint16_t a = f2bf((float)((t_form ? 1.0 : -2.0) * kC * (double)Wl[(size_t)r * W + k]));
+        const float v = (float)((t_form ? 1.0 : -2.0) * kC * (double)Wl[(size_t)r * W + k]);
+        const uint16_t a = f2h(v);
         A[(size_t)r * W + k] = a;
-        acc += (double)bf2f(a);
+        acc += (double)h2f(a);
       }
       init[r] = (float)(kC * (double)bl[r] - (t_form ? 0.0 : 0.5 * acc));
     }
@@ -307,8 +323,8 @@ int dmip_mlp_create(int in_dim, int out_dim, int n_hidden, const int* widths, in
         for (int r = 0; r < 16; ++r) bh[((size_t)(li * T + rt) * 2 + h) * 16 + r] = init[rt * 32 + acc_row(r, h)];
   }
 
-  // ---- output layer: A = bf16(-2 W), init = b - 0.5 sum_k A (no tanh scale: raw drift a);
-  // t-form input (L == 1: directly after layer 1's double tanh): A = bf16(W), init = b
+  // ---- output layer (fp16 image): A = fp16(-2 W), init = b - 0.5 sum_k A (no tanh scale: raw
+  // drift a); t-form input (L == 1: directly after layer 1's double tanh): A = fp16(W), init = b
   const float* Wo = weights[L];
   const float* bo = biases[L];
   const bool out_t_form = L == 1;
@@ -317,9 +333,10 @@ int dmip_mlp_create(int in_dim, int out_dim, int n_hidden, const int* widths, in
   for (int d = 0; d < out_dim; ++d) {
     double acc = 0.0;
     for (int k = 0; k < W; ++k) {
-      const uint16_t a = f2bf((float)((out_t_form ? 1.0 : -2.0) * (double)Wo[(size_t)d * W + k]));
+      const float v = (float)((out_t_form ? 1.0 : -2.0) * (double)Wo[(size_t)d * W + k]);
+      const uint16_t a = f2h(v);
       Ao[(size_t)d * W + k] = a;
-      acc += (double)bf2f(a);
+      acc += (double)h2f(a);
     }
     init_o[d] = (float)((double)bo[d] - (out_t_form ? 0.0 : 0.5 * acc));
   }

@@ -22,6 +22,13 @@ __device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, const
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
+// the same 32x32x16 tile on fp16 operands; the 16-bit fragments live in bf16x8 registers either way
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ f32x16 mfma32h(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0,
+                                                0);
+}
+
 // ------------------------------------------------------------------------------------ RNG
 struct Rng {
   uint32_t s0, s1, s2, s3;
@@ -138,46 +145,67 @@ __device__ __forceinline__ float em_update(float x, float a, float xi, const Ste
 }
 
 // ---------------------------------------------------------------------------- activation
-// The kernels propagate r = 1/(1+exp(2z)) instead of tanh(z) = 1 - 2r; the "1 - 2r" is folded
+// Hidden layers propagate r = 1/(1+exp(2z)) instead of tanh(z) = 1 - 2r; the "1 - 2r" is folded
 // into the next layer on the host (weights -2W, bias b + sum_k W). The pre-activation arrives
 // already multiplied by 2*log2(e), so one layer's activation is exp2 + add + rcp.
 __device__ __forceinline__ float act_r(float zs) {
   return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(zs));
 }
-// tanh(tanh(z)) of the reference's first layer (nets.py:21-26 double Tanh), returned in t-form
-// (the value itself; the host packs the next layer for a t-form input). With e = exp(-2|z|) in
-// (0, 1], tanh|z| = (1 - e)/(1 + e) and tanh(tanh|z|) = (1 - e) q(e), q a degree-4 fit (max abs
-// error 1.7e-5 in f32 Horner, exact 0 at z = 0; bf16 rounding of the result is ~100x larger).
-// One transcendental + 5 FMAs + copysign: 32 issue cycles per unit against 40 for the two
-// exp + rcp stages (exp, fma, rcp, exp, fma, rcp) it replaces.
-__device__ __forceinline__ float act_t_twice(float zs) {
-  const float e = __builtin_amdgcn_exp2f(-__builtin_fabsf(zs));
-  float q = __builtin_fmaf(-0.17045435309410095f, e, 0.5245547890663147f);
-  q = __builtin_fmaf(q, e, -0.5390751957893372f);
-  q = __builtin_fmaf(q, e, -0.07747964560985565f);
-  q = __builtin_fmaf(q, e, 0.761600136756897f);
-  return __builtin_copysignf(__builtin_fmaf(-e, q, q), zs);
-}
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // two f32 -> one dword of two bf16 (v_cvt_pk_bf16_f32, round to nearest even; a in the low half).
 // Converting explicit pairs keeps the packed conversion without letting the SLP vectoriser also
 // fuse the neighbouring scalar FMAs into v_pk_fma_f32 (a measured anti-lever beside MFMAs).
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{a, b}, bf16x2));
 }
+__device__ __forceinline__ uint32_t cvt_pk_f16(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{a, b}, f16x2));
+}
 
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+// tanh(tanh(z)) of the reference's first layer (nets.py:21-26 double Tanh) for a PAIR of units,
+// returned in t-form (the value itself; the host packs the next layer for a t-form input) as an fp16
+// pair. With e = exp(-2|z|) in (0, 1], tanh|z| = (1 - e)/(1 + e) and tanh(tanh|z|) = (1 - e) q(e),
+// q a degree-4 fit (max abs error 1.7e-5, exact 0 at z = 0). e is computed in f32, the Horner
+// steps in packed fp16 (v_pk_fma_f16: two units per instruction), the signs of z moved in with one
+// v_perm + v_bfi: 24 issue cycles per unit against 34 for the same polynomial in scalar f32
+// (profiles/README.md, r2 variants). fp16 evaluation error <= ~5e-4 absolute, at the size of the
+// 16-bit rounding of the result itself.
+__device__ __forceinline__ uint32_t act_t_twice_pk_f16(float za, float zb) {
+  const f32x2 e32 = {__builtin_amdgcn_exp2f(-__builtin_fabsf(za)), __builtin_amdgcn_exp2f(-__builtin_fabsf(zb))};
+  const f16x2 e = __builtin_convertvector(e32, f16x2);
+  auto c = [](float v) { return f16x2{(_Float16)v, (_Float16)v}; };
+  f16x2 q = __builtin_elementwise_fma(e, c(-0.17045435309410095f), c(0.5245547890663147f));
+  q = __builtin_elementwise_fma(q, e, c(-0.5390751957893372f));
+  q = __builtin_elementwise_fma(q, e, c(-0.07747964560985565f));
+  q = __builtin_elementwise_fma(q, e, c(0.761600136756897f));
+  const f16x2 r = __builtin_elementwise_fma(-e, q, q);
+  const uint32_t sg = __builtin_amdgcn_perm(__float_as_uint(zb), __float_as_uint(za), 0x07000300u);
+  return (sg & 0x80008000u) | (__builtin_bit_cast(uint32_t, r) & 0x7FFF7FFFu);
+}
 
+// activate one 32x32 accumulator tile into the next layer's fp16 B fragments (lo: registers 0-7,
+// hi: registers 8-15). TWICE: layer 1's double tanh (t-form), else the r-form of a hidden layer.
+// CAST_ONLY: timing ablation (the pre-activation itself).
 template <bool TWICE, bool CAST_ONLY = false>
 __device__ __forceinline__ void act_pack(const f32x16& acc, bf16x8& lo, bf16x8& hi) {
-  auto act = [](float z) { return CAST_ONLY ? z : (TWICE ? act_t_twice(z) : act_r(z)); };
   u32x4 l, h;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    l[i] = cvt_pk_bf16(act(acc[2 * i]), act(acc[2 * i + 1]));
-    h[i] = cvt_pk_bf16(act(acc[8 + 2 * i]), act(acc[8 + 2 * i + 1]));
+    if constexpr (CAST_ONLY) {
+      l[i] = cvt_pk_f16(acc[2 * i], acc[2 * i + 1]);
+      h[i] = cvt_pk_f16(acc[8 + 2 * i], acc[8 + 2 * i + 1]);
+    } else if constexpr (TWICE) {
+      l[i] = act_t_twice_pk_f16(acc[2 * i], acc[2 * i + 1]);
+      h[i] = act_t_twice_pk_f16(acc[8 + 2 * i], acc[8 + 2 * i + 1]);
+    } else {
+      l[i] = cvt_pk_f16(act_r(acc[2 * i]), act_r(acc[2 * i + 1]));
+      h[i] = cvt_pk_f16(act_r(acc[8 + 2 * i]), act_r(acc[8 + 2 * i + 1]));
+    }
   }
   lo = __builtin_bit_cast(bf16x8, l);
   hi = __builtin_bit_cast(bf16x8, h);

@@ -74,18 +74,20 @@ __device__ __forceinline__ void lds_wait(bf16x8& guarded) {
   asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(guarded) : "i"(N));
 }
 
-template <int KS, int PF, int S = 0>
+template <int KS, int PF, bool F16, int S = 0>
 __device__ __forceinline__ void mfma_chain(lds_cptr a_lane, const bf16x8 (&H)[KS], f32x16& acc, bf16x8 (&a)[PF + 1]) {
   if constexpr (S < KS) {
     if constexpr (S + PF < KS) a[(S + PF) % (PF + 1)] = lds_read_b128<(S + PF) * 1024>(a_lane);
     constexpr int younger = (KS - 1 - S) < PF ? (KS - 1 - S) : PF;  // reads issued after fragment S
     lds_wait<younger>(a[S % (PF + 1)]);
-    acc = mfma32(a[S % (PF + 1)], H[S], acc);
-    mfma_chain<KS, PF, S + 1>(a_lane, H, acc, a);
+    if constexpr (F16) acc = mfma32h(a[S % (PF + 1)], H[S], acc);
+    else acc = mfma32(a[S % (PF + 1)], H[S], acc);
+    mfma_chain<KS, PF, F16, S + 1>(a_lane, H, acc, a);
   }
 }
 
-template <int KS, int PF = 3>
+// F16: fp16 operands (the engine's hidden and output layers), else bf16
+template <int KS, bool F16, int PF = 3>
 __device__ __forceinline__ void mfma_row_tile(const char* a_lane_g, const bf16x8 (&H)[KS], f32x16& acc) {
   const lds_cptr a_lane = (lds_cptr)a_lane_g;
   bf16x8 a[PF + 1];
@@ -93,19 +95,24 @@ __device__ __forceinline__ void mfma_row_tile(const char* a_lane_g, const bf16x8
   if constexpr (PF >= 2 && KS > 1) a[1] = lds_read_b128<1024>(a_lane);
   if constexpr (PF >= 3 && KS > 2) a[2] = lds_read_b128<2048>(a_lane);
   static_assert(PF >= 1 && PF <= 3, "prefetch depth");
-  mfma_chain<KS, PF>(a_lane, H, acc, a);
+  mfma_chain<KS, PF, F16>(a_lane, H, acc, a);
 }
 
 // ------------------------------------------------------------------- network evaluation engine
 // Evaluates NNET networks on one 32-chain tile per wave and sums their output layers into one
 // accumulator tile (rows = output dims; the host packers define the row maps).
+// Operand types: layer 1 is a bf16 MFMA over split-bf16 inputs (~fp32 chain state). The W x W hidden
+// layers and the output layer are fp16 MFMAs (v_mfma_f32_32x32x16_f16, the bf16 rate) over fp16
+// weights and fp16 activations in (-1, 1): 3 more mantissa bits than bf16 for the same issue, and
+// layer 1's double tanh runs in packed fp16 (act_t_twice_pk_f16, two units per instruction).
+// Measured against the all-bf16 engine on one box (profiles/README.md, r2 A/B): 1.5 % faster, and
+// the 512-chain smoke trajectory 7x closer to the exact oracle (3.5e-4 vs 2.4e-3).
+// Schedule: a layer's last tile is activated inside the next layer's first tile block (beside its
+// MFMAs over the other k-steps), and a ring tile's bias is read before the ring barrier, whose
+// compiler-visible lgkmcnt(0) covers it, so the first MFMA waits only for its own fragment.
 // DIAG (timing ablations only, never on the product path): bit 0 = no ring barrier/DMA,
-// bit 1 = hidden activations replaced by a bf16 cast, bit 2 = layer-1 activation replaced by a cast.
-// SPLIT: the two waves of a SIMD (waves w and w + NW/2) issue a hidden tile in complementary orders
-// (MFMAs first / previous tile's activation first) so one wave's VALU work runs beside the other's
-// MFMAs instead of both waves wanting the same pipe in lockstep.
-template <int W, int NL, int K1S, int NNET, int NW, int R, bool RES, bool CONSERVATIVE, int DIAG = 0,
-          bool SPLIT = false>
+// bit 1 = hidden activations replaced by a cast, bit 2 = layer-1 activation replaced by a cast.
+template <int W, int NL, int K1S, int NNET, int NW, int R, bool RES, bool CONSERVATIVE, int DIAG = 0>
 struct Engine {
   using L = Lay<W, NL, K1S, NNET, R, RES>;
   static constexpr int T = L::T;
@@ -152,6 +159,7 @@ struct Engine {
     } else {
       if constexpr (CONSERVATIVE) wait_vmcnt<0>();
       else wait_vmcnt<(R - 2) * PPW>();
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) the compiler sees: covers the bias reads
       lds_barrier();
       if constexpr (STATIC_RING) {
         ring_issue_at((k + R - 1) % L::NCT, (k + R - 1) % R);
@@ -173,61 +181,17 @@ struct Engine {
     return acc;
   }
 
-  // one W x W layer; the activation of tile rt-1 is issued in tile rt's block so it overlaps the
-  // MFMAs (the compiler interleaves them; explicit orders measured slower, profiles/README.md)
-  template <int NI, int LI>
-  __device__ __forceinline__ void hidden_layer(const bf16x8 (&Hin)[KS], bf16x8 (&Hout)[KS]) {
-    f32x16 pend;
-#pragma unroll
-    for (int rt = 0; rt < T; ++rt) {
-      const char* wb;
-      if constexpr (RES) {
-        // keep the resident weights in LDS: without this the compiler hoists every fragment
-        // read out of the step loop into (spilled) registers
-        asm volatile("" ::: "memory");
-        wb = lds + L::W_OFF + ((NI * (NL - 1) + LI) * T + rt) * L::CHUNK;
-      } else {
-        wb = chunk_sync((NI * (NL - 1) + LI) * T + rt);
-      }
-      if constexpr (SPLIT) {
-        if (w >= NW / 2) {  // activation first
-          if (rt > 0) act_pack<false, (DIAG & 2) != 0>(pend, Hout[2 * (rt - 1)], Hout[2 * (rt - 1) + 1]);
-          __builtin_amdgcn_sched_barrier(0);
-          f32x16 acc = bias_tile(L::BH_OFF + NI * L::BH_BYTES + ((LI * T + rt) * 2) * 64);
-          mfma_row_tile<KS>(wb + lane * 16, Hin, acc);
-          pend = acc;
-        } else {  // MFMAs first
-          f32x16 acc = bias_tile(L::BH_OFF + NI * L::BH_BYTES + ((LI * T + rt) * 2) * 64);
-          mfma_row_tile<KS>(wb + lane * 16, Hin, acc);
-          __builtin_amdgcn_sched_barrier(0);
-          if (rt > 0) act_pack<false, (DIAG & 2) != 0>(pend, Hout[2 * (rt - 1)], Hout[2 * (rt - 1) + 1]);
-          pend = acc;
-        }
-      } else {
-        f32x16 acc = bias_tile(L::BH_OFF + NI * L::BH_BYTES + ((LI * T + rt) * 2) * 64);
-        mfma_row_tile<KS>(wb + lane * 16, Hin, acc);
-        if (rt > 0) act_pack<false, (DIAG & 2) != 0>(pend, Hout[2 * (rt - 1)], Hout[2 * (rt - 1) + 1]);
-        pend = acc;
-      }
-    }
-    act_pack<false, (DIAG & 2) != 0>(pend, Hout[2 * (T - 1)], Hout[2 * (T - 1) + 1]);
+  // the last tile of a layer, activated inside the next layer's first tile block; TW: layer 1's
+  // double tanh (t-form, packed fp16) or a hidden layer's r-form
+  template <bool TW>
+  __device__ __forceinline__ void act_carry(const f32x16& carry, bf16x8 (&H)[KS]) {
+    act_pack<TW, (DIAG & (TW ? 4 : 2)) != 0>(carry, H[2 * (T - 1)], H[2 * (T - 1) + 1]);
   }
 
-  // hidden layers LI.. of net NI, then its output layer accumulated into `out`
-  template <int NI, int LI>
-  __device__ __forceinline__ void hidden_stack(bf16x8 (&Ha)[KS], bf16x8 (&Hb)[KS], f32x16& out) {
-    if constexpr (LI == NL - 1) {
-      asm volatile("" ::: "memory");
-      mfma_row_tile<KS>(lds + L::AO_OFF + NI * L::AO_BYTES + lane * 16, Ha, out);
-    } else {
-      hidden_layer<NI, LI>(Ha, Hb);
-      hidden_stack<NI, LI + 1>(Hb, Ha, out);
-    }
-  }
-
-  // layer 1 of net NI from the B1 operand (split-bf16 inputs), double tanh (nets.py:21-26)
+  // layer 1 of net NI from the B1 operand (split-bf16 inputs), double tanh (nets.py:21-26); returns
+  // the last tile's pre-activation
   template <int NI>
-  __device__ __forceinline__ void layer1(const bf16x8 (&B1)[K1S], bf16x8 (&H)[KS]) {
+  __device__ __forceinline__ f32x16 layer1(const bf16x8 (&B1)[K1S], bf16x8 (&H)[KS]) {
     f32x16 pend;
 #pragma unroll
     for (int rt = 0; rt < T; ++rt) {
@@ -241,14 +205,57 @@ struct Engine {
       if (rt > 0) act_pack<true, (DIAG & 4) != 0>(pend, H[2 * (rt - 1)], H[2 * (rt - 1) + 1]);
       pend = acc;
     }
-    act_pack<true, (DIAG & 4) != 0>(pend, H[2 * (T - 1)], H[2 * (T - 1) + 1]);
+    return pend;
+  }
+
+  // one W x W layer (fp16 MFMAs); the activation of tile rt-1 is issued in tile rt's block so it
+  // overlaps the MFMAs (the compiler interleaves them; explicit orders measured slower,
+  // profiles/README.md). Returns the last tile's pre-activation.
+  template <int NI, int LI, bool TW>
+  __device__ __forceinline__ f32x16 hidden_layer(bf16x8 (&Hin)[KS], const f32x16& carry, bf16x8 (&Hout)[KS]) {
+    f32x16 pend;
+#pragma unroll
+    for (int rt = 0; rt < T; ++rt) {
+      const int boff = L::BH_OFF + NI * L::BH_BYTES + ((LI * T + rt) * 2) * 64;
+      f32x16 acc;
+      const char* wb;
+      if constexpr (RES) {
+        // keep the resident weights in LDS: without this the compiler hoists every fragment
+        // read out of the step loop into (spilled) registers
+        asm volatile("" ::: "memory");
+        wb = lds + L::W_OFF + ((NI * (NL - 1) + LI) * T + rt) * L::CHUNK;
+        acc = bias_tile(boff);
+      } else {
+        acc = bias_tile(boff);
+        wb = chunk_sync((NI * (NL - 1) + LI) * T + rt);
+      }
+      if (rt == 0) act_carry<TW>(carry, Hin);
+      mfma_row_tile<KS, true>(wb + lane * 16, Hin, acc);
+      if (rt > 0) act_pack<false, (DIAG & 2) != 0>(pend, Hout[2 * (rt - 1)], Hout[2 * (rt - 1) + 1]);
+      pend = acc;
+    }
+    return pend;
+  }
+
+  // hidden layers LI.. of net NI, then its output layer accumulated into `out`
+  template <int NI, int LI, bool TW>
+  __device__ __forceinline__ void hidden_stack(bf16x8 (&Ha)[KS], bf16x8 (&Hb)[KS], const f32x16& carry,
+                                               f32x16& out) {
+    if constexpr (LI == NL - 1) {
+      asm volatile("" ::: "memory");
+      act_carry<TW>(carry, Ha);
+      mfma_row_tile<KS, true>(lds + L::AO_OFF + NI * L::AO_BYTES + lane * 16, Ha, out);
+    } else {
+      const f32x16 c2 = hidden_layer<NI, LI, TW>(Ha, carry, Hb);
+      hidden_stack<NI, LI + 1, false>(Hb, Ha, c2, out);
+    }
   }
 
   template <int NI>
   __device__ __forceinline__ void eval_net(const bf16x8 (&B1)[K1S], f32x16& out) {
     bf16x8 Ha[KS], Hb[KS];
-    layer1<NI>(B1, Ha);
-    hidden_stack<NI, 0>(Ha, Hb, out);
+    const f32x16 c1 = layer1<NI>(B1, Ha);
+    hidden_stack<NI, 0, true>(Ha, Hb, c1, out);
   }
 
   // sum over the networks of their outputs (+ the summed output bias)
@@ -373,8 +380,6 @@ constexpr int k1s_of(int slots) { return (slots + 15) / 16; }
 // does not depend on which wave runs it: results are bit-identical to an unsplit run.
 // STAMP: diagnostic build only (dmip_em_sample_stamps) -- per-wave cycle sums of the step phases
 // [layer 1 + B1, hidden layers, output layer + RNG + EM update], written to p.stamps.
-// TUNE (development variants): bit 0 = complementary tile order per wave half (Engine SPLIT),
-// bit 1 = s_setprio 1 for the second-dispatched wave half.
 template <int MODE, int W, int NL, int D, int M, int NW, int R, bool RES>
 struct SamplerLds {
   static constexpr int NNET = MODE == MODE_POSTERIOR ? 2 : 1;
@@ -392,7 +397,7 @@ struct Seg {
 };
 
 template <int MODE, int W, int NL, int D, int M, int NW, int R, bool RES, bool NOISE, bool STAMP = false,
-          int DIAG = 0, int TUNE = 0>
+          int DIAG = 0>
 __global__ void __launch_bounds__(NW * 64, (NW * 64 + 255) / 256)
 em_sampler_kernel(SamplerParams p) {
   using SL = SamplerLds<MODE, W, NL, D, M, NW, R, RES>;
@@ -411,10 +416,7 @@ em_sampler_kernel(SamplerParams p) {
   const int h = lane >> 5;
   const int yi = blockIdx.y;
 
-  Engine<W, NL, K1S, NNET, NW, R, RES, NOISE, DIAG, (TUNE & 1) != 0> eng{lds, {p.hidden, p.hidden2}, 0, w, lane};
-  if constexpr ((TUNE & 2) != 0) {
-    if (w >= NW / 2) __builtin_amdgcn_s_setprio(1);
-  }
+  Engine<W, NL, K1S, NNET, NW, R, RES, NOISE, DIAG> eng{lds, {p.hidden, p.hidden2}, 0, w, lane};
   {
     const size_t a1_stride = (size_t)L::T * K1S * 1024;
     const char* const a1[2] = {p.a1 + (p.a1_per_y ? yi * a1_stride : 0), p.a1_2};
@@ -858,8 +860,7 @@ static hipError_t launch_forward_t(const ForwardParams& p, hipStream_t st) {
   DMIP_SHAPES(X, MODE_CDIFFE, DMIP_NO_W512, 2, 23)
 
 // Development knob (not part of the ABI): DMIP_SAMPLER_VARIANT=10x runs the timing ablations
-// (DIAG = x) and 20x the tuning variants (TUNE = x) of the width-256 CDE sampler; see
-// profiles/README.md.
+// (DIAG = x) of the width-256 CDE sampler; see profiles/README.md.
 static int sampler_variant() {
   const char* e = getenv("DMIP_SAMPLER_VARIANT");
   return e ? atoi(e) : 0;
@@ -870,7 +871,7 @@ hipError_t launch_sampler(const SamplerParams& p_in, int mode, int width, int n_
   *supported = true;
   const int var = sampler_variant();
   if (mode == MODE_CDE && width == 256 && n_hidden == 3 && xdim == 3 &&
-      ((var >= 101 && var <= 107) || (var >= 201 && var <= 203))) {
+      var >= 101 && var <= 107) {
     const dim3 grid(sampler_wgs_per_y(em_sampler_kernel<MODE_CDE, 256, 3, 3, 0, 8, 4, false, false>, 512,
                                       p_in.n_chains, n_y, st),
                     (unsigned)n_y);
@@ -883,10 +884,6 @@ hipError_t launch_sampler(const SamplerParams& p_in, int mode, int width, int n_
   case 100 + d: hipLaunchKernelGGL((em_sampler_kernel<MODE_CDE, 256, 3, 3, 0, 8, 4, false, false, false, d>), grid, dim3(512), 0, st, p); break;
       DG(1) DG(2) DG(3) DG(4) DG(5) DG(6) DG(7)
 #undef DG
-#define TG(t) \
-  case 200 + t: hipLaunchKernelGGL((em_sampler_kernel<MODE_CDE, 256, 3, 3, 0, 8, 4, false, false, false, 0, t>), grid, dim3(512), 0, st, p); break;
-      TG(1) TG(2) TG(3)
-#undef TG
       default: break;
     }
     e = hipGetLastError();
