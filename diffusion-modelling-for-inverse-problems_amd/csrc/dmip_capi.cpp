@@ -557,6 +557,13 @@ static int em_sample_f32(int mode, const dmip_mlp* net0, const dmip_mlp* net1, c
   p.mean = a.mean;
   p.stdv = a.stdv;
   p.seed = a.seed;
+  p.err = status_word(dmip::stream_device(st));
+  if (!p.err) {
+    if (l1y) (void)hipFreeAsync(l1y, st);
+    return fail(DMIP_ERR_ALLOC, "device status word");
+  }
+  p.debug_flags = debug_no_handover();
+  p.spin_limit = p.debug_flags ? (1u << 10) : (1u << 22);
   bool ok = false;
   hipError_t e = dmip::launch_f32_sampler(p, mode, net0->width, net0->n_hidden, xdim, ydim, a.n_y, st, &ok);
   if (l1y) (void)hipFreeAsync(l1y, st);

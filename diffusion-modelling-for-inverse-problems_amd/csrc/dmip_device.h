@@ -211,6 +211,93 @@ __device__ __forceinline__ void act_pack(const f32x16& acc, bf16x8& lo, bf16x8& 
   hi = __builtin_bit_cast(bf16x8, h);
 }
 
+// ------------------------------------------------------------- balanced persistent schedule
+// The persistent samplers' work distribution (dmip_kernels.hip em_sampler_kernel, dmip_f32.h
+// f32_sampler_kernel): the tiles_y * S wave-steps of one y are cut into one equal segment of
+// C = ceil(tiles_y S / n_waves) steps per wave of the grid (McNaughton's wrap-around rule), so every
+// wave stays busy to the end whatever the chain count. A tile cut by a segment boundary runs its
+// first part at the START of the earlier wave's segment and its second part at the END of the next
+// wave's (order-safe since C >= S); its state goes through global memory with a release/acquire
+// flag. All waves of a workgroup run exactly C steps (an idle segment computes on a dummy tile), so
+// the weight ring's barriers stay paired. A chain's arithmetic does not depend on which wave runs it.
+// Segment kinds: 0 whole tile, 1 first part handed over, 2 second part taken over, 3 idle.
+struct Seg {
+  int job, s0, s1, kind;
+};
+
+struct WaveSchedule {
+  long long C, used;
+  int S, a_job, a_len, b_job, b_from, f_first, n_full, n_seg;
+
+  __device__ __forceinline__ WaveSchedule(long long tiles_y, int S_, long long n_waves, long long gw) {
+    S = S_;
+    C = S;
+    a_job = -1, a_len = 0, b_job = -1, b_from = 0, f_first = 0, n_full = 0;
+    if (tiles_y <= n_waves) {
+      if (gw < tiles_y) f_first = (int)gw, n_full = 1;
+    } else {
+      C = (tiles_y * S + n_waves - 1) / n_waves;  // > S
+      const long long lo = gw * C;
+      const long long hi = lo + C < tiles_y * S ? lo + C : tiles_y * S;
+      if (lo < hi) {
+        const int j_lo = (int)(lo / S), r_lo = (int)(lo % S);
+        const int j_hi = (int)(hi / S), r_hi = (int)(hi % S);
+        if (r_lo > 0) b_job = j_lo, b_from = r_lo;
+        if (r_hi > 0) a_job = j_hi, a_len = r_hi;
+        f_first = r_lo > 0 ? j_lo + 1 : j_lo;
+        n_full = j_hi - f_first > 0 ? j_hi - f_first : 0;
+      }
+    }
+    used = (long long)a_len + (long long)n_full * S + (b_job >= 0 ? S - b_from : 0);
+    n_seg = __builtin_amdgcn_readfirstlane((a_job >= 0) + n_full + (b_job >= 0) + (C > used));
+  }
+
+  // order: A, whole tiles, idle, B -- B must END at step C (the last wave's segment is short)
+  __device__ __forceinline__ Seg segment_raw(int k) const {
+    if (a_job >= 0) {
+      if (k == 0) return Seg{a_job, 0, a_len, 1};
+      --k;
+    }
+    if (k < n_full) return Seg{f_first + k, 0, S, 0};
+    k -= n_full;
+    if (C > used) {
+      if (k == 0) return Seg{-1, 0, (int)(C - used), 3};
+      --k;
+    }
+    return Seg{b_job, b_from, S, 2};
+  }
+
+  // wave-uniform by construction; said so, or a ring counter would be treated as divergent
+  __device__ __forceinline__ Seg segment(int k) const {
+    const Seg s = segment_raw(k);
+    return Seg{__builtin_amdgcn_readfirstlane(s.job), __builtin_amdgcn_readfirstlane(s.s0),
+               __builtin_amdgcn_readfirstlane(s.s1), __builtin_amdgcn_readfirstlane(s.kind)};
+  }
+};
+
+// consumer side of a hand-over: wait (bounded) for the producer's flag. Giving up is an error the
+// host sees through dmip_device_status (kErrHandover), never silently wrong chains: returns true
+// when the state never arrived (the caller then poisons the tile's output).
+__device__ __forceinline__ bool handover_wait(const unsigned* flag, unsigned spin_limit, unsigned* err, unsigned code,
+                                              int lane) {
+  bool lost = false;
+  for (unsigned spins = 0; __hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0u;) {
+    if (++spins > spin_limit) {
+      lost = true;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(8);
+  }
+  if (lost && lane == 0) __hip_atomic_store(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return lost;
+}
+
+// producer side: every lane's state stores are visible device-wide before the flag
+__device__ __forceinline__ void handover_publish(unsigned* flag, int lane, int debug_flags) {
+  __threadfence();
+  if (lane == 0 && !(debug_flags & 1)) __hip_atomic_store(flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // ------------------------------------------------------------------------ sync primitives
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {

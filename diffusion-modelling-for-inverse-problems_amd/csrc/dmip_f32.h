@@ -216,8 +216,10 @@ constexpr int kMaxHidden = 3;  // hidden layers compiled: 1..3 (bias staging bou
 //   MODE_CDIFFE     y_t = eps std(tau) + mean_weight(tau) y, a = net(x, y_t, tau)[:D]   (+ Langevin
 //                   corrector steps before each predictor step, as the bf16 kernel)
 // then mu = g a + 0.5 beta x, x <- x + delta mu + sqrt(delta) g xi (dmip_device.h em_update).
-// Work: each wave runs one 16-chain tile for all steps per round; the grid is at most one resident
-// wave set, and every wave of a workgroup runs the same number of rounds (ring barriers paired).
+// Work: the grid is at most one resident wave set; a y's 16-chain tiles are spread over its waves by
+// the balanced WaveSchedule of dmip_device.h (equal segments of C wave-steps, split tiles handed over
+// through global memory), so 100k chains cost 3.05 rounds of the GPU's capacity, not 4. Every lane
+// group of a chain holds the same state, so the hand-over stores all 64 lanes like the 16-bit kernel.
 template <int MODE, int W, int D, int M>
 struct SamplerCfg {
   static constexpr int NNET = MODE == SAMPLER_POSTERIOR ? 2 : 1;
@@ -264,18 +266,33 @@ __global__ void __launch_bounds__(Shape<W>::NW * 64, 1) f32_sampler_kernel(F32Sa
   const float* yobs = (const float*)(lds + L::YOBS);
 
   const int S = p.num_steps;
-  const long long tiles = (p.n_chains + 15) / 16;
-  const long long per_round = (long long)gridDim.x * NW;
-  const long long rounds = (tiles + per_round - 1) / per_round;
+  const long long tiles_y = (p.n_chains + 15) / 16;
+  const long long n_waves = (long long)gridDim.x * NW;  // waves sharing this y
+  const long long gw = (long long)blockIdx.x * NW + w;  // this wave among them
+  constexpr int XW = sampler_xfer_words(D);
+  const WaveSchedule sched(tiles_y, S, n_waves, gw);
   const size_t noise_step = (size_t)gridDim.y * p.n_chains * D;
 
-  for (long long rd = 0; rd < rounds; ++rd) {
-    const long long c_local = ((rd * gridDim.x + blockIdx.x) * NW + w) * 16 + j;
-    const bool valid = c_local < p.n_chains;
+  for (int sgi = 0; sgi < sched.n_seg; ++sgi) {
+    const Seg sg = sched.segment(sgi);
+    const long long c_local = (long long)(sg.job >= 0 ? sg.job : 0) * 16 + j;
+    const bool valid = sg.job >= 0 && c_local < p.n_chains;
     const long long c_rd = valid ? c_local : 0;
-    Rng rng = rng_init(p.seed, (uint64_t)(p.chain_offset + c_local), (uint64_t)yi);
+    Rng rng;
     float x[D];
-    {
+    bool lost = false;  // the hand-over never arrived: the tile's output is poisoned and reported
+    if (sg.kind == 2) {  // resume the tile the previous wave of the grid handed over
+      const size_t slot = (size_t)yi * n_waves + gw - 1;
+      lost = handover_wait(p.xflag + slot, p.spin_limit, p.err, kErrHandover, lane);
+      const float* src = p.xfer + slot * XW;
+#pragma unroll
+      for (int k = 0; k < D; ++k) x[k] = lost ? __builtin_nanf("") : src[k * 64 + lane];
+      rng.s0 = __float_as_uint(src[(D + 0) * 64 + lane]);
+      rng.s1 = __float_as_uint(src[(D + 1) * 64 + lane]);
+      rng.s2 = __float_as_uint(src[(D + 2) * 64 + lane]);
+      rng.s3 = __float_as_uint(src[(D + 3) * 64 + lane]);
+    } else {
+      rng = rng_init(p.seed, (uint64_t)(p.chain_offset + c_local), (uint64_t)yi);
       float n0[D];
       if constexpr (NOISE) {
         const float* src = p.noise + ((size_t)yi * p.n_chains + c_rd) * D;
@@ -288,7 +305,8 @@ __global__ void __launch_bounds__(Shape<W>::NW * 64, 1) f32_sampler_kernel(F32Sa
       for (int k = 0; k < D; ++k) x[k] = __fadd_rn(__fmul_rn(n0[k], p.stdv), p.mean);
     }
 
-    for (int i = 0; i < S; ++i) {
+    for (int i0 = sg.s0; i0 < sg.s1; ++i0) {
+      const int i = sg.kind == 3 ? 0 : i0;  // idle steps: a dummy tile at step 0, discarded
       const StepCoef cf = step_coef(i, S, p.T, p.bmin, p.bdiff);
       float v[C::NV0];
 #pragma unroll
@@ -369,11 +387,22 @@ __global__ void __launch_bounds__(Shape<W>::NW * 64, 1) f32_sampler_kernel(F32Sa
         x[k] = em_update(x[k], ak, xi[k], cf, p.delta, p.sqrt_delta);
       }
     }
-    if (valid && g == 0) {
+    if (sg.kind == 1) {  // hand the tile over to the next wave of the grid
+      const size_t slot = (size_t)yi * n_waves + gw;
+      float* dst = p.xfer + slot * XW;
+#pragma unroll
+      for (int k = 0; k < D; ++k) dst[k * 64 + lane] = x[k];
+      dst[(D + 0) * 64 + lane] = __uint_as_float(rng.s0);
+      dst[(D + 1) * 64 + lane] = __uint_as_float(rng.s1);
+      dst[(D + 2) * 64 + lane] = __uint_as_float(rng.s2);
+      dst[(D + 3) * 64 + lane] = __uint_as_float(rng.s3);
+      handover_publish(p.xflag + slot, lane, p.debug_flags);
+    } else if (sg.kind != 3 && valid && g == 0) {
       float* dst = p.x_out + ((size_t)yi * p.n_chains + c_local) * D;
 #pragma unroll
       for (int k = 0; k < D; ++k) dst[k] = x[k];
     }
+    (void)lost;
   }
   eng.finish();
 }
@@ -456,8 +485,16 @@ inline hipError_t launch_f32_sampler_t(const F32SamplerParams& p, int n_y, hipSt
   const long long cap = (tiles + NW - 1) / NW;
   if (g > cap) g = cap;
   if (g < 1) g = 1;
-  hipLaunchKernelGGL(kern, dim3((unsigned)g, (unsigned)n_y), dim3(NW * 64), 0, st, p);
-  return hipGetLastError();
+  // the balanced schedule's hand-over needs every workgroup of the grid resident at once: g is
+  // capped by the stream device's occupancy above
+  F32SamplerParams q = p;
+  char* buf = nullptr;
+  hipError_t e = alloc_handover((size_t)g * n_y * NW, D, st, &buf, &q.xfer, &q.xflag);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(kern, dim3((unsigned)g, (unsigned)n_y), dim3(NW * 64), 0, st, q);
+  e = hipGetLastError();
+  (void)hipFreeAsync(buf, st);
+  return e;
 }
 
 template <int MODE, int W, int D, int M>

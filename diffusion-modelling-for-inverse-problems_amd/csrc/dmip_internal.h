@@ -70,6 +70,11 @@ struct SamplerParams {
 // device status codes written by kernels into the per-device status word
 constexpr unsigned kErrHandover = 1u;
 
+// hand-over state of a split tile, per grid wave: x[D] + the xoshiro128** state, one word per lane
+constexpr int sampler_xfer_words(int D) { return (D + 4) * 64; }
+// zeroed hand-over buffers for `slots` grid waves (freed by the caller with hipFreeAsync(*buf))
+hipError_t alloc_handover(size_t slots, int d, hipStream_t st, char** buf, float** xfer, unsigned** xflag);
+
 struct ForwardParams {
   const char* hidden;
   const char* a1;             // [W/32][K1S] KiB, all inputs varying
@@ -196,6 +201,13 @@ struct F32SamplerParams {
   int num_steps;
   float T, bmin, bdiff, delta, sqrt_delta, mean, stdv;
   unsigned long long seed;
+  // balanced schedule (as SamplerParams): hand-over state and flags per y and grid wave, the device
+  // status word, the consumer's spin bound and the test hook (bit 0: producers never publish)
+  float* xfer;
+  unsigned int* xflag;
+  unsigned int* err;
+  unsigned int spin_limit;
+  int debug_flags;
 };
 
 struct F32ForwardParams {

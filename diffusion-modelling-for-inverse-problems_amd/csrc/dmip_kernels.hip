@@ -368,16 +368,10 @@ constexpr int k1s_of(int slots) { return (slots + 15) / 16; }
 // then mu = g a + 0.5 beta x, x <- x + delta mu + sqrt(delta) g xi.
 //
 // Work distribution (persistent, preemptive): the G = grid.x workgroups of a y -- at most as many as
-// the GPU holds at once -- share its 32-chain tiles. A tile is a job of S steps; the y's tiles * S
-// wave-steps are cut into G * NW equal segments of C = ceil(tiles S / (G NW)) steps (McNaughton's
-// wrap-around rule), one per wave, so every wave of every CU stays busy to the end: a chain count
-// that is not a multiple of the GPU's one-round capacity no longer costs a half-empty extra round.
-// A tile cut by a segment boundary runs its first part at the START of the earlier wave's segment
-// and its second part at the END of the next wave's (order-safe since C >= S); the state (x, RNG)
-// goes through global memory with a release/acquire flag (the consumer normally finds it set: the
-// first part ended C - S steps before it is needed). All waves of a workgroup run C steps (idle
-// steps compute on a dummy tile), keeping the weight ring's barriers paired. A chain's arithmetic
-// does not depend on which wave runs it: results are bit-identical to an unsplit run.
+// the GPU holds at once -- share its 32-chain tiles through the balanced WaveSchedule of
+// dmip_device.h (McNaughton's wrap-around rule, hand-over of split tiles through global memory):
+// every wave of every CU stays busy to the end, and a chain's arithmetic does not depend on which
+// wave runs it (bit-identical to an unsplit run).
 // STAMP: diagnostic build only (dmip_em_sample_stamps) -- per-wave cycle sums of the step phases
 // [layer 1 + B1, hidden layers, output layer + RNG + EM update], written to p.stamps.
 template <int MODE, int W, int NL, int D, int M, int NW, int R, bool RES>
@@ -387,13 +381,6 @@ struct SamplerLds {
   static constexpr int K1S = k1s_of(3 * NV + 2);
   using L = Lay<W, NL, K1S, NNET, R, RES>;
   static constexpr int TOTAL = L::TOTAL;
-};
-constexpr int sampler_xfer_words(int D) { return (D + 4) * 64; }  // x[D] + xoshiro128** state, per lane
-
-// segment of a wave's schedule: tile, first step, end step, kind (0 whole tile, 1 first part handed
-// over, 2 second part taken over, 3 idle)
-struct Seg {
-  int job, s0, s1, kind;
 };
 
 template <int MODE, int W, int NL, int D, int M, int NW, int R, bool RES, bool NOISE, bool STAMP = false,
@@ -437,39 +424,8 @@ em_sampler_kernel(SamplerParams p) {
   const long long n_waves = (long long)gridDim.x * NW;  // waves sharing this y
   const long long gw = (long long)blockIdx.x * NW + w;  // this wave among them
   constexpr int XW = sampler_xfer_words(D);
-  long long C = S;
-  int a_job = -1, a_len = 0, b_job = -1, b_from = 0, f_first = 0, n_full = 0;
-  if (tiles_y <= n_waves) {
-    if (gw < tiles_y) f_first = (int)gw, n_full = 1;
-  } else {
-    C = (tiles_y * S + n_waves - 1) / n_waves;  // > S
-    const long long lo = gw * C;
-    const long long hi = lo + C < tiles_y * S ? lo + C : tiles_y * S;
-    if (lo < hi) {
-      const int j_lo = (int)(lo / S), r_lo = (int)(lo % S);
-      const int j_hi = (int)(hi / S), r_hi = (int)(hi % S);
-      if (r_lo > 0) b_job = j_lo, b_from = r_lo;
-      if (r_hi > 0) a_job = j_hi, a_len = r_hi;
-      f_first = r_lo > 0 ? j_lo + 1 : j_lo;
-      n_full = j_hi - f_first > 0 ? j_hi - f_first : 0;
-    }
-  }
-  const long long used = (long long)a_len + (long long)n_full * S + (b_job >= 0 ? S - b_from : 0);
-  const int n_seg = __builtin_amdgcn_readfirstlane((a_job >= 0) + n_full + (b_job >= 0) + (C > used));
-  // order: A, whole tiles, idle, B -- B must END at step C (the last wave's segment is short)
-  auto segment = [&](int k) -> Seg {
-    if (a_job >= 0) {
-      if (k == 0) return Seg{a_job, 0, a_len, 1};
-      --k;
-    }
-    if (k < n_full) return Seg{f_first + k, 0, S, 0};
-    k -= n_full;
-    if (C > used) {
-      if (k == 0) return Seg{-1, 0, (int)(C - used), 3};
-      --k;
-    }
-    return Seg{b_job, b_from, S, 2};
-  };
+  const WaveSchedule sched(tiles_y, S, n_waves, gw);
+  const int n_seg = sched.n_seg;
 
   unsigned long long ph[3] = {0, 0, 0};
   unsigned long long clk0 = 0, rt0 = 0;
@@ -480,10 +436,7 @@ em_sampler_kernel(SamplerParams p) {
   const size_t noise_step = (size_t)gridDim.y * p.n_chains * D;
 
   for (int sgi = 0; sgi < n_seg; ++sgi) {
-  // wave-uniform by construction; say so, or the ring's chunk counter would be treated as divergent
-  const Seg s_ = segment(sgi);
-  const Seg sg{__builtin_amdgcn_readfirstlane(s_.job), __builtin_amdgcn_readfirstlane(s_.s0),
-               __builtin_amdgcn_readfirstlane(s_.s1), __builtin_amdgcn_readfirstlane(s_.kind)};
+  const Seg sg = sched.segment(sgi);
   const long long c_local = (long long)(sg.job >= 0 ? sg.job : 0) * 32 + (lane & 31);
   const bool valid = sg.job >= 0 && c_local < p.n_chains;
   const long long c_rd = valid ? c_local : 0;
@@ -492,16 +445,8 @@ em_sampler_kernel(SamplerParams p) {
   bool lost = false;  // the hand-over never arrived: the tile's output is poisoned and reported
   if (sg.kind == 2) {  // resume the tile the previous wave of the grid handed over
     const size_t slot = (size_t)yi * n_waves + gw - 1;
-    for (unsigned spins = 0; __hip_atomic_load(p.xflag + slot, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0u;) {
-      // bounded: never hang the GPU (the flag is normally set C - S steps early). Giving up is an
-      // error the host sees through dmip_device_status, never silently wrong chains.
-      if (++spins > p.spin_limit) {
-        lost = true;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(8);
-    }
-    if (lost && lane == 0) __hip_atomic_store(p.err, kErrHandover, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // bounded: never hang the GPU (the flag is normally set C - S steps early)
+    lost = handover_wait(p.xflag + slot, p.spin_limit, p.err, kErrHandover, lane);
     const float* src = p.xfer + slot * XW;
 #pragma unroll
     for (int k = 0; k < D; ++k) x[k] = lost ? __builtin_nanf("") : src[k * 64 + lane];
@@ -603,9 +548,7 @@ em_sampler_kernel(SamplerParams p) {
     dst[(D + 1) * 64 + lane] = __uint_as_float(rng.s1);
     dst[(D + 2) * 64 + lane] = __uint_as_float(rng.s2);
     dst[(D + 3) * 64 + lane] = __uint_as_float(rng.s3);
-    __threadfence();  // every lane's state is visible device-wide before the flag
-    if (lane == 0 && !(p.debug_flags & 1))
-      __hip_atomic_store(p.xflag + slot, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    handover_publish(p.xflag + slot, lane, p.debug_flags);
   } else if (sg.kind != 3 && valid && h == 0) {
     float* dst = p.x_out + ((size_t)yi * p.n_chains + c_local) * D;
 #pragma unroll
@@ -797,12 +740,15 @@ static unsigned sampler_wgs_per_y(Kern kern, int nthreads, long long n_chains, i
 
 // the hand-over buffers of a launch: per y and grid wave, the state words and a flag (zeroed)
 static hipError_t with_xfer(SamplerParams& p, const dim3& grid, int nw, int d, hipStream_t st, char** buf) {
-  const size_t slots = (size_t)grid.x * grid.y * nw;
+  return alloc_handover((size_t)grid.x * grid.y * nw, d, st, buf, &p.xfer, &p.xflag);
+}
+
+hipError_t alloc_handover(size_t slots, int d, hipStream_t st, char** buf, float** xfer, unsigned** xflag) {
   const size_t state_bytes = slots * sampler_xfer_words(d) * sizeof(float);
   hipError_t e = hipMallocAsync((void**)buf, state_bytes + slots * sizeof(unsigned), st);
   if (e != hipSuccess) return e;
-  p.xfer = (float*)*buf;
-  p.xflag = (unsigned*)(*buf + state_bytes);
+  *xfer = (float*)*buf;
+  *xflag = (unsigned*)(*buf + state_bytes);
   // state and flags zeroed: nothing in the buffer is ever uninitialised memory
   return hipMemsetAsync(*buf, 0, state_bytes + slots * sizeof(unsigned), st);
 }

@@ -51,6 +51,11 @@ constexpr int OUT = D;          // CDE drift
 constexpr int NWV = DMIP_TRAIN_NWV;
 constexpr bool GACC_GLOBAL = NWV > 2;
 constexpr int NS = 16;          // samples per tile
+// row stride (bf16 elements) of the per-wave transposed scratch [unit][sample]: 16 samples padded
+// to 24 (48 bytes), so put_t's four lane groups (rows 4 apart) land on disjoint banks (row offsets
+// 0 / 48 / 32 / 16 banks) and tread's 16-byte rows stay aligned and conflict-free (12-bank steps);
+// unpadded (32 bytes) groups 0/2 and 1/3 collided: ~75 % of LDS-active cycles were bank conflicts
+constexpr int RS = 24;
 constexpr int NSTREAM = 8;      // P, V, C, E0, E1, E00, E01, E11
 static_assert(W == 64 && D == 2, "compiled for the linear problem's width-64 CDE");
 static_assert(3 * IN + 2 <= 32, "layer-1 split operand fits one k-step");
@@ -74,7 +79,7 @@ struct TL {
   static constexpr int WAVE = COL + D * W * 4;
   static constexpr int GACC = 0;                         // per wave: fp32 gradient partial (param order, LDS mode)
   static constexpr int SCR = GACC_GLOBAL ? 0 : ((PART * 4 + 15) / 16) * 16;  // per wave: 6 transposed [64][16] bf16
-  static constexpr int WAVE_BYTES = SCR + 6 * W * NS * 2;
+  static constexpr int WAVE_BYTES = SCR + 6 * W * RS * 2;
   static constexpr int TOTAL = WAVE + NWV * WAVE_BYTES;
   static_assert(TOTAL <= 160 * 1024, "LDS budget");
 };
@@ -122,7 +127,7 @@ __device__ __forceinline__ void put_t(__bf16* scr, const f32x4 (&z)[4], int g, i
 #pragma unroll
   for (int R = 0; R < 4; ++R)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) scr[(16 * R + 4 * g + r) * NS + c16] = (__bf16)z[R][r];
+    for (int r = 0; r < 4; ++r) scr[(16 * R + 4 * g + r) * RS + c16] = (__bf16)z[R][r];
 }
 
 __device__ __forceinline__ void pack_b(const f32x4 (&z)[4], bf16x8 (&b)[2]) {
@@ -161,7 +166,7 @@ __device__ __forceinline__ f32x4 mm3(const bf16x8& a0, const bf16x8& a1, const b
 // the 32x32x16 operand of a sample-contracted product: lane (i, hh) reads row (row0 + i), samples 8hh..8hh+7
 __device__ __forceinline__ bf16x8 tread(const __bf16* scr, int row, bool ok, int hh) {
   if (!ok) return bf16x8{};
-  return *(const bf16x8*)(scr + row * NS + 8 * hh);
+  return *(const bf16x8*)(scr + row * RS + 8 * hh);
 }
 
 // The shared part of the LDS image (weight fragments, biases, layer-1 columns), packed ONCE per
@@ -266,7 +271,7 @@ __global__ void __launch_bounds__(NWV * 64, 1) loss_grad_kernel(TrainParams p) {
   char* wave_base = lds + L::WAVE + w * L::WAVE_BYTES;
   float* gacc = GACC_GLOBAL ? p.partials + ((size_t)blockIdx.x * NWV + w) * L::PART : (float*)(wave_base + L::GACC);
   __bf16* scr = (__bf16*)(wave_base + L::SCR);
-  auto S_ = [&](int k) { return scr + k * W * NS; };
+  auto S_ = [&](int k) { return scr + k * W * RS; };
 
   f32x4 bbar[NL > 1 ? NL - 1 : 1][4];  // per-lane bias-gradient partials of the hidden W x W layers
 #pragma unroll
@@ -555,7 +560,7 @@ __global__ void __launch_bounds__(NWV * 64, 1) loss_grad_kernel(TrainParams p) {
 #pragma unroll
           for (int S = 0; S < 3; ++S)
 #pragma unroll
-            for (int o = 0; o < OUT; ++o) S_(S)[o * NS + c16] = (__bf16)ab[S][o];
+            for (int o = 0; o < OUT; ++o) S_(S)[o * RS + c16] = (__bf16)ab[S][o];
 #pragma unroll
           for (int o = 0; o < OUT; ++o) bobar[o] += abP[o] + abC[o];
         }
@@ -621,8 +626,8 @@ __global__ void __launch_bounds__(NWV * 64, 1) loss_grad_kernel(TrainParams p) {
 #pragma unroll
           for (int S = 0; S < 3; ++S) {
 #pragma unroll
-            for (int k = 0; k < IN; ++k) S_(3 + S)[k * NS + c16] = (__bf16)us[S][k];
-            S_(3 + S)[IN * NS + c16] = (__bf16)(S == 1 ? 0.0f : 1.0f);
+            for (int k = 0; k < IN; ++k) S_(3 + S)[k * RS + c16] = (__bf16)us[S][k];
+            S_(3 + S)[IN * RS + c16] = (__bf16)(S == 1 ? 0.0f : 1.0f);
           }
         }
       } else if (li >= 1) {

@@ -38,8 +38,10 @@ typedef enum { DMIP_INPUT_X_Y_T = 0, DMIP_INPUT_X_T = 1 } dmip_input_layout;
 typedef enum { DMIP_ACT_TANH_TWICE_FIRST = 0, DMIP_ACT_TANH = 1 } dmip_act;
 
 /* Arithmetic of the network GEMMs; the chain state, the schedule and the SDE update are fp32 in both.
- *   DMIP_PREC_BF16  bf16 MFMA operands, fp32 accumulation (layer 1 takes its inputs as split hi+lo
- *                   bf16, i.e. ~fp32); tanh by exp2 + rcp. The throughput mode (BASELINE headline).
+ *   DMIP_PREC_BF16  16-bit MFMA operands, fp32 accumulation: layer 1 is a bf16 MFMA over split hi+lo
+ *                   bf16 inputs (~fp32), the hidden and output layers fp16 MFMAs over fp16 weights and
+ *                   activations (3 more mantissa bits than bf16 at the same rate); tanh by exp2 + rcp,
+ *                   layer 1's double tanh in packed fp16. The throughput mode (BASELINE headline).
  *   DMIP_PREC_F32   exact f32: every product and sum in f32 (v_mfma_f32_16x16x4_f32, an fmaf chain),
  *                   libm-accurate tanh -- the reference's own arithmetic (nets.py:32-35 in fp32).
  *                   The parity mode; ~1/6 of the bf16 throughput. Same RNG stream per chain as bf16,
@@ -67,7 +69,8 @@ typedef struct dmip_mlp dmip_mlp;
  *   widths       L hidden widths (all equal; 64, 128 or 256 compiled)
  *   weights[i]   layer i weight, i = 0..L (L+1 linear layers)
  *   biases[i]    layer i bias
- * The handle owns packed device copies (bf16 MFMA fragments in the kernels' layouts). */
+ * The handle owns packed device copies (16-bit MFMA fragments in the kernels' layouts, and the exact-f32
+ * images of the DMIP_PREC_F32 kernels). */
 int dmip_mlp_create(int in_dim, int out_dim, int n_hidden, const int* widths, int act_mode, int input_layout,
                     int xdim, const float* const* weights, const float* const* biases, dmip_mlp** out);
 

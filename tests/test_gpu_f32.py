@@ -271,3 +271,36 @@ def test_posterior_parity_both_precisions(dmip, golden, tag):
     assert max(b["ks_draws"]["stat"]) < b["ks_draws"]["crit"], b
     assert all(s <= 5 * n for s, n in zip(b["w1_draws"]["stat"], b["w1_draws"]["null"])), b
     assert b["sliced_w1_draws"]["stat"] <= 5 * b["sliced_w1_draws"]["null"], b
+
+
+@pytest.mark.parametrize("cls,W,n", [("CDE", 256, 70001), ("CDE", 512, 40001), ("PosteriorDiffusionEstimator", 256, 70001),
+                                     ("CDiffE", 256, 70001)])
+def test_f32_balanced_schedule_matches_unsplit_runs(dmip, cls, W, n):
+    """Chain counts above the f32 engine's one-round capacity (256 CUs x 8 waves x 16 chains at width
+    256, half that at 512) split tiles between waves (the balanced WaveSchedule, state handed over
+    through global memory). Every chain equals a launch small enough to run each tile whole."""
+    torch.manual_seed(W + n)
+    m = getattr(dmip, cls)(3, 23, [W] * 3)
+    y = torch.from_numpy(np.random.default_rng(5).uniform(0, 1, 23).astype(np.float32)).to(DEV)
+    S = 6
+    full = m.sample_device(y, n, S, seed=11, precision="fp32")[0]
+    for lo in (0, n // 2 + 5, n - 333):
+        part = m.sample_device(y, 333, S, seed=11, chain_offset=lo, precision="fp32")[0]
+        assert torch.equal(full[lo:lo + 333], part), lo
+    assert torch.isfinite(full).all()
+
+
+def test_f32_handover_timeout_is_reported_not_silent(dmip, golden, monkeypatch):
+    """DMIP_DEBUG_NO_HANDOVER=1 in the f32 engine: consumers give up, the chains of the split tiles come
+    out NaN and the device status raises; a clean run afterwards reports nothing."""
+    m = _cde(dmip, "scat", golden("ckpt_scat.npz"))
+    y = torch.from_numpy(golden("data_scat.npz")["y_test"][0]).to(DEV)
+    monkeypatch.setenv("DMIP_DEBUG_NO_HANDOVER", "1")
+    x = m.sample_device(y, 50000, 4, seed=1, precision="fp32")
+    with pytest.raises(RuntimeError, match="hand-over"):
+        dmip._lib.device_status(x.device)
+    assert torch.isnan(x).any() and torch.isfinite(x).any()
+    monkeypatch.delenv("DMIP_DEBUG_NO_HANDOVER")
+    x = m.sample_device(y, 50000, 4, seed=1, precision="fp32")
+    dmip._lib.device_status(x.device)
+    assert torch.isfinite(x).all()
