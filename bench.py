@@ -65,6 +65,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fp32", action="store_true", help="skip the exact-f32 run beside the headline")
     ap.add_argument("--fp32-steps", type=int, default=2)
+    ap.add_argument("--no-other-configs", action="store_true",
+                    help="skip the one-GPU runs of BASELINE configs 3-5 and the reference width reported beside the headline")
     ap.add_argument("--master-port", type=int, default=29511)
     ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)  # CPU/gloo launcher test only
     return ap.parse_args()
@@ -276,6 +278,79 @@ def timed(wl, steps, dist, world, dev, seed0=0, **over):
     return elapsed, launch_ms, x
 
 
+def other_configs(args, pkg, lib, dev):
+    """The other BASELINE configurations on this GPU, timed beside the headline so the driver observes
+    them (each: one warm-up launch, then timed launches with HIP events): configs[2] CDiffE
+    predictor-corrector (the per-GPU share of 1M chains over 8 GPUs), configs[3] DPS (256k samples),
+    configs[4] the PINNLoss training step (whole step on the device), and the reference configs'
+    own width [512]*3 for the CDE sampler. Not the headline; errors are reported, not raised."""
+    import copy
+    import torch
+    out = {}
+
+    def sampler(name, workload, chains, reps, **kw):
+        try:
+            a = copy.copy(args)
+            a.workload, a.chains, a.chains_total = workload, chains, 0
+            for k, v in kw.items():
+                setattr(a, k, v)
+            wl = Workload(a, pkg, dev, 0, 1)
+            if workload == "cde" and kw.get("width"):
+                torch.manual_seed(0)
+                wl.model = pkg.CDE(XDIM, YDIM, [kw["width"]] * NH)
+                wl.model.sde.a.to(dev)
+                wl.flops_sample_step = flops_per_sample_step(w=kw["width"])
+                wl.kernel, wl.workload = f"em_sampler_kernel<0,{kw['width']},3,3,...>", "CDE at the reference width"
+                wl.weights = "random-init"
+            wl.step(3000)
+            el, lm, x = timed(wl, reps, None, 1, dev, seed0=3100)
+            lib.device_status(dev)
+            ach = wl.flops_sample_step * a.num_steps * wl.n_local / (lm * 1e-3) / 1e12
+            out[name] = {"workload": wl.workload, "chains": wl.n_local, "sde_steps": a.num_steps,
+                         "value": wl.n_local * reps / el, "unit": "samples/s", "launch_ms": lm,
+                         "roofline": {"achieved": ach, "peak": wl.peak, "unit": "TFLOP/s", "frac": ach / wl.peak},
+                         "kernel": wl.kernel, "weights": wl.weights, "finite": bool(torch.isfinite(x).all())}
+        except Exception as e:  # noqa: BLE001 -- reported in the line, never fatal to the headline
+            out[name] = {"error": f"{type(e).__name__}: {e}"}
+
+    sampler("config3_cdiffe_pc_per_gpu", "cdiffe-pc", 125000, 2)
+    sampler("config4_dps", "dps", 262144, 1)
+    sampler("cde_reference_width_512", "cde", 100000, 2, width=512)
+    try:
+        tr = importlib.import_module(PKG + ".training")
+        torch.manual_seed(0)
+        prob = pkg.LinearForwardProblem()
+        lf = pkg.PINNLoss(prob.score_posterior, lam=1e-3, lam2=0.1, pde_loss="FPE", ic_metric="L2", pde_metric="L1")
+        m = pkg.CDE(2, 2, [64] * 3)
+        B = 65536
+        xb = torch.randn(B, 2, device=dev)
+        yb = xb @ prob.A.to(dev).T + prob.b.to(dev) + 0.3 * torch.randn(B, 2, device=dev)
+        opt = torch.optim.Adam(m.sde.a.parameters(), lr=1e-4)
+        step = tr.DeviceTrainStep(m, lf, opt, precision="bf16")
+        for _ in range(3):
+            step(xb, yb)
+        st = torch.cuda.current_stream(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record(st)
+        K = 20
+        for _ in range(K):
+            out_loss = step(xb, yb)
+        e1.record(st)
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / K
+        F = 2 * (5 * 64 + 2 * 64 * 64 + 64 * 2)
+        ach = 16.94 * F * B / (ms * 1e-3) / 1e12
+        out["config5_pinn_train_step"] = {
+            "workload": "PINNLoss train step, linear CDE [64]*3, batch 65536: t/eps draws + fused loss/grad + Adam",
+            "value": B / (ms * 1e-3), "unit": "samples/s", "ms_per_step": ms,
+            "roofline": {"achieved": ach, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": ach / PEAK_BF16_TFLOPS},
+            "loss_finite": bool(torch.isfinite(out_loss).all())}
+    except Exception as e:  # noqa: BLE001
+        out["config5_pinn_train_step"] = {"error": f"{type(e).__name__}: {e}"}
+    return out
+
+
 def main_worker(args):
     import torch
     import torch.distributed as dist
@@ -305,7 +380,7 @@ def main_worker(args):
     value = wl.n_total * args.steps / elapsed
     flops_launch = wl.flops_sample_step * S * wl.n_local
     achieved = flops_launch / (launch_ms * 1e-3) / 1e12
-    dtype = "bf16" if (args.workload != "dps" and args.precision == "bf16") else "f32"
+    dtype = "fp16" if (args.workload != "dps" and args.precision == "bf16") else "f32"
     line = {
         "metric": "posterior samples/sec (1000-step reverse SDE)",
         "value": value,
@@ -322,11 +397,13 @@ def main_worker(args):
         "config": {"workload": wl.workload, "xdim": XDIM, "ydim": YDIM, "hidden_layers": [WIDTH] * NH,
                    "sde_steps": S, "chains_per_gpu": wl.n_local, "chains_total": wl.n_total,
                    "parallelism": f"sample-parallel x{world}" + (" + RCCL all_gather" if world > 1 else ""),
-                   "arith": ("bf16 MFMA operands, fp32 accumulate; fp32 chain state / SDE update" if dtype == "bf16"
+                   "arith": ("16-bit MFMA operands (layer 1: bf16 over split hi+lo inputs, ~fp32; hidden and output "
+                             "layers: fp16 weights and activations), fp32 accumulate; fp32 chain state / SDE update"
+                             if dtype == "fp16"
                              else "exact f32 MFMA (v_mfma_f32_16x16x4_f32); fp32 chain state / SDE update")},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": wl.peak, "unit": "TFLOP/s",
                      "frac": achieved / wl.peak,
-                     "traffic": pmc_traffic() if (args.workload == "cde" and dtype == "bf16") else None,
+                     "traffic": pmc_traffic() if (args.workload == "cde" and dtype == "fp16") else None,
                      "kernel": wl.kernel, "launch_ms": launch_ms, "flops_per_launch": flops_launch},
     }
     rep = None
@@ -350,6 +427,8 @@ def main_worker(args):
                              "frac": a32 / PEAK_F32_TFLOPS},
                 "ks_vs_ref": ks_field(rep32), "w1_vs_ref": w1_field(rep32),
                 "parity": {"pass": rep32["pass"]} if rep32 else None}
+    if rank == 0 and world == 1 and args.workload == "cde" and not args.no_other_configs:
+        line["other_configs"] = other_configs(args, pkg, lib, dev)
     if rank == 0 and world == 1 and args.workload == "cde" and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(S, args.cpu_chains)
     if rank == 0:
