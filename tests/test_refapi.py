@@ -51,3 +51,28 @@ def test_reference_drivers_import_against_shim(shim_path, dmip, script, monkeypa
     assert ns["utils"].get_model_from_args is dmip.get_model_from_args
     if "CDE" in ns:
         assert ns["CDE"] is dmip.CDE
+
+
+def test_reference_linear_train_runs_through_shim(shim_path, dmip, monkeypatch, tmp_path):
+    """Not just import: the reference's own `train` (main_diffusion_linear.py:19-51) executes through the
+    shim -- its loader, `model.train_epoch`, SummaryWriter scalars and the checkpoint -- on a CPU model
+    (the autograd path; the HIP path of the same train_epoch is tests/test_gpu_drivers.py)."""
+    path = os.path.join(REF, "main_diffusion_linear.py")
+    if not os.path.exists(path):
+        pytest.skip("reference checkout not present (GPU box)")
+    import torch
+    monkeypatch.chdir(REF)
+    ns = runpy.run_path(path, run_name="not_main")
+    torch.manual_seed(0)
+    m = dmip.CDE(2, 2, [16] * 2)
+    m.sde.a.to("cpu")
+    f = dmip.LinearForwardProblem()
+    xs = torch.randn(300, 2)
+    ys = f(xs)
+    opt = torch.optim.Adam(m.sde.a.parameters(), lr=1e-3)
+    loss_fn = dmip.PINNLoss(f.score_posterior, lam=1e-3, lam2=0.1, pde_loss="FPE", ic_metric="L2", pde_metric="L1")
+    out = ns["train"](m, opt, loss_fn, vars(f), str(tmp_path / "ckpt"), str(tmp_path / "log"), 2, 100, xs, ys)
+    assert out is m
+    sd = torch.load(tmp_path / "ckpt" / "current_model.pt", weights_only=True)
+    assert set(sd) == {"0.weight", "0.bias", "3.weight", "3.bias", "5.weight", "5.bias"}
+    assert all(torch.isfinite(v).all() for v in sd.values())
