@@ -17,16 +17,17 @@ namespace gemm {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int BM = 64, BN = 64, KB = 16, PAD = 4;
-constexpr int NT = 256;  // 4 waves: 2 x 2 wave tiles of 32 x 32 (2 x 2 MFMA tiles of 16 x 16 each)
+constexpr int KB = 16;
+constexpr int NT = 256;  // 4 waves: 2 x 2 wave tiles
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
 // epilogue of one output element (m, n) from the accumulated value v
-__device__ __forceinline__ void epilogue(const GemmParams& p, long long m, int n, float v) {
-  switch (p.epi) {
+template <int EPI>
+__device__ __forceinline__ void epilogue_k(const GemmParams& p, long long m, int n, float v) {
+  switch (EPI) {
     case GEMM_EPI_NONE:
       p.c[m * p.ldc + n] = v;
       break;
@@ -58,53 +59,75 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, long long m, int n
   }
 }
 
+__device__ __forceinline__ void epilogue(const GemmParams& p, long long m, int n, float v) {
+  switch (p.epi) {
+    case GEMM_EPI_NONE: epilogue_k<GEMM_EPI_NONE>(p, m, n, v); break;
+    case GEMM_EPI_BIAS: epilogue_k<GEMM_EPI_BIAS>(p, m, n, v); break;
+    case GEMM_EPI_BIAS_TANH: epilogue_k<GEMM_EPI_BIAS_TANH>(p, m, n, v); break;
+    case GEMM_EPI_BIAS_TANH2: epilogue_k<GEMM_EPI_BIAS_TANH2>(p, m, n, v); break;
+    case GEMM_EPI_MUL_AUX: epilogue_k<GEMM_EPI_MUL_AUX>(p, m, n, v); break;
+    case GEMM_EPI_WGRAD: epilogue_k<GEMM_EPI_WGRAD>(p, m, n, v); break;
+    default: break;
+  }
+}
+
 // C (M x N) = A (M x K) B (K x N) with A(m, k) = TA ? A[k lda + m] : A[m lda + k] and
 // B(k, n) = TB ? B[n ldb + k] : B[k ldb + n]. grid.z > 1: split-K partials (raw sums) into p.part.
-template <bool TA, bool TB>
+// Tile T x T (T = 64 or 128), 4 waves as 2 x 2 wave tiles of T/2 x T/2, i.e. (T/32)^2 MFMA tiles of
+// 16 x 16 per wave; KB = 16 k per LDS slice, double-buffered with the next slice's global loads in
+// flight during the MFMAs. Every output element accumulates over k in the same order whatever T, so
+// both tile sizes give bit-identical results (and the split-K boundaries are multiples of KB).
+// LDS rows are padded to a stride of 16 banks mod 64, so the four lane groups g of an operand read
+// hit disjoint banks. T = 128 quarters the global and LDS traffic per flop of the 64 tile: the
+// training GEMMs at width 512 ran at ~0.3 of the f32 MFMA peak with T = 64.
+template <bool TA, bool TB, int T>
 __global__ void __launch_bounds__(NT) gemm_f32_kernel(GemmParams p) {
-  __shared__ float As[2][KB][BM + PAD];
-  __shared__ float Bs[2][KB][BN + PAD];
+  constexpr int TW = T / 32;         // MFMA tiles per wave per dimension
+  constexpr int LDR = T + 16;        // padded LDS row (floats)
+  constexpr int PER = T * KB / NT;   // elements of each operand slice loaded per thread
+  __shared__ float As[2][KB][LDR];
+  __shared__ float Bs[2][KB][LDR];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int i = lane & 15, g = lane >> 4;
-  const long long m0 = (long long)blockIdx.y * BM;
-  const int n0 = blockIdx.x * BN;
-  const int wm = (w >> 1) * 32, wn = (w & 1) * 32;
+  const long long m0 = (long long)blockIdx.y * T;
+  const int n0 = blockIdx.x * T;
+  const int wm = (w >> 1) * (T / 2), wn = (w & 1) * (T / 2);
   // this split's k range
   const long long kchunk = ((p.k + gridDim.z - 1) / gridDim.z + KB - 1) / KB * KB;
   const long long k_lo = (long long)blockIdx.z * kchunk;
   const long long k_hi = k_lo + kchunk < p.k ? k_lo + kchunk : p.k;
 
-  f32x4 acc[2][2];
+  f32x4 acc[TW][TW];
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int a = 0; a < TW; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b) acc[a][b] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    for (int b = 0; b < TW; ++b) acc[a][b] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
 
-  // global -> registers for one KB slice (4 elements of A and of B per thread)
-  float ra[4], rb[4];
+  // global -> registers for one KB slice (PER consecutive elements of A and of B per thread)
+  float ra[PER], rb[PER];
   auto load = [&](long long k0) __attribute__((always_inline)) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int e = tid * 4 + q;  // element of the 64 x 16 slice
+    for (int q = 0; q < PER; ++q) {
+      const int e = tid * PER + q;  // element of the T x KB slice
       int mm, kk;
-      if (TA) { kk = e / BM; mm = e % BM; } else { mm = e / KB; kk = e % KB; }
+      if (TA) { kk = e / T; mm = e % T; } else { mm = e / KB; kk = e % KB; }
       const long long m = m0 + mm, k = k0 + kk;
       ra[q] = (m < p.m && k < k_hi) ? (TA ? p.a[k * p.lda + m] : p.a[m * p.lda + k]) : 0.0f;
       int nn, kb;
-      if (TB) { nn = e / KB; kb = e % KB; } else { kb = e / BN; nn = e % BN; }
+      if (TB) { nn = e / KB; kb = e % KB; } else { kb = e / T; nn = e % T; }
       const long long n = n0 + nn, kq = k0 + kb;
       rb[q] = (n < p.n && kq < k_hi) ? (TB ? p.b[n * p.ldb + kq] : p.b[kq * p.ldb + n]) : 0.0f;
     }
   };
   auto store = [&](int buf) __attribute__((always_inline)) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int e = tid * 4 + q;
+    for (int q = 0; q < PER; ++q) {
+      const int e = tid * PER + q;
       int mm, kk;
-      if (TA) { kk = e / BM; mm = e % BM; } else { mm = e / KB; kk = e % KB; }
+      if (TA) { kk = e / T; mm = e % T; } else { mm = e / KB; kk = e % KB; }
       As[buf][kk][mm] = ra[q];
       int nn, kb;
-      if (TB) { nn = e / KB; kb = e % KB; } else { kb = e / BN; nn = e % BN; }
+      if (TB) { nn = e / KB; kb = e % KB; } else { kb = e / T; nn = e % T; }
       Bs[buf][kb][nn] = rb[q];
     }
   };
@@ -120,35 +143,55 @@ __global__ void __launch_bounds__(NT) gemm_f32_kernel(GemmParams p) {
     if (more) load(k0 + KB);  // global loads of the next slice in flight during the MFMAs
 #pragma unroll
     for (int ks = 0; ks < KB / 4; ++ks) {
-      float av[2], bv[2];
+      float av[TW], bv[TW];
 #pragma unroll
-      for (int a = 0; a < 2; ++a) av[a] = As[buf][ks * 4 + g][wm + a * 16 + i];
+      for (int a = 0; a < TW; ++a) av[a] = As[buf][ks * 4 + g][wm + a * 16 + i];
 #pragma unroll
-      for (int b = 0; b < 2; ++b) bv[b] = Bs[buf][ks * 4 + g][wn + b * 16 + i];
+      for (int b = 0; b < TW; ++b) bv[b] = Bs[buf][ks * 4 + g][wn + b * 16 + i];
 #pragma unroll
-      for (int a = 0; a < 2; ++a)
+      for (int a = 0; a < TW; ++a)
 #pragma unroll
-        for (int b = 0; b < 2; ++b) acc[a][b] = mfma4(av[a], bv[b], acc[a][b]);
+        for (int b = 0; b < TW; ++b) acc[a][b] = mfma4(av[a], bv[b], acc[a][b]);
     }
     if (more) store(buf ^ 1);
     __syncthreads();
     buf ^= 1;
   }
 
-  // lane (g, j = i) of MFMA tile (a, b) holds rows 4g + r of column j
+  // lane (g, j = i) of MFMA tile (a, b) holds rows 4g + r of column j. The epilogue kind is
+  // dispatched once, outside the fully unrolled element loop (a switch per element kept the loop
+  // rolled and indexed the accumulators dynamically, through scratch)
+  auto emit = [&](auto f) __attribute__((always_inline)) {
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < TW; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
+      for (int b = 0; b < TW; ++b)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const long long m = m0 + wm + a * 16 + 4 * g + r;
-        const int n = n0 + wn + b * 16 + i;
-        if (m < p.m && n < p.n) {
-          if (gridDim.z > 1) p.part[((long long)blockIdx.z * p.m + m) * p.n + n] = acc[a][b][r];
-          else epilogue(p, m, n, acc[a][b][r]);
+        for (int r = 0; r < 4; ++r) {
+          const long long m = m0 + wm + a * 16 + 4 * g + r;
+          const int n = n0 + wn + b * 16 + i;
+          if (m < p.m && n < p.n) f(m, n, acc[a][b][r]);
         }
-      }
+  };
+  if (gridDim.z > 1) {
+    emit([&](long long m, int n, float v) { p.part[((long long)blockIdx.z * p.m + m) * p.n + n] = v; });
+    return;
+  }
+  switch (p.epi) {
+    case GEMM_EPI_NONE: emit([&](long long m, int n, float v) { epilogue_k<GEMM_EPI_NONE>(p, m, n, v); }); break;
+    case GEMM_EPI_BIAS: emit([&](long long m, int n, float v) { epilogue_k<GEMM_EPI_BIAS>(p, m, n, v); }); break;
+    case GEMM_EPI_BIAS_TANH:
+      emit([&](long long m, int n, float v) { epilogue_k<GEMM_EPI_BIAS_TANH>(p, m, n, v); });
+      break;
+    case GEMM_EPI_BIAS_TANH2:
+      emit([&](long long m, int n, float v) { epilogue_k<GEMM_EPI_BIAS_TANH2>(p, m, n, v); });
+      break;
+    case GEMM_EPI_MUL_AUX:
+      emit([&](long long m, int n, float v) { epilogue_k<GEMM_EPI_MUL_AUX>(p, m, n, v); });
+      break;
+    case GEMM_EPI_WGRAD: emit([&](long long m, int n, float v) { epilogue_k<GEMM_EPI_WGRAD>(p, m, n, v); }); break;
+    default: break;
+  }
 }
 
 // split-K: sum the partials in split order (deterministic), then the epilogue
@@ -260,11 +303,17 @@ hipError_t launch_gemm_f32(const GemmParams& p_in, bool ta, bool tb, int splits,
   GemmParams p = p_in;
   if (p.m <= 0 || p.n <= 0) return hipSuccess;
   if (splits < 1) splits = 1;
-  const dim3 grid((unsigned)((p.n + gemm::BN - 1) / gemm::BN), (unsigned)((p.m + gemm::BM - 1) / gemm::BM),
-                  (unsigned)splits);
   if (splits > 1 && !p.part) return hipErrorInvalidValue;
-#define G(TA_, TB_) \
-  if (ta == TA_ && tb == TB_) hipLaunchKernelGGL((gemm::gemm_f32_kernel<TA_, TB_>), grid, dim3(gemm::NT), 0, st, p);
+  // 128 x 128 tiles where both output dimensions fill them (the width-256/512 layers); 64 x 64 for the
+  // narrow ones (width 64, output layers), where a 128 tile would be mostly empty
+  const bool big = p.m >= 128 && p.n >= 128;
+  const int T = big ? 128 : 64;
+  const dim3 grid((unsigned)((p.n + T - 1) / T), (unsigned)((p.m + T - 1) / T), (unsigned)splits);
+#define G(TA_, TB_)                                                                                          \
+  if (ta == TA_ && tb == TB_) {                                                                              \
+    if (big) hipLaunchKernelGGL((gemm::gemm_f32_kernel<TA_, TB_, 128>), grid, dim3(gemm::NT), 0, st, p);     \
+    else hipLaunchKernelGGL((gemm::gemm_f32_kernel<TA_, TB_, 64>), grid, dim3(gemm::NT), 0, st, p);          \
+  }
   G(false, false) G(false, true) G(true, false) G(true, true)
 #undef G
   hipError_t e = hipGetLastError();
