@@ -103,12 +103,14 @@ __global__ void __launch_bounds__(NT) gemm_f32_kernel(GemmParams p) {
 #pragma unroll
     for (int b = 0; b < TW; ++b) acc[a][b] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
 
-  // global -> registers for one KB slice (PER consecutive elements of A and of B per thread)
+  // global -> registers for one KB slice, PER elements of A and of B per thread. Element e = q NT + tid:
+  // consecutive lanes take consecutive elements along each operand's contiguous dimension, so one
+  // wave-load touches 4 rows x 64 B (k-contiguous operands) or 256 contiguous bytes
   float ra[PER], rb[PER];
   auto load = [&](long long k0) __attribute__((always_inline)) {
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
-      const int e = tid * PER + q;  // element of the T x KB slice
+      const int e = q * NT + tid;  // element of the T x KB slice
       int mm, kk;
       if (TA) { kk = e / T; mm = e % T; } else { mm = e / KB; kk = e % KB; }
       const long long m = m0 + mm, k = k0 + kk;
@@ -122,7 +124,7 @@ __global__ void __launch_bounds__(NT) gemm_f32_kernel(GemmParams p) {
   auto store = [&](int buf) __attribute__((always_inline)) {
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
-      const int e = tid * PER + q;
+      const int e = q * NT + tid;
       int mm, kk;
       if (TA) { kk = e / T; mm = e % T; } else { mm = e / KB; kk = e % KB; }
       As[buf][kk][mm] = ra[q];
