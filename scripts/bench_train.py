@@ -7,7 +7,8 @@ For each (width, precision) it times with HIP events on the launching stream:
                    loss + gradients -> dmip_adam_step, no host synchronisation),
   * ms_epoch_step  CDE.train_epoch's step (host t / eps draws, torch Adam, the reference's per-batch
                    loss.item()), host-timed,
-and once, the same step through torch autograd on the GPU and on the host CPU (bounded batch).
+and once, the same step through torch autograd on the GPU and on the host CPU (bounded batch); plus
+PosteriorLoss (A18, dmip_posterior_loss_grad) at widths 256 and 512 on scatterometry-shaped data.
 Algorithmic flops per sample: 16.94 F, F = 2 (5 W + 2 W^2 + 2 W). One JSON line.
     python scripts/bench_train.py [--batch 65536] [--steps 20] [--cpu-batch 4096]"""
 import argparse
@@ -90,6 +91,27 @@ def main():
                                     "device_step_samples_per_s": B / (ms_dev * 1e-3),
                                     "loss_grad_tflops": tf, "frac_of_dense_peak": tf / PEAK[prec]}
     os.environ.pop("DMIP_TRAIN_PRECISION", None)
+
+    # A18: PosteriorLoss (prior DSM + likelihood target through the surrogate), exact f32, the fused
+    # dmip_posterior_loss_grad on scatterometry-shaped data
+    gold = os.path.join(ROOT, "tests", "golden")
+    fm, prm = pkg.load_forward_model(gold)
+    fm = fm.to(dev)
+    xs = torch.rand(B, 3, device=dev) * 2 - 1
+    with torch.no_grad():
+        ysc = fm(xs)
+    ysc = ysc + (prm["a"] * ysc.abs() + prm["b"]) * torch.randn_like(ysc)
+    for width in (256, 512):
+        mp = pkg.PosteriorDiffusionEstimator(3, 23, [width] * 3)
+        mp.sde.a.to(dev)
+        plf = pkg.PosteriorLoss(fm, prm["a"], prm["b"], 0.01)
+        tp = mp.sample_t(xs).detach()
+        ep = torch.randn_like(xs)
+        run = lambda: tr.posterior_loss_grad(mp, plf, xs, ysc, tp, ep)
+        for _ in range(a.warmup):
+            run()
+        ms = timed(run, a.steps)
+        rows[f"posterior_loss_w{width}_fp32"] = {"ms_loss_grad": ms, "samples_per_s": B / (ms * 1e-3)}
 
     m = pkg.CDE(2, 2, [64] * 3)
     opt = torch.optim.Adam(m.sde.a.parameters(), lr=1e-4)
