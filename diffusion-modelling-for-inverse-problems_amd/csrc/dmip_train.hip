@@ -234,6 +234,15 @@ __global__ void __launch_bounds__(256) train_pack_kernel(TrainParams p) {
   pack_weights<NL>(p, p.packed, blockIdx.x * blockDim.x + threadIdx.x, gridDim.x * blockDim.x);
 }
 
+// add into the wave's gradient partial: in global memory a no-return float atomic (the wave does not
+// wait for a load of its own row before every update: those read-modify-write round trips sat on the
+// tile's dependency chain); the row is the wave's own, and its updates to one address are issued in
+// program order, so the sums keep a fixed order. In LDS a plain add.
+__device__ __forceinline__ void gadd(float* a, float v) {
+  if constexpr (GACC_GLOBAL) (void)__hip_atomic_fetch_add(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *a += v;
+}
+
 template <int NL>
 __global__ void __launch_bounds__(NWV * 64, 1) loss_grad_kernel(TrainParams p) {
   using L = TL<NL>;
@@ -257,6 +266,7 @@ __global__ void __launch_bounds__(NWV * 64, 1) loss_grad_kernel(TrainParams p) {
     } else {
       float* gacc = p.partials + ((size_t)blockIdx.x * NWV + w) * L::PART;
       for (int e = lane; e < L::PART; e += 64) gacc[e] = 0.0f;
+      __threadfence();  // the zeroes are in L2 before the first atomic of this wave lands
     }
   }
   __syncthreads();
@@ -577,7 +587,7 @@ __global__ void __launch_bounds__(NWV * 64, 1) loss_grad_kernel(TrainParams p) {
           }
           if (hh == 0) {
 #pragma unroll
-            for (int o = 0; o < OUT; ++o) gacc[L::p_w(NL) + o * W + 32 * U + i32] += acc[o];
+            for (int o = 0; o < OUT; ++o) gadd(&gacc[L::p_w(NL) + o * W + 32 * U + i32], acc[o]);
           }
         }
 #pragma unroll
@@ -649,8 +659,8 @@ __global__ void __launch_bounds__(NWV * 64, 1) loss_grad_kernel(TrainParams p) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int row = 32 * T + (r & 3) + 8 * (r >> 2) + 4 * hh;
-            if (i32 < IN) gacc[L::p_w(0) + row * IN + i32] += acc[r];
-            else if (i32 == IN) gacc[L::p_b(0) + row] += acc[r];
+            if (i32 < IN) gadd(&gacc[L::p_w(0) + row * IN + i32], acc[r]);
+            else if (i32 == IN) gadd(&gacc[L::p_b(0) + row], acc[r]);
           }
         }
       } else {
@@ -669,7 +679,7 @@ __global__ void __launch_bounds__(NWV * 64, 1) loss_grad_kernel(TrainParams p) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
               const int row = 32 * T + (r & 3) + 8 * (r >> 2) + 4 * hh;
-              gacc[pw + row * W + 32 * U + i32] += acc[r];
+              gadd(&gacc[pw + row * W + 32 * U + i32], acc[r]);
             }
           }
         // h-bar of layer li-1 = W_li^T zbar
@@ -700,14 +710,14 @@ __global__ void __launch_bounds__(NWV * 64, 1) loss_grad_kernel(TrainParams p) {
         float v = bbar[l][R][r];
 #pragma unroll
         for (int m = 1; m < 16; m <<= 1) v += __shfl_xor(v, m, 64);
-        if (c16 == 0) gacc[L::p_b(l + 1) + 16 * R + 4 * g + r] += v;
+        if (c16 == 0) gadd(&gacc[L::p_b(l + 1) + 16 * R + 4 * g + r], v);
       }
 #pragma unroll
   for (int o = 0; o < OUT; ++o) {
     float v = g == 0 ? bobar[o] : 0.0f;
 #pragma unroll
     for (int m = 1; m < 64; m <<= 1) v += __shfl_xor(v, m, 64);
-    if (lane == 0) gacc[L::p_b(NL) + o] += v;
+    if (lane == 0) gadd(&gacc[L::p_b(NL) + o], v);
   }
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
@@ -719,13 +729,15 @@ __global__ void __launch_bounds__(NWV * 64, 1) loss_grad_kernel(TrainParams p) {
   if constexpr (GACC_GLOBAL) {
     // fold the workgroup's NWV rows into its first row, in wave order (deterministic), so the
     // reduction reads one row per workgroup
-    __threadfence_block();
+    __threadfence();
     __syncthreads();
     float* rows = p.partials + (size_t)blockIdx.x * NWV * L::PART;
+    // the rows were updated by L2 atomics: read them at agent scope (past this CU's L1)
+    auto rd = [](float* a) { return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
     for (int e = tid; e < L::PART; e += NWV * 64) {
-      float v = rows[e];
+      float v = rd(rows + e);
 #pragma unroll
-      for (int ww = 1; ww < NWV; ++ww) v += rows[(size_t)ww * L::PART + e];
+      for (int ww = 1; ww < NWV; ++ww) v += rd(rows + (size_t)ww * L::PART + e);
       rows[e] = v;
     }
     return;
