@@ -800,8 +800,9 @@ int dmip_loss_grad_f32(int in_dim, int out_dim, int n_hidden, const int* widths,
       !grad_out_dev || !loss_out_dev)
     return fail(DMIP_ERR_INVALID, "null argument");
   if (n_hidden < 1 || n_hidden > dmip::kJetsMaxLayers - 1) return fail(DMIP_ERR_UNSUPPORTED, "n_hidden must be in [1, 8]");
-  if (xdim < 1 || xdim > 4 || out_dim != xdim)
-    return fail(DMIP_ERR_UNSUPPORTED, "f32 training: CDE networks (out_dim == xdim) with xdim in [1, 4]");
+  if (out_dim != xdim) return fail(DMIP_ERR_UNSUPPORTED, "f32 training: score networks with out_dim == xdim");
+  if (xdim < 1 || xdim > (cfg->kind == DMIP_LOSS_DSM ? dmip::kJetsMaxDsmDim : 4))
+    return fail(DMIP_ERR_UNSUPPORTED, "f32 training: xdim in [1, 4] (DSMLoss: [1, 64])");
   const int ydim = in_dim - xdim - 1;
   if (ydim < 0) return fail(DMIP_ERR_INVALID, "in_dim must be xdim + ydim + 1");
   for (int i = 0; i < n_hidden; ++i)

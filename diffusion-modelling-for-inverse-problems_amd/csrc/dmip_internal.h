@@ -288,6 +288,8 @@ struct PosteriorParams {
 
 // ---- exact-f32 score-matching losses at any width (dmip_jets.hip): stacked jet streams
 constexpr int kJetsMaxLayers = 9;
+// DSMLoss needs only the primal stream: any state dimension up to this (CDiffE trains on z = (x, y))
+constexpr int kJetsMaxDsmDim = 64;
 
 struct JetsParams {
   long long batch;

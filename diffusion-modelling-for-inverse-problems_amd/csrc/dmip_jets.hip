@@ -161,12 +161,18 @@ __global__ void jets_loss_kernel(JetsParams p, const float* A, const float* bout
   float s[4], dsdt[4], dls[4] = {0, 0, 0, 0}, dlv[4] = {0, 0, 0, 0};
   const float invB = 1.0f / (float)B;
   float dsm = 0.0f;
+  float* zb = p.zbar;  // [nb][B][O]
   for (int i = 0; i < D; ++i) {
     const float aP = ar(0, i) + bout[i];
-    s[i] = aP / g;
-    if (p.blk_v >= 0) dsdt[i] = ar(p.blk_v, i) / g - aP * dg / (g * g);
-    const float r = s[i] * sd + p.eps[b * D + i];  // DSMLoss (losses.py:50-52)
+    const float si = aP / g;
+    const float r = si * sd + p.eps[b * D + i];  // DSMLoss (losses.py:50-52)
     dsm += r * r;
+    if (i >= 4) {  // DSMLoss only (the C-ABI admits D > 4 for no other loss): the adjoint directly
+      zb[b * O + i] = r * sd * invB / g;
+      continue;
+    }
+    s[i] = si;
+    if (p.blk_v >= 0) dsdt[i] = ar(p.blk_v, i) / g - aP * dg / (g * g);
     if (p.has_dsm) dls[i] += r * sd * invB;
   }
   dsm *= 0.5f;
@@ -207,8 +213,8 @@ __global__ void jets_loss_kernel(JetsParams p, const float* A, const float* bout
     }
   }
   float ic = 0.0f;
-  float* zb = p.zbar;  // [nb][B][O]
   for (int i = 0; i < O; ++i) {
+    if (i >= 4 && i < D) continue;  // written above
     zb[b * O + i] = i < D ? dls[i] / g : 0.0f;
     if (p.blk_v >= 0) zb[((long long)p.blk_v * B + b) * O + i] = i < D ? dlv[i] : 0.0f;
   }

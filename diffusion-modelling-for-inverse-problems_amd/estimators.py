@@ -319,9 +319,18 @@ class CDiffE(BaseClassDiffusionModel):
                                drift, xd, xd, y_resample)
 
     def train_epoch(self, optimizer, loss_fn, epoch_data_loader):
+        """models/diffusion.py:123-156. On a HIP device DSMLoss on the joint z = (x, y) runs through the
+        exact-f32 fused loss + gradient engine (training.joint_fused_config); otherwise autograd."""
+        from .training import fused_loss_grad, joint_fused_config
+        cfg = joint_fused_config(self, loss_fn)
+
         def batch_loss(x, y):
             z = torch.concat([x, y], dim=1)
             t = self.sample_t(z)
+            if cfg is not None:
+                eps = torch.randn_like(z)  # base_sde.sample's draw (sdes.py:37-49)
+                optimizer.zero_grad()
+                return _FusedStep(*fused_loss_grad(self, loss_fn, cfg, z, None, t, eps))
             diffused, target, std, g = self.sde.base_sde.sample(t, z, return_noise=True)
             x_t, y_t = diffused[:, :self.xdim], diffused[:, self.xdim:]
             if loss_fn.name == 'DSMLoss':

@@ -10,7 +10,9 @@ not accumulated). Two device paths:
   * "bf16": dmip_loss_grad -- the persistent bf16-MFMA kernel of BASELINE config 5 (the linear
     problem's width-64 CDE with its analytic IC target), selected with $DMIP_TRAIN_PRECISION=bf16.
 It is what CDE.train_epoch runs on a HIP device when `fused_config` accepts the network and loss;
-everything else (CDiffE's joint training, CPU tensors) takes the autograd path of losses.py.
+CDiffE.train_epoch runs its DSMLoss (the only loss the reference's joint training accepts) through the
+same f32 engine on z = (x, y) (`joint_fused_config`); everything else (CPU tensors, other shapes)
+takes the autograd path of losses.py.
 """
 import os
 
@@ -74,15 +76,47 @@ def fused_config(model, loss_fn):
     return cfg
 
 
+def joint_fused_config(model, loss_fn):
+    """dmip_loss_cfg for CDiffE's joint training (models/diffusion.py:123-156), or None. The reference
+    trains CDiffE with DSMLoss only: its other losses call sde.a(x_t, y, t) with the joint x_t and fail
+    on the input width. DSM on z = (x, y) is the engine's DSM with state z and no condition (ydim 0)."""
+    if os.environ.get("DMIP_TRAIN_FUSED", "1") == "0" or type(loss_fn) is not DSMLoss:
+        return None
+    net = model.sde.a
+    if not hasattr(net, "linear_layers"):
+        return None
+    layers = net.linear_layers()
+    p0 = layers[0][0]
+    zdim = model.xdim + model.ydim
+    if not p0.is_cuda or p0.dtype != torch.float32 or net.output_dim != zdim or net.input_dim != zdim + 1 \
+            or zdim > 64 or len(layers) - 1 > 8:
+        return None
+    cfg = _lib.DmipLossCfg()
+    cfg.kind, cfg.pde = _lib.DMIP_LOSS_DSM, _lib.DMIP_PDE_NONE
+    return cfg
+
+
 def fused_loss_grad(model, loss_fn, cfg, x, y, t, eps, precision=None):
     """One fused loss + gradient evaluation. Returns (loss, info) like the reference loss objects:
     a 0-d tensor and {component name: 0-d tensor}. precision: "fp32" (dmip_loss_grad_f32, default) or
-    "bf16" (dmip_loss_grad, where compiled: the linear problem's width-64 CDE, analytic IC)."""
+    "bf16" (dmip_loss_grad, where compiled: the linear problem's width-64 CDE, analytic IC).
+    y=None: joint training (CDiffE), x is the state z = (x, y) and the network has no condition input."""
     net = model.sde.a
     layers = [(w.detach(), b.detach()) for w, b in net.linear_layers()]
     dev = layers[0][0].device
     f32 = dict(device=dev, dtype=torch.float32)
     x = x.detach().to(**f32).contiguous()
+    if y is None:  # ydim 0: the pointer is never read
+        t = t.detach().to(**f32).reshape(-1).contiguous()
+        eps = eps.detach().to(**f32).contiguous()
+        params = list(net.parameters())
+        flat = torch.empty(sum(p.numel() for p in params), **f32)
+        out = torch.empty(4, **f32)
+        base = model.sde.base_sde
+        sde = _lib.vpsde(base.beta_min, base.beta_max, 1.0)
+        _lib.loss_grad_f32(layers, net.input_dim, net.output_dim, x.shape[1], sde, cfg, x, x, t, eps, flat, out)
+        _set_grads(params, flat)
+        return loss_info(cfg.kind, out)
     y = y.detach().to(**f32).contiguous()
     t = t.detach().to(**f32).reshape(-1).contiguous()
     eps = eps.detach().to(**f32).contiguous()
@@ -106,11 +140,15 @@ def fused_loss_grad(model, loss_fn, cfg, x, y, t, eps, precision=None):
                 ic = loss_fn.initial_condition(x, y)
             ic = ic.detach().to(**f32)[:, :model.xdim].contiguous()
         _lib.loss_grad_f32(layers, net.input_dim, net.output_dim, model.xdim, sde, cfg, x, y, t, eps, flat, out, ic)
+    _set_grads(params, flat)
+    return loss_info(cfg.kind, out)
+
+
+def _set_grads(params, flat):
     off = 0
     for p in params:
         p.grad = flat[off:off + p.numel()].view_as(p)
         off += p.numel()
-    return loss_info(cfg.kind, out)
 
 
 def loss_info(kind, out):

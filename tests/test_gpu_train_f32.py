@@ -166,3 +166,68 @@ def test_train_epoch_default_is_exact_f32_and_tracks_autograd(dmip, monkeypatch)
     assert lf == pytest.approx(la, rel=1e-3)
     for k in info_a:
         assert info_f[k] == pytest.approx(info_a[k], rel=1e-2, abs=1e-6)
+
+
+def _cdiffe_dsm_f64(m, z, t, eps):
+    """CDiffE.train_epoch's DSM batch loss (models/diffusion.py:128-136, losses.py:50-52) by float64
+    autograd on the CPU: the reference semantics at a precision well above the kernel's."""
+    import copy
+    net = copy.deepcopy(m.sde.a).cpu().double()
+    base = m.sde.base_sde
+    z, t, eps = (v.detach().cpu().double() for v in (z, t, eps))
+    std = base.var(t) ** 0.5
+    zt = eps * std + base.mean_weight(t) * z
+    g = base.g(t, zt)
+    score = net(zt[:, :m.xdim], zt[:, m.xdim:], t) / g
+    loss = (((score * std + eps) ** 2).sum(1) / 2).mean()
+    loss.backward()
+    return float(loss), [p.grad.numpy() for p in net.parameters()]
+
+
+@pytest.mark.parametrize("xd,yd,W,n", [(2, 2, 64, 1000), (2, 2, 512, 4096), (3, 23, 256, 777), (3, 23, 512, 2048)])
+def test_cdiffe_joint_dsm_vs_autograd(dmip, xd, yd, W, n):
+    """CDiffE's joint DSM (state z = (x, y), 26-D for scatterometry) through dmip_loss_grad_f32 with
+    ydim 0, against float64 autograd of the reference loss on the same (z, t, eps). Tolerances: loss
+    1e-4 relative, every gradient tensor 2e-3 relative L2 (exact f32 vs f64)."""
+    torch.manual_seed(W + xd)
+    m = dmip.CDiffE(xd, yd, [W] * 3)
+    lf = dmip.DSMLoss()
+    cfg = _tr().joint_fused_config(m, lf)
+    assert cfg is not None
+    g = torch.Generator().manual_seed(3)
+    z = torch.randn(n, xd + yd, generator=g)
+    t = (1e-4 + torch.rand(n, 1, generator=g)).clamp(max=1.0)
+    eps = torch.randn(n, xd + yd, generator=g)
+    before = dmip._lib.calls.get("loss_grad_f32", 0)
+    loss, info = _tr().fused_loss_grad(m, lf, cfg, z.to(DEV), None, t.to(DEV), eps.to(DEV))
+    assert dmip._lib.calls["loss_grad_f32"] == before + 1 and info == {}
+    grads = [p.grad.detach().cpu().numpy() for p in m.sde.a.parameters()]
+    ref_loss, ref_grads = _cdiffe_dsm_f64(m, z, t, eps)
+    assert float(loss) == pytest.approx(ref_loss, rel=1e-4)
+    errs = [_rel(gk, rk) for gk, rk in zip(grads, ref_grads)]
+    assert max(errs) < 2e-3, errs
+
+
+def test_cdiffe_train_epoch_fused_tracks_autograd(dmip, monkeypatch):
+    """CDiffE.train_epoch (scatterometry shape, [256]*3, DSMLoss) takes the fused engine on the device and
+    follows the autograd path (DMIP_TRAIN_FUSED=0) batch by batch from the same seeds."""
+    def run(fused):
+        monkeypatch.setenv("DMIP_TRAIN_FUSED", "1" if fused else "0")
+        torch.manual_seed(0)
+        m = dmip.CDiffE(3, 23, [256] * 3)
+        opt = torch.optim.Adam(m.sde.a.parameters(), lr=1e-4)
+        gen = torch.Generator().manual_seed(1)
+        x = torch.rand(2048, 3, generator=gen).to(DEV)
+        y = torch.randn(2048, 23, generator=gen).to(DEV)
+
+        def loader():
+            for i in range(0, 2048, 512):
+                yield x[i:i + 512], y[i:i + 512]
+        before = dmip._lib.calls.get("loss_grad_f32", 0)
+        torch.manual_seed(5)
+        loss, _ = m.train_epoch(opt, dmip.DSMLoss(), loader)
+        return float(loss), dmip._lib.calls.get("loss_grad_f32", 0) - before
+    lf, nf = run(True)
+    la, na = run(False)
+    assert nf == 4 and na == 0
+    assert lf == pytest.approx(la, rel=1e-3)
