@@ -34,7 +34,7 @@ EXPORTED = (
     "dmip_loss_grad_supported", "dmip_histogram", "dmip_surrogate_create", "dmip_surrogate_destroy",
     "dmip_surrogate_forward", "dmip_log_posterior", "dmip_mh_sample", "dmip_dps_sample", "dmip_device_status",
     "dmip_sampler_supported_f32", "dmip_posterior_loss_grad", "dmip_loss_grad_f32", "dmip_train_draws",
-    "dmip_adam_step",
+    "dmip_adam_step", "dmip_em_sample_snapshots",
 )
 DMIP_DPS_NLL, DMIP_DPS_NORM = 0, 1
 
@@ -97,6 +97,10 @@ def _declare(lib):
     lib.dmip_em_sample_cdiffe.argtypes = [_c_void_p, ctypes.POINTER(DmipVpsde), _c_void_p, _i32, _i32, _i32,
                                           _i64, _i64, _i32, _f32, _f32, _u64, _i32, _i32, _f32, _c_void_p,
                                           _c_void_p]
+    if hasattr(lib, "dmip_em_sample_snapshots"):  # (absent from older builds loaded by A/B timing scripts)
+        lib.dmip_em_sample_snapshots.argtypes = [_i32, _c_void_p, _c_void_p, ctypes.POINTER(DmipVpsde), _c_void_p, _i32,
+                                                 _i32, _i32, _i64, _i64, _i32, _f32, _f32, _u64, _i32, _i32, _f32,
+                                                 _i32, _c_void_p, _c_void_p, _c_void_p]
     lib.dmip_loss_grad.argtypes = [_i32, _i32, _i32, ctypes.POINTER(_i32), _i32, ctypes.POINTER(_c_void_p),
                                    ctypes.POINTER(_c_void_p), ctypes.POINTER(DmipVpsde), ctypes.POINTER(DmipLossCfg),
                                    _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _c_void_p, _c_void_p,
@@ -243,6 +247,20 @@ def em_sample_cdiffe(handle, sde, y, n_chains, chain_offset, num_steps, mean, st
                                       int(n_chains), int(chain_offset), int(num_steps), float(mean), float(std),
                                       ctypes.c_uint64(int(seed) & 0xFFFFFFFFFFFFFFFF), precision_code(precision),
                                       int(corrector_steps), float(snr), ptr(out), stream_of(y.device)))
+
+
+def em_sample_snapshots(mode, net, prior, sde, y, n_chains, chain_offset, num_steps, mean, std, seed, snapshot_every,
+                        snaps, out, corrector_steps=0, snr=0.16, precision="bf16"):
+    """dmip_em_sample_snapshots: the fused sampler of `mode` that also writes x after every
+    snapshot_every-th step into snaps [num_steps // snapshot_every][n_y][n_chains][xdim]."""
+    calls["em_sample_snapshots"] = calls.get("em_sample_snapshots", 0) + 1
+    n_y, ydim = y.shape
+    check(lib().dmip_em_sample_snapshots(int(mode), net.h, prior.h if prior is not None else None, ctypes.byref(sde),
+                                         ptr(y), n_y, ydim, net.xdim, int(n_chains), int(chain_offset),
+                                         int(num_steps), float(mean), float(std),
+                                         ctypes.c_uint64(int(seed) & 0xFFFFFFFFFFFFFFFF), precision_code(precision),
+                                         int(corrector_steps), float(snr), int(snapshot_every), ptr(snaps), ptr(out),
+                                         stream_of(y.device)))
 
 
 def sampler_supported(width, n_hidden, xdim, ydim=0, mode=DMIP_SAMPLER_CDE, precision="bf16"):

@@ -509,6 +509,8 @@ struct SampleArgs {
   uint64_t* stamps;
   int n_corr = 0;
   float snr = 0.16f;
+  int snap_every = 0;
+  float* snap_out_dev = nullptr;
 };
 
 static void fill_schedule(const SampleArgs& a, float& T, float& bmin, float& bdiff, float& delta, float& sqrt_delta) {
@@ -550,6 +552,8 @@ static int em_sample_f32(int mode, const dmip_mlp* net0, const dmip_mlp* net1, c
   p.snr = a.snr;
   p.noise = a.noise_dev;
   p.x_out = a.x_out_dev;
+  p.snap_out = a.snap_out_dev;
+  p.snap_every = a.snap_every;
   p.n_chains = a.n_chains;
   p.chain_offset = a.chain_offset;
   p.num_steps = a.num_steps;
@@ -650,6 +654,8 @@ static int em_sample_impl(int mode, const dmip_mlp* net0, const dmip_mlp* net1, 
   p.snr = a.snr;
   p.noise = a.noise_dev;
   p.x_out = a.x_out_dev;
+  p.snap_out = a.snap_out_dev;
+  p.snap_every = a.snap_every;
   p.n_chains = a.n_chains;
   p.chain_offset = a.chain_offset;
   p.num_steps = a.num_steps;
@@ -705,6 +711,29 @@ int dmip_em_sample_cdiffe(const dmip_mlp* net, const dmip_vpsde* sde, const floa
   a.n_corr = corrector_steps;
   a.snr = snr;
   return em_sample_impl(DMIP_SAMPLER_CDIFFE, net, nullptr, a);
+}
+
+int dmip_em_sample_snapshots(int mode, const dmip_mlp* net, const dmip_mlp* prior, const dmip_vpsde* sde,
+                             const float* y_dev, int n_y, int ydim, int xdim, int64_t n_chains, int64_t chain_offset,
+                             int num_steps, float mean, float stdv, uint64_t seed, int precision, int corrector_steps,
+                             float snr, int snapshot_every, float* snap_out_dev, float* x_out_dev, void* stream) {
+  if (mode != DMIP_SAMPLER_CDE && mode != DMIP_SAMPLER_POSTERIOR && mode != DMIP_SAMPLER_CDIFFE)
+    return fail(DMIP_ERR_INVALID, "unknown sampler mode");
+  if (snapshot_every < 1 || snapshot_every > num_steps)
+    return fail(DMIP_ERR_INVALID, "snapshot_every must be in [1, num_steps]");
+  if (!snap_out_dev) return fail(DMIP_ERR_INVALID, "null snapshot buffer");
+  if (mode == DMIP_SAMPLER_POSTERIOR && !prior) return fail(DMIP_ERR_INVALID, "null argument");
+  if (mode != DMIP_SAMPLER_CDIFFE && corrector_steps != 0)
+    return fail(DMIP_ERR_INVALID, "corrector steps: CDiffE sampler only");
+  if (corrector_steps < 0) return fail(DMIP_ERR_INVALID, "corrector_steps must be >= 0");
+  if (corrector_steps > 0 && !(snr > 0.0f)) return fail(DMIP_ERR_INVALID, "snr must be > 0");
+  SampleArgs a{sde,  y_dev, n_y,       ydim,      xdim,    n_chains, chain_offset, num_steps,
+               mean, stdv,  seed,      precision, nullptr, x_out_dev, stream,      nullptr};
+  a.n_corr = corrector_steps;
+  a.snr = snr;
+  a.snap_every = snapshot_every;
+  a.snap_out_dev = snap_out_dev;
+  return em_sample_impl(mode, net, mode == DMIP_SAMPLER_POSTERIOR ? prior : nullptr, a);
 }
 
 int dmip_em_sample_stamps(const dmip_mlp* net, const dmip_vpsde* sde, const float* y_dev, int n_y, int ydim,

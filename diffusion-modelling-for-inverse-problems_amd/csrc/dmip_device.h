@@ -144,6 +144,25 @@ __device__ __forceinline__ float em_update(float x, float a, float xi, const Ste
   return __fadd_rn(drift, __fmul_rn(__fmul_rn(sqrt_delta, c.g), xi));
 }
 
+// Trajectory snapshots: x of a chain after every `every`-th step (0-based step i, i + 1 a multiple
+// of every) into snap [S / every][n_y][n_chains][D] -- the only HBM writes of a chain before its final
+// state. The cursor holds the next snapshot step of the segment [s0, s1), so a step pays one scalar
+// compare (-1: snapshots off).
+struct SnapCursor {
+  int next;
+  __device__ __forceinline__ SnapCursor(int every, int s0) : next(every > 0 ? (s0 / every + 1) * every : -1) {}
+  template <int D>
+  __device__ __forceinline__ void at_step(int i, int every, float* snap, int n_y, int yi, long long n_chains,
+                                          long long c, bool write, const float (&x)[D]) {
+    if (i + 1 != next) return;
+    next += every;
+    if (!write) return;
+    float* dst = snap + (((size_t)((i + 1) / every - 1) * n_y + yi) * n_chains + c) * D;
+#pragma unroll
+    for (int k = 0; k < D; ++k) dst[k] = x[k];
+  }
+};
+
 // ---------------------------------------------------------------------------- activation
 // Hidden layers propagate r = 1/(1+exp(2z)) instead of tanh(z) = 1 - 2r; the "1 - 2r" is folded
 // into the next layer on the host (weights -2W, bias b + sum_k W). The pre-activation arrives

@@ -305,6 +305,7 @@ __global__ void __launch_bounds__(Shape<W>::NW * 64, 1) f32_sampler_kernel(F32Sa
       for (int k = 0; k < D; ++k) x[k] = __fadd_rn(__fmul_rn(n0[k], p.stdv), p.mean);
     }
 
+    SnapCursor snap(p.snap_every, sg.s0);
     for (int i0 = sg.s0; i0 < sg.s1; ++i0) {
       const int i = sg.kind == 3 ? 0 : i0;  // idle steps: a dummy tile at step 0, discarded
       const StepCoef cf = step_coef(i, S, p.T, p.bmin, p.bdiff);
@@ -386,6 +387,7 @@ __global__ void __launch_bounds__(Shape<W>::NW * 64, 1) f32_sampler_kernel(F32Sa
         const float ak = MODE == SAMPLER_POSTERIOR ? __fmul_rn(cf.g, a[k]) : a[k];
         x[k] = em_update(x[k], ak, xi[k], cf, p.delta, p.sqrt_delta);
       }
+      snap.at_step<D>(i0, p.snap_every, p.snap_out, gridDim.y, yi, p.n_chains, c_local, sg.kind != 3 && valid && g == 0, x);
     }
     if (sg.kind == 1) {  // hand the tile over to the next wave of the grid
       const size_t slot = (size_t)yi * n_waves + gw;

@@ -50,6 +50,8 @@ struct SamplerParams {
   float snr;                  // CDiffE: corrector signal-to-noise ratio
   const float* noise;         // injected normals [S+1][n_y][n_chains][D] (slot 0 -> x0) or null
   float* x_out;               // [n_y][n_chains][D]
+  float* snap_out;            // trajectory snapshots [S / snap_every][n_y][n_chains][D] or null
+  int snap_every;             // write x after every snap_every-th step (0: final output only)
   long long n_chains;         // chains per y
   long long chain_offset;     // global index of chain 0 (keys the RNG)
   int num_steps;
@@ -197,6 +199,8 @@ struct F32SamplerParams {
   float snr;
   const float* noise;         // CDE: injected normals [S+1][n_y][n_chains][D] or null
   float* x_out;               // [n_y][n_chains][D]
+  float* snap_out;            // trajectory snapshots [S / snap_every][n_y][n_chains][D] or null
+  int snap_every;             // 0: none
   long long n_chains, chain_offset;
   int num_steps;
   float T, bmin, bdiff, delta, sqrt_delta, mean, stdv;

@@ -468,6 +468,7 @@ em_sampler_kernel(SamplerParams p) {
     for (int k = 0; k < D; ++k) x[k] = __fadd_rn(__fmul_rn(n[k], p.stdv), p.mean);
   }
 
+  SnapCursor snap(p.snap_every, sg.s0);
   for (int i = sg.s0; i < sg.s1; ++i) {
     unsigned long long t0 = 0, t1 = 0, t2 = 0;
     if constexpr (STAMP) t0 = stamp();
@@ -531,6 +532,7 @@ em_sampler_kernel(SamplerParams p) {
       const float a = MODE == MODE_POSTERIOR ? __fmul_rn(cf.g, out[k]) : out[k];
       x[k] = em_update(x[k], a, xi[k], cf, p.delta, p.sqrt_delta);
     }
+    snap.at_step<D>(i, p.snap_every, p.snap_out, gridDim.y, yi, p.n_chains, c_local, sg.kind != 3 && valid && h == 0, x);
     if constexpr (STAMP) {
       const unsigned long long t3 = stamp();
       ph[0] += t1 - t0;

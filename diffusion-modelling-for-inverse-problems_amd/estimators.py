@@ -84,6 +84,37 @@ class BaseClassDiffusionModel:
         _lib.device_status(x.device)  # asynchronous kernel failures surface here, not as silent NaNs
         return x.cpu().numpy()
 
+    def sample_trajectory(self, y, num_samples=2000, num_steps=200, snapshot_every=10, mean=0, std=1, seed=None,
+                          chain_offset=0, precision=None, corrector_steps=0, snr=0.16):
+        """The fused sampler with trajectory snapshots (dmip_em_sample_snapshots): returns device tensors
+        (x (n_y, num_samples, xdim), snaps (num_steps // snapshot_every, n_y, num_samples, xdim)), snaps[k]
+        = the chains after step (k + 1) * snapshot_every of the loop of models/diffusion.py:27-46 (the
+        reference returns only the final state). Same chains, RNG and sharding as sample_device."""
+        if isinstance(self, PosteriorDiffusionEstimator):
+            score = self.sde.a
+            nets, mode = [score.prior_net, score.likelihood_net], _lib.DMIP_SAMPLER_POSTERIOR
+        elif isinstance(self, (CDE, CDiffE)):
+            nets = [self.sde.a]
+            mode = _lib.DMIP_SAMPLER_CDIFFE if isinstance(self, CDiffE) else _lib.DMIP_SAMPLER_CDE
+        else:
+            raise NotImplementedError(f"{type(self).__name__}: no fused trajectory sampler")
+        if corrector_steps and mode != _lib.DMIP_SAMPLER_CDIFFE:
+            raise ValueError("corrector steps: CDiffE only")
+        dev, ys, sde, out = self._prepare(y, num_samples, num_steps, nets)
+        handles = [n.dmip_handle(dev, self.xdim) for n in nets]
+        net, prior = handles[-1], (handles[0] if len(handles) > 1 else None)
+        if prior is not None and (prior.width, prior.n_hidden) != (net.width, net.n_hidden):
+            raise ValueError("prior and likelihood networks must have the same hidden layers")
+        prec = _fused_precision(precision or self.precision, mode, net.width, net.n_hidden, self.xdim, self.ydim)
+        if prec is None:
+            raise ValueError("no fused sampler for this network shape")
+        snaps = torch.empty(int(num_steps) // int(snapshot_every), ys.shape[0], int(num_samples), self.xdim,
+                            device=dev, dtype=torch.float32)
+        seed = _draw_seed() if seed is None else seed
+        _lib.em_sample_snapshots(mode, net, prior, sde, ys, num_samples, chain_offset, num_steps, mean, std, seed,
+                                 snapshot_every, snaps, out, corrector_steps, snr, prec)
+        return out, snaps
+
     def _exec_device(self, y):
         if isinstance(y, torch.Tensor) and y.is_cuda:
             return y.device

@@ -125,6 +125,19 @@ int dmip_em_sample_cdiffe(const dmip_mlp* net, const dmip_vpsde* sde, const floa
                           int64_t n_chains, int64_t chain_offset, int num_steps, float mean, float stdv, uint64_t seed,
                           int precision, int corrector_steps, float snr, float* x_out_dev, void* stream);
 
+/* Trajectory snapshots (north_star: "coalesced HBM writes only at snapshot steps"). The sampler of
+ * `mode` (DMIP_SAMPLER_CDE: net; _POSTERIOR: net = the likelihood, prior = the prior; _CDIFFE: net, with
+ * corrector_steps / snr as dmip_em_sample_cdiffe) in one launch as above, which additionally writes
+ * every chain's x after each snapshot_every-th EM step:
+ *   snap_out_dev  [num_steps / snapshot_every][n_y][n_chains][xdim] fp32, slot k = x after step
+ *                 (k + 1) * snapshot_every (the last slot equals x_out when snapshot_every divides num_steps)
+ * The reference keeps only the final samples (models/diffusion.py:27-46); the snapshots are the states
+ * its loop holds at those steps. Between snapshots chain state stays in registers. */
+int dmip_em_sample_snapshots(int mode, const dmip_mlp* net, const dmip_mlp* prior, const dmip_vpsde* sde,
+                             const float* y_dev, int n_y, int ydim, int xdim, int64_t n_chains, int64_t chain_offset,
+                             int num_steps, float mean, float stdv, uint64_t seed, int precision, int corrector_steps,
+                             float snr, int snapshot_every, float* snap_out_dev, float* x_out_dev, void* stream);
+
 /* ---- training: fused loss value + parameter gradients ----------------------------------------- */
 typedef enum { DMIP_LOSS_DSM = 0, DMIP_LOSS_DSM_PDE = 1, DMIP_LOSS_PINN = 2, DMIP_LOSS_PINN2 = 3 } dmip_loss_kind;
 typedef enum { DMIP_PDE_NONE = 0, DMIP_PDE_FPE = 1, DMIP_PDE_CFPE = 2 } dmip_pde_kind;

@@ -300,14 +300,14 @@ def em_sample(a_fn, x0, num_steps, T=1.0, noise=None, rng_state=None, xdim=None,
 
 
 def cde_sample(params, y, num_samples, num_steps, seed, mean=0.0, std=1.0, chain_offset=0,
-               stream=0, T=1.0):
+               stream=0, T=1.0, snapshots=None):
     """Product-RNG CDE sampler: x0 = normals*std + mean (models/diffusion.py:32-33), then EM."""
     xdim = params[-1][0].shape[0]
     st = rng_init(seed, np.arange(chain_offset, chain_offset + num_samples), stream)
     x0 = (rng_normals(st, xdim) * F32(std) + F32(mean)).astype(F32)
     y = np.asarray(y, F32)
     return em_sample(lambda x, tau: cde_a(params, x, y, tau), x0, num_steps, T=T,
-                     rng_state=st, xdim=xdim)
+                     rng_state=st, xdim=xdim, snapshots=snapshots)
 
 
 def posterior_sample(prior_params, lik_params, y, num_samples, num_steps, seed, mean=0.0, std=1.0,

@@ -304,3 +304,50 @@ def test_f32_handover_timeout_is_reported_not_silent(dmip, golden, monkeypatch):
     x = m.sample_device(y, 50000, 4, seed=1, precision="fp32")
     dmip._lib.device_status(x.device)
     assert torch.isfinite(x).all()
+
+
+# ------------------------------------------------------------------- trajectory snapshots
+@pytest.mark.parametrize("W", [64, 256])
+def test_f32_snapshots_vs_oracle(dmip, W):
+    """dmip_em_sample_snapshots (exact f32): every snapshot against the oracle's loop state at that
+    step (oracle.em_sample snapshots), and the last snapshot bit-equal to the final output."""
+    xd, yd = 3, 23
+    torch.manual_seed(W)
+    m = dmip.CDE(xd, yd, [W] * 3)
+    params = _linear_params(m.sde.a)
+    y = np.random.default_rng(5).uniform(0, 1, yd).astype(np.float32)
+    n, S, every, seed = 700, 6, 2, 99
+    x, snaps = m.sample_trajectory(torch.from_numpy(y).to(DEV), n, S, every, seed=seed, precision="fp32")
+    assert tuple(snaps.shape) == (S // every, 1, n, xd)
+    ref, ref_snaps = O.cde_sample(params, y, n, S, seed, snapshots={2, 4, 6})
+    for k in range(S // every):
+        r = ref_snaps[(k + 1) * every]
+        assert np.abs(snaps[k, 0].cpu().numpy() - r).max() < 1e-4 * max(1.0, np.abs(r).max())
+    assert torch.equal(snaps[-1], x)
+    # the same chains as the plain sampler
+    x_plain = m.sample_device(torch.from_numpy(y).to(DEV), n, S, seed=seed, precision="fp32")
+    assert torch.equal(x_plain, x)
+
+
+@pytest.mark.parametrize("cls", ["CDE", "PosteriorDiffusionEstimator", "CDiffE"])
+@pytest.mark.parametrize("precision", ["bf16", "fp32"])
+def test_snapshots_balanced_schedule_all_estimators(dmip, cls, precision):
+    """Snapshots through the balanced persistent schedule (more chains than one GPU round, so tiles
+    are split between waves mid-trajectory), both engines, all three estimators: the final snapshot is
+    the output, the output equals the plain sampler's, and a sharded run's snapshots are the slices
+    of the whole run's (chain-keyed RNG)."""
+    xd, yd = (3, 23) if cls != "CDiffE" else (2, 2)
+    torch.manual_seed(1)
+    m = getattr(dmip, cls)(xd, yd, [64] * 3)
+    y = torch.from_numpy(np.random.default_rng(2).uniform(0, 1, (2, yd)).astype(np.float32)).to(DEV)
+    n, S, every, seed = 90000, 40, 8, 7
+    x, snaps = m.sample_trajectory(y, n, S, every, seed=seed, precision=precision)
+    assert tuple(snaps.shape) == (S // every, 2, n, xd)
+    assert torch.equal(snaps[-1], x)
+    assert torch.isfinite(snaps).all()
+    assert torch.equal(m.sample_device(y, n, S, seed=seed, precision=precision), x)
+    lo, hi = 30011, 61000
+    xs, ss = m.sample_trajectory(y, hi - lo, S, every, seed=seed, chain_offset=lo, precision=precision)
+    assert torch.equal(ss, snaps[:, :, lo:hi]) and torch.equal(xs, x[:, lo:hi])
+    # snapshots move: consecutive states differ
+    assert not torch.equal(snaps[0], snaps[1])
