@@ -34,7 +34,8 @@ EXPORTED = (
     "dmip_loss_grad_supported", "dmip_histogram", "dmip_surrogate_create", "dmip_surrogate_destroy",
     "dmip_surrogate_forward", "dmip_log_posterior", "dmip_mh_sample", "dmip_dps_sample", "dmip_device_status",
     "dmip_sampler_supported_f32", "dmip_posterior_loss_grad", "dmip_loss_grad_f32", "dmip_train_draws",
-    "dmip_adam_step", "dmip_em_sample_snapshots",
+    "dmip_adam_step", "dmip_em_sample_snapshots", "dmip_train_plan_create", "dmip_train_plan_step",
+    "dmip_train_plan_set_counters", "dmip_train_plan_destroy",
 )
 DMIP_DPS_NLL, DMIP_DPS_NORM = 0, 1
 
@@ -47,6 +48,20 @@ class DmipLossCfg(ctypes.Structure):
     _fields_ = [("kind", ctypes.c_int), ("pde", ctypes.c_int), ("pde_metric", ctypes.c_int),
                 ("ic_metric", ctypes.c_int), ("lam", ctypes.c_float), ("lam2", ctypes.c_float),
                 ("ic_A", ctypes.c_float * 4), ("ic_b", ctypes.c_float * 2), ("ic_Sinv", ctypes.c_float * 4)]
+
+
+class DmipTrainPlanDesc(ctypes.Structure):
+    """dmip_train_plan_desc (include/dmip.h)."""
+    _fields_ = [("in_dim", ctypes.c_int), ("out_dim", ctypes.c_int), ("n_hidden", ctypes.c_int),
+                ("widths", ctypes.c_void_p), ("xdim", ctypes.c_int), ("weights_dev", ctypes.c_void_p),
+                ("biases_dev", ctypes.c_void_p), ("sde", DmipVpsde), ("cfg", DmipLossCfg),
+                ("precision", ctypes.c_int), ("batch", ctypes.c_int64), ("seed", ctypes.c_uint64),
+                ("first_draw", ctypes.c_uint64), ("debias", ctypes.c_int), ("t_epsilon", ctypes.c_double),
+                ("t_add", ctypes.c_float), ("n_tensors", ctypes.c_int), ("params", ctypes.c_void_p),
+                ("grads", ctypes.c_void_p), ("exp_avg", ctypes.c_void_p), ("exp_avg_sq", ctypes.c_void_p),
+                ("numel", ctypes.c_void_p), ("lr", ctypes.c_double), ("beta1", ctypes.c_double),
+                ("beta2", ctypes.c_double), ("eps", ctypes.c_double), ("step0", ctypes.c_int64),
+                ("t_dev", ctypes.c_void_p), ("eps_dev", ctypes.c_void_p), ("loss_dev", ctypes.c_void_p)]
 
 
 class DmipScatNoise(ctypes.Structure):
@@ -101,6 +116,11 @@ def _declare(lib):
         lib.dmip_em_sample_snapshots.argtypes = [_i32, _c_void_p, _c_void_p, ctypes.POINTER(DmipVpsde), _c_void_p, _i32,
                                                  _i32, _i32, _i64, _i64, _i32, _f32, _f32, _u64, _i32, _i32, _f32,
                                                  _i32, _c_void_p, _c_void_p, _c_void_p]
+    if hasattr(lib, "dmip_train_plan_create"):
+        lib.dmip_train_plan_create.argtypes = [ctypes.POINTER(DmipTrainPlanDesc), ctypes.POINTER(_c_void_p)]
+        lib.dmip_train_plan_step.argtypes = [_c_void_p, _c_void_p, _c_void_p, _c_void_p]
+        lib.dmip_train_plan_set_counters.argtypes = [_c_void_p, _u64, _i64, _c_void_p]
+        lib.dmip_train_plan_destroy.argtypes = [_c_void_p]
     lib.dmip_loss_grad.argtypes = [_i32, _i32, _i32, ctypes.POINTER(_i32), _i32, ctypes.POINTER(_c_void_p),
                                    ctypes.POINTER(_c_void_p), ctypes.POINTER(DmipVpsde), ctypes.POINTER(DmipLossCfg),
                                    _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _c_void_p, _c_void_p,

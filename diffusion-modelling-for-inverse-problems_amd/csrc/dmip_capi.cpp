@@ -757,10 +757,22 @@ int dmip_loss_grad_supported(int in_dim, int out_dim, int n_hidden, const int* w
   return train_shape_ok(in_dim, out_dim, n_hidden, widths, xdim) ? 1 : 0;
 }
 
-int dmip_loss_grad(int in_dim, int out_dim, int n_hidden, const int* widths, int xdim,
-                   const float* const* weights_dev, const float* const* biases_dev, const dmip_vpsde* sde,
-                   const dmip_loss_cfg* cfg, const float* x_dev, const float* y_dev, const float* t_dev,
-                   const float* eps_dev, int64_t batch, float* grad_out_dev, float* loss_out_dev, void* stream) {
+}  // extern "C"
+
+// Scratch of a loss + gradient launch sequence: null = stream-ordered allocation per call (the C-ABI
+// entry points); query = report the bytes only (no launch); else the caller's persistent buffer (the
+// captured training-step graph, dmip_train_plan).
+struct Workspace {
+  char* ptr = nullptr;
+  size_t bytes = 0;
+  bool query = false;
+};
+
+static int loss_grad_bf16_impl(int in_dim, int out_dim, int n_hidden, const int* widths, int xdim,
+                               const float* const* weights_dev, const float* const* biases_dev, const dmip_vpsde* sde,
+                               const dmip_loss_cfg* cfg, const float* x_dev, const float* y_dev, const float* t_dev,
+                               const float* eps_dev, int64_t batch, float* grad_out_dev, float* loss_out_dev,
+                               void* stream, Workspace* ws) {
   if (!weights_dev || !biases_dev || !sde || !cfg || !x_dev || !y_dev || !t_dev || !eps_dev || !grad_out_dev ||
       !loss_out_dev)
     return fail(DMIP_ERR_INVALID, "null argument");
@@ -810,21 +822,31 @@ int dmip_loss_grad(int in_dim, int out_dim, int n_hidden, const int* widths, int
       (size_t)n_wg * dmip::train_partials_per_wg() * dmip::train_partial_stride(n_hidden) * sizeof(float);
   // one scratch allocation: the partial rows, then the packed LDS image of the weights
   const size_t part_pad = (part_bytes + 255) / 256 * 256;
+  const size_t need = part_pad + (size_t)dmip::train_packed_bytes(n_hidden);
+  if (ws && ws->query) {
+    ws->bytes = need;
+    return DMIP_OK;
+  }
   float* partials = nullptr;
-  hipError_t e = hipMallocAsync((void**)&partials, part_pad + (size_t)dmip::train_packed_bytes(n_hidden), st);
-  if (e != hipSuccess) return fail(DMIP_ERR_ALLOC, std::string("hipMallocAsync: ") + hipGetErrorString(e));
+  hipError_t e = hipSuccess;
+  if (ws) {
+    if (ws->bytes < need) return fail(DMIP_ERR_INVALID, "workspace too small");
+    partials = (float*)ws->ptr;
+  } else if ((e = hipMallocAsync((void**)&partials, need, st)) != hipSuccess) {
+    return fail(DMIP_ERR_ALLOC, std::string("hipMallocAsync: ") + hipGetErrorString(e));
+  }
   p.packed = (char*)partials + part_pad;
   e = dmip::launch_loss_grad(p, n_hidden, grad_out_dev, loss_out_dev, partials, n_wg, st);
-  (void)hipFreeAsync(partials, st);
+  if (!ws) (void)hipFreeAsync(partials, st);
   if (e != hipSuccess) return hip_fail(e, "loss_grad launch");
   return DMIP_OK;
 }
 
-int dmip_loss_grad_f32(int in_dim, int out_dim, int n_hidden, const int* widths, int xdim,
-                       const float* const* weights_dev, const float* const* biases_dev, const dmip_vpsde* sde,
-                       const dmip_loss_cfg* cfg, const float* x_dev, const float* y_dev, const float* t_dev,
-                       const float* eps_dev, const float* ic_target_dev, int64_t batch, float* grad_out_dev,
-                       float* loss_out_dev, void* stream) {
+static int loss_grad_f32_impl(int in_dim, int out_dim, int n_hidden, const int* widths, int xdim,
+                              const float* const* weights_dev, const float* const* biases_dev, const dmip_vpsde* sde,
+                              const dmip_loss_cfg* cfg, const float* x_dev, const float* y_dev, const float* t_dev,
+                              const float* eps_dev, const float* ic_target_dev, int64_t batch, float* grad_out_dev,
+                              float* loss_out_dev, void* stream, Workspace* ws) {
   if (!widths || !weights_dev || !biases_dev || !sde || !cfg || !x_dev || !y_dev || !t_dev || !eps_dev ||
       !grad_out_dev || !loss_out_dev)
     return fail(DMIP_ERR_INVALID, "null argument");
@@ -880,7 +902,7 @@ int dmip_loss_grad_f32(int in_dim, int out_dim, int n_hidden, const int* widths,
   p.n_streams = p.n_bwd + p.n_e + p.n_pair;
   int wmax = in_dim + 1;
   for (int i = 0; i < n_hidden; ++i) wmax = std::max(wmax, widths[i] + 1);
-  p.splits = (int)std::max<int64_t>(1, std::min<int64_t>(64, (int64_t)p.n_bwd * B / 4096));
+  p.splits = 64;  // the cap: each weight-gradient GEMM picks its own split count (dmip_jets.hip wgrad_splits)
   const int64_t nS = p.n_streams, nb = p.n_bwd;
   std::vector<std::pair<float**, size_t>> plan;
   for (int l = 0; l <= n_hidden; ++l) plan.emplace_back(&p.h[l], (size_t)nS * B * ((l == 0 ? in_dim : widths[l - 1]) + 1));
@@ -897,9 +919,18 @@ int dmip_loss_grad_f32(int in_dim, int out_dim, int n_hidden, const int* widths,
   plan.emplace_back(&p.part, (size_t)p.splits * wmax * wmax);
   size_t total = 0;
   for (auto& q : plan) total += (q.second * sizeof(float) + 255) / 256 * 256;
+  if (ws && ws->query) {
+    ws->bytes = total;
+    return DMIP_OK;
+  }
   char* scratch = nullptr;
-  hipError_t e = hipMallocAsync((void**)&scratch, total, st);
-  if (e != hipSuccess) return fail(DMIP_ERR_ALLOC, std::string("hipMallocAsync: ") + hipGetErrorString(e));
+  hipError_t e = hipSuccess;
+  if (ws) {
+    if (ws->bytes < total) return fail(DMIP_ERR_INVALID, "workspace too small");
+    scratch = ws->ptr;
+  } else if ((e = hipMallocAsync((void**)&scratch, total, st)) != hipSuccess) {
+    return fail(DMIP_ERR_ALLOC, std::string("hipMallocAsync: ") + hipGetErrorString(e));
+  }
   size_t o = 0;
   for (auto& q : plan) {
     *q.first = (float*)(scratch + o);
@@ -907,18 +938,38 @@ int dmip_loss_grad_f32(int in_dim, int out_dim, int n_hidden, const int* widths,
   }
   p.loss_out = loss_out_dev;
   e = dmip::launch_jets_loss_grad(p, n_hidden, widths, weights_dev, biases_dev, grad_out_dev, st);
-  (void)hipFreeAsync(scratch, st);
+  if (!ws) (void)hipFreeAsync(scratch, st);
   if (e != hipSuccess) return hip_fail(e, "loss_grad_f32 launch");
   return DMIP_OK;
 }
 
-int dmip_train_draws(uint64_t seed, uint64_t stream_id, int64_t batch, int xdim, int debias, const dmip_vpsde* sde,
-                     double t_epsilon, float t_add, float* t_out_dev, float* eps_out_dev, void* stream) {
+extern "C" {
+
+int dmip_loss_grad(int in_dim, int out_dim, int n_hidden, const int* widths, int xdim,
+                   const float* const* weights_dev, const float* const* biases_dev, const dmip_vpsde* sde,
+                   const dmip_loss_cfg* cfg, const float* x_dev, const float* y_dev, const float* t_dev,
+                   const float* eps_dev, int64_t batch, float* grad_out_dev, float* loss_out_dev, void* stream) {
+  return loss_grad_bf16_impl(in_dim, out_dim, n_hidden, widths, xdim, weights_dev, biases_dev, sde, cfg, x_dev,
+                             y_dev, t_dev, eps_dev, batch, grad_out_dev, loss_out_dev, stream, nullptr);
+}
+
+int dmip_loss_grad_f32(int in_dim, int out_dim, int n_hidden, const int* widths, int xdim,
+                       const float* const* weights_dev, const float* const* biases_dev, const dmip_vpsde* sde,
+                       const dmip_loss_cfg* cfg, const float* x_dev, const float* y_dev, const float* t_dev,
+                       const float* eps_dev, const float* ic_target_dev, int64_t batch, float* grad_out_dev,
+                       float* loss_out_dev, void* stream) {
+  return loss_grad_f32_impl(in_dim, out_dim, n_hidden, widths, xdim, weights_dev, biases_dev, sde, cfg, x_dev, y_dev,
+                            t_dev, eps_dev, ic_target_dev, batch, grad_out_dev, loss_out_dev, stream, nullptr);
+}
+
+}  // extern "C"
+
+static int draws_params(uint64_t seed, uint64_t stream_id, int64_t batch, int xdim, int debias, const dmip_vpsde* sde,
+                        double t_epsilon, float t_add, float* t_out_dev, float* eps_out_dev, dmip::TrainDrawsParams& p) {
   if (!sde || !t_out_dev || !eps_out_dev) return fail(DMIP_ERR_INVALID, "null argument");
   if (batch < 0 || xdim < 1 || xdim > 4) return fail(DMIP_ERR_INVALID, "batch >= 0 and xdim in [1, 4]");
   if (!(sde->T > 0.0) || !(sde->beta_min > 0.0)) return fail(DMIP_ERR_INVALID, "bad SDE parameters");
-  if (batch == 0) return DMIP_OK;
-  dmip::TrainDrawsParams p{};
+  p = dmip::TrainDrawsParams{};
   p.batch = batch;
   p.xdim = xdim;
   p.debias = debias ? 1 : 0;
@@ -939,18 +990,17 @@ int dmip_train_draws(uint64_t seed, uint64_t stream_id, int64_t batch, int xdim,
   p.Z = (float)(te * r_te + std::log(std::expm1(B_T)) - A_te);
   p.t = t_out_dev;
   p.eps = eps_out_dev;
-  hipError_t e = dmip::launch_train_draws(p, (hipStream_t)stream);
-  return e == hipSuccess ? DMIP_OK : hip_fail(e, "train_draws launch");
+  return DMIP_OK;
 }
 
-int dmip_adam_step(int n_tensors, float* const* params, const float* const* grads, float* const* exp_avg,
-                   float* const* exp_avg_sq, const int64_t* numel, double lr, double beta1, double beta2, double eps,
-                   int64_t step, void* stream) {
+static int adam_params(int n_tensors, float* const* params, const float* const* grads, float* const* exp_avg,
+                       float* const* exp_avg_sq, const int64_t* numel, double lr, double beta1, double beta2,
+                       double eps, int64_t step, dmip::AdamParams& p) {
   if (!params || !grads || !exp_avg || !exp_avg_sq || !numel) return fail(DMIP_ERR_INVALID, "null argument");
   if (n_tensors < 1 || n_tensors > dmip::kAdamMaxTensors)
     return fail(DMIP_ERR_UNSUPPORTED, "n_tensors must be in [1, 16]");
   if (step < 1) return fail(DMIP_ERR_INVALID, "step must be >= 1 (torch increments before the update)");
-  dmip::AdamParams p{};
+  p = dmip::AdamParams{};
   p.n = n_tensors;
   p.off[0] = 0;
   for (int k = 0; k < n_tensors; ++k) {
@@ -970,8 +1020,175 @@ int dmip_adam_step(int n_tensors, float* const* params, const float* const* grad
   p.beta2 = (float)beta2;
   p.w2 = (float)(1.0 - beta2);
   p.eps = (float)eps;
+  p.lr_d = lr;
+  p.beta1_d = beta1;
+  p.beta2_d = beta2;
+  return DMIP_OK;
+}
+
+// ----------------------------------------------------------------- captured training-step graph
+struct dmip_train_plan {
+  hipGraphExec_t exec = nullptr;
+  int64_t batch = 0;
+  int xdim = 0, ydim = 0;
+  float *x = nullptr, *y = nullptr;          // staging: the batch is copied in before each replay
+  float *t = nullptr, *eps = nullptr, *loss = nullptr;  // caller-owned
+  char* ws = nullptr;
+  dmip::StepCounters* ctr = nullptr;
+  int device = 0;
+};
+
+static void plan_free(dmip_train_plan* pl) {
+  if (!pl) return;
+  if (pl->exec) (void)hipGraphExecDestroy(pl->exec);
+  for (void* q : {(void*)pl->x, (void*)pl->y, (void*)pl->ws, (void*)pl->ctr})
+    if (q) (void)hipFree(q);
+  delete pl;
+}
+
+extern "C" {
+
+int dmip_train_draws(uint64_t seed, uint64_t stream_id, int64_t batch, int xdim, int debias, const dmip_vpsde* sde,
+                     double t_epsilon, float t_add, float* t_out_dev, float* eps_out_dev, void* stream) {
+  dmip::TrainDrawsParams p{};
+  const int rc = draws_params(seed, stream_id, batch, xdim, debias, sde, t_epsilon, t_add, t_out_dev, eps_out_dev, p);
+  if (rc != DMIP_OK || batch == 0) return rc;
+  hipError_t e = dmip::launch_train_draws(p, (hipStream_t)stream);
+  return e == hipSuccess ? DMIP_OK : hip_fail(e, "train_draws launch");
+}
+
+int dmip_adam_step(int n_tensors, float* const* params, const float* const* grads, float* const* exp_avg,
+                   float* const* exp_avg_sq, const int64_t* numel, double lr, double beta1, double beta2, double eps,
+                   int64_t step, void* stream) {
+  dmip::AdamParams p{};
+  const int rc = adam_params(n_tensors, params, grads, exp_avg, exp_avg_sq, numel, lr, beta1, beta2, eps, step, p);
+  if (rc != DMIP_OK) return rc;
   hipError_t e = dmip::launch_adam(p, (hipStream_t)stream);
   return e == hipSuccess ? DMIP_OK : hip_fail(e, "adam launch");
+}
+
+int dmip_train_plan_create(const dmip_train_plan_desc* d, dmip_train_plan** out) {
+  if (!d || !out || !d->widths || !d->weights_dev || !d->biases_dev || !d->t_dev || !d->eps_dev || !d->loss_dev)
+    return fail(DMIP_ERR_INVALID, "null argument");
+  *out = nullptr;
+  if (d->batch < 1) return fail(DMIP_ERR_INVALID, "batch must be >= 1");
+  if (d->precision != DMIP_PREC_BF16 && d->precision != DMIP_PREC_F32) return fail(DMIP_ERR_INVALID, "unknown precision");
+  const int ydim = d->in_dim - d->xdim - 1;
+  if (d->xdim < 1 || d->xdim > 4 || ydim < 0) return fail(DMIP_ERR_INVALID, "xdim in [1, 4] and in_dim = xdim + ydim + 1");
+  const bool has_ic = d->cfg.kind == DMIP_LOSS_PINN || d->cfg.kind == DMIP_LOSS_PINN2;
+  if (has_ic && (d->xdim != 2 || ydim != 2))
+    return fail(DMIP_ERR_UNSUPPORTED, "captured steps take the built-in (linear-problem) initial condition only");
+  const bool bf16 = d->precision == DMIP_PREC_BF16;
+  if (bf16 && !train_shape_ok(d->in_dim, d->out_dim, d->n_hidden, d->widths, d->xdim))
+    return fail(DMIP_ERR_UNSUPPORTED, "no compiled bf16 training kernel for this network");
+  dmip::AdamParams ap{};
+  int rc = adam_params(d->n_tensors, d->params, d->grads, d->exp_avg, d->exp_avg_sq, d->numel, d->lr, d->beta1,
+                       d->beta2, d->eps, 1, ap);
+  if (rc != DMIP_OK) return rc;
+  for (int k = 1; k < d->n_tensors; ++k)
+    if (d->grads[k] != d->grads[0] + ap.off[k])
+      return fail(DMIP_ERR_INVALID, "grads must be consecutive views of one flat buffer (reference parameter order)");
+  auto* pl = new dmip_train_plan();
+  pl->batch = d->batch;
+  pl->xdim = d->xdim;
+  pl->ydim = ydim;
+  pl->t = d->t_dev;
+  pl->eps = d->eps_dev;
+  pl->loss = d->loss_dev;
+  (void)hipGetDevice(&pl->device);
+  const int64_t B = d->batch;
+  auto alloc = [&](void** q, size_t bytes) { return hipMalloc(q, bytes < 4 ? 4 : bytes); };
+  hipError_t e = hipSuccess;
+  if ((e = alloc((void**)&pl->x, (size_t)B * d->xdim * 4)) != hipSuccess ||
+      (e = alloc((void**)&pl->y, (size_t)B * ydim * 4)) != hipSuccess ||
+      (e = alloc((void**)&pl->ctr, sizeof(dmip::StepCounters))) != hipSuccess) {
+    plan_free(pl);
+    return fail(DMIP_ERR_ALLOC, std::string("hipMalloc: ") + hipGetErrorString(e));
+  }
+  dmip::StepCounters c0{0ull, (long long)d->step0};
+  if ((e = hipMemcpy(pl->ctr, &c0, sizeof(c0), hipMemcpyHostToDevice)) != hipSuccess) {
+    plan_free(pl);
+    return hip_fail(e, "counter init");
+  }
+  // workspace of the loss sequence, sized by a query pass
+  Workspace ws;
+  ws.query = true;
+  auto loss_seq = [&](hipStream_t st, Workspace* w) {
+    return bf16 ? loss_grad_bf16_impl(d->in_dim, d->out_dim, d->n_hidden, d->widths, d->xdim, d->weights_dev,
+                                      d->biases_dev, &d->sde, &d->cfg, pl->x, pl->y, pl->t, pl->eps, B,
+                                      d->grads[0], pl->loss, st, w)
+                : loss_grad_f32_impl(d->in_dim, d->out_dim, d->n_hidden, d->widths, d->xdim, d->weights_dev,
+                                     d->biases_dev, &d->sde, &d->cfg, pl->x, pl->y, pl->t, pl->eps, nullptr, B,
+                                     d->grads[0], pl->loss, st, w);
+  };
+  if ((rc = loss_seq(nullptr, &ws)) != DMIP_OK) {
+    plan_free(pl);
+    return rc;
+  }
+  if ((e = alloc((void**)&pl->ws, ws.bytes)) != hipSuccess) {
+    plan_free(pl);
+    return fail(DMIP_ERR_ALLOC, std::string("hipMalloc: ") + hipGetErrorString(e));
+  }
+  ws.ptr = pl->ws;
+  ws.query = false;
+  dmip::TrainDrawsParams dp{};
+  if ((rc = draws_params(d->seed, d->first_draw, B, d->xdim, d->debias, &d->sde, d->t_epsilon, d->t_add, pl->t,
+                         pl->eps, dp)) != DMIP_OK) {
+    plan_free(pl);
+    return rc;
+  }
+  dp.draw_ctr = &pl->ctr->draw;
+  ap.step_ctr = &pl->ctr->step;
+  // capture: draws -> loss + gradients -> Adam -> advance the counters
+  hipStream_t cs = nullptr;
+  if ((e = hipStreamCreateWithFlags(&cs, hipStreamNonBlocking)) != hipSuccess) {
+    plan_free(pl);
+    return hip_fail(e, "capture stream");
+  }
+  hipGraph_t g = nullptr;
+  e = hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed);
+  if (e == hipSuccess) {
+    hipError_t le = dmip::launch_train_draws(dp, cs);
+    int lrc = le == hipSuccess ? loss_seq(cs, &ws) : DMIP_ERR_HIP;
+    if (lrc == DMIP_OK && (le = dmip::launch_adam(ap, cs)) == hipSuccess) le = dmip::launch_counters_advance(pl->ctr, cs);
+    e = hipStreamEndCapture(cs, &g);
+    if (e == hipSuccess && (le != hipSuccess || lrc != DMIP_OK)) e = le != hipSuccess ? le : hipErrorUnknown;
+  }
+  if (e == hipSuccess) e = hipGraphInstantiate(&pl->exec, g, nullptr, nullptr, 0);
+  if (g) (void)hipGraphDestroy(g);
+  (void)hipStreamDestroy(cs);
+  if (e != hipSuccess) {
+    plan_free(pl);
+    return hip_fail(e, "training-step graph capture");
+  }
+  *out = pl;
+  return DMIP_OK;
+}
+
+int dmip_train_plan_step(dmip_train_plan* pl, const float* x_dev, const float* y_dev, void* stream) {
+  if (!pl || !x_dev || (pl->ydim > 0 && !y_dev)) return fail(DMIP_ERR_INVALID, "null argument");
+  hipStream_t st = (hipStream_t)stream;
+  hipError_t e = hipMemcpyAsync(pl->x, x_dev, (size_t)pl->batch * pl->xdim * 4, hipMemcpyDeviceToDevice, st);
+  if (e == hipSuccess && pl->ydim > 0)
+    e = hipMemcpyAsync(pl->y, y_dev, (size_t)pl->batch * pl->ydim * 4, hipMemcpyDeviceToDevice, st);
+  if (e == hipSuccess) e = hipGraphLaunch(pl->exec, st);
+  return e == hipSuccess ? DMIP_OK : hip_fail(e, "training-step graph launch");
+}
+
+int dmip_train_plan_set_counters(dmip_train_plan* pl, uint64_t draws_done, int64_t steps_done, void* stream) {
+  if (!pl) return fail(DMIP_ERR_INVALID, "null argument");
+  if (steps_done < 0) return fail(DMIP_ERR_INVALID, "steps_done must be >= 0");
+  // stream-ordered after earlier replays; the source is copied before this call returns
+  const dmip::StepCounters c{(unsigned long long)draws_done, (long long)steps_done};
+  hipError_t e = hipMemcpyAsync(pl->ctr, &c, sizeof(c), hipMemcpyHostToDevice, (hipStream_t)stream);
+  if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)stream);
+  return e == hipSuccess ? DMIP_OK : hip_fail(e, "counter update");
+}
+
+int dmip_train_plan_destroy(dmip_train_plan* pl) {
+  if (pl) (void)hipDeviceSynchronize();  // no replay may still be running
+  plan_free(pl);
+  return DMIP_OK;
 }
 
 int dmip_histogram(const float* x_dev, int64_t n, int d, int nbins, double lo, double hi, int n_hist,
@@ -1279,7 +1496,8 @@ hipError_t mlp_backward_f32(const MlpDims& dm, const float* const* W, const MlpT
       g.epi = dmip::GEMM_EPI_WGRAD;
       g.bias_out = grads + off[l] + (size_t)dm.out[l] * dm.in[l];
       g.part = part;
-      if ((e = dmip::launch_gemm_f32(g, true, false, splits, st)) != hipSuccess) return e;
+      if ((e = dmip::launch_gemm_f32(g, true, false, dmip::gemm_wgrad_splits(g.m, g.n, g.k, splits), st)) != hipSuccess)
+        return e;
     }
     if (l == 0 && !in_grad) break;
     dmip::GemmParams g{};
@@ -1345,7 +1563,7 @@ int dmip_posterior_loss_grad(int xdim, int ydim, int n_hidden, const int* widths
   }
   int wmax = xdim + ydim + 2;
   for (int i = 0; i < n_hidden; ++i) wmax = std::max(wmax, widths[i] + 1);
-  const int splits = (int)std::max<int64_t>(1, std::min<int64_t>(64, B / 2048));
+  const int splits = 64;  // the cap of every weight-gradient GEMM's own split count (gemm_wgrad_splits)
   // scratch (one allocation, carved in 256-byte aligned pieces)
   std::vector<std::pair<float**, size_t>> plan;
   auto need = [&](float** p, size_t n) { plan.emplace_back(p, n); };

@@ -12,6 +12,8 @@
 #include "dmip_device.h"
 #include "dmip_internal.h"
 
+#include <algorithm>
+
 namespace dmip {
 namespace gemm {
 
@@ -301,6 +303,17 @@ __global__ void ones_column_kernel(float* h, long long rows, int ld) {
 }  // namespace gemm
 
 // ----------------------------------------------------------------------------------- launches
+// K splits of a weight-gradient GEMM (out x (in + 1) over the n_bwd B sample rows): enough workgroups
+// for ~4 per CU at any batch -- a small batch no longer runs its whole sample reduction on the few
+// output tiles' workgroups -- with at least 128 rows per split; at most `cap` (the partial buffer).
+int gemm_wgrad_splits(long long m, long long n, long long k, int cap) {
+  const long long T = (m >= 128 && n >= 128) ? 128 : 64;
+  const long long tiles = ((m + T - 1) / T) * ((n + T - 1) / T);
+  long long s = (1024 + tiles - 1) / tiles;
+  s = std::min(s, std::max(1LL, k / 128));
+  return (int)std::max(1LL, std::min<long long>(s, cap));
+}
+
 hipError_t launch_gemm_f32(const GemmParams& p_in, bool ta, bool tb, int splits, hipStream_t st) {
   GemmParams p = p_in;
   if (p.m <= 0 || p.n <= 0) return hipSuccess;

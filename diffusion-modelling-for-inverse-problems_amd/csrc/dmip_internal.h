@@ -328,6 +328,9 @@ hipError_t launch_jets_loss_grad(const JetsParams& p, int n_hidden, const int* w
                                  const float* const* b, float* grads, hipStream_t st);
 
 hipError_t launch_gemm_f32(const GemmParams& p, bool ta, bool tb, int splits, hipStream_t st);
+// split count of a weight-gradient GEMM [m x n] over k sample rows: ~4 workgroups per CU, >= 128 rows
+// per split, at most cap
+int gemm_wgrad_splits(long long m, long long n, long long k, int cap);
 
 // ---- device-side rest of a training step (dmip_step.hip)
 struct TrainDrawsParams {
@@ -338,6 +341,9 @@ struct TrainDrawsParams {
   float a, b, te, r_te, A_te, Z;  // sample_vp_truncated_q constants (sdes.py), host-computed in f64
   float* t;                       // [B]
   float* eps;                     // [B][xdim]
+  // captured step graphs (dmip_train_plan): the step's draw stream is stream_id + *draw_ctr, read on
+  // the device, so one graph replays every step (null: stream_id alone)
+  const unsigned long long* draw_ctr;
 };
 
 constexpr int kAdamMaxTensors = 16;
@@ -352,7 +358,18 @@ struct AdamParams {
   // torch's scalars, each rounded from Python double as torch passes them: lerp weight 1 - beta1,
   // beta2, addcmul value 1 - beta2, eps, lr / bias_correction1, sqrt(bias_correction2)
   float w1, beta2, w2, eps, step_size, bc2_sqrt;
+  // captured step graphs: the step is *step_ctr + 1 (torch increments before the update) and the
+  // bias corrections are formed on the device in double from lr / beta1 / beta2 (null: the host's)
+  const long long* step_ctr;
+  double lr_d, beta1_d, beta2_d;
 };
+
+// the per-step counters a captured training-step graph advances at its end
+struct StepCounters {
+  unsigned long long draw;  // draws' stream offset
+  long long step;           // optimizer steps taken
+};
+hipError_t launch_counters_advance(StepCounters* c, hipStream_t st);
 
 hipError_t launch_train_draws(const TrainDrawsParams& p, hipStream_t st);
 hipError_t launch_adam(const AdamParams& p, hipStream_t st);

@@ -17,6 +17,7 @@
 #include "dmip_device.h"
 #include "dmip_internal.h"
 
+#include <algorithm>
 #include <vector>
 
 namespace dmip {
@@ -349,7 +350,7 @@ hipError_t launch_jets_loss_grad(const JetsParams& p_in, int n_hidden, const int
     g.epi = GEMM_EPI_WGRAD;
     g.bias_out = grads + poff[l] + (size_t)out_w(l) * in_w(l);
     g.part = p.part;
-    if ((e = launch_gemm_f32(g, true, false, p.splits, st)) != hipSuccess) return e;
+    if ((e = launch_gemm_f32(g, true, false, gemm_wgrad_splits(g.m, g.n, g.k, p.splits), st)) != hipSuccess) return e;
     if (l == 0) break;
     GemmParams h{};
     h.a = zb;

@@ -16,7 +16,8 @@ namespace step {
 __global__ void train_draws_kernel(TrainDrawsParams p) {
   const long long b = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= p.batch) return;
-  Rng r = rng_init(p.seed, (uint64_t)b, p.stream_id);
+  const unsigned long long sid = p.stream_id + (p.draw_ctr ? *p.draw_ctr : 0ull);
+  Rng r = rng_init(p.seed, (uint64_t)b, sid);
   const float u = (float)(rng_next(r) >> 8) * 0x1p-24f;  // [0, 1)
   float t;
   if (p.debias) {
@@ -57,14 +58,32 @@ __global__ void adam_kernel(AdamParams p) {
   v = __fmul_rn(v, p.beta2) + __fmul_rn(p.w2 * g, g);  // mul_(beta2).addcmul_(g, g, value=w2)
   p.m[k][i] = m;
   p.v[k][i] = v;
-  const float denom = sqrtf(v) / p.bc2_sqrt + p.eps;
-  p.param[k][i] = p.param[k][i] - p.step_size * (m / denom);
+  float step_size = p.step_size, bc2_sqrt = p.bc2_sqrt;
+  if (p.step_ctr) {  // torch's scalars in double, as the host path forms them
+    const double step = (double)(*p.step_ctr + 1);
+    step_size = (float)(p.lr_d / (1.0 - pow(p.beta1_d, step)));
+    bc2_sqrt = (float)sqrt(1.0 - pow(p.beta2_d, step));
+  }
+  const float denom = sqrtf(v) / bc2_sqrt + p.eps;
+  p.param[k][i] = p.param[k][i] - step_size * (m / denom);
+}
+
+__global__ void counters_advance_kernel(StepCounters* c) {
+  if (threadIdx.x == 0) {
+    c->draw += 1;
+    c->step += 1;
+  }
 }
 
 }  // namespace step
 
 hipError_t launch_train_draws(const TrainDrawsParams& p, hipStream_t st) {
   hipLaunchKernelGGL(step::train_draws_kernel, dim3((unsigned)((p.batch + 255) / 256)), dim3(256), 0, st, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_counters_advance(StepCounters* c, hipStream_t st) {
+  hipLaunchKernelGGL(step::counters_advance_kernel, dim3(1), dim3(64), 0, st, c);
   return hipGetLastError();
 }
 

@@ -200,6 +200,53 @@ int dmip_adam_step(int n_tensors, float* const* params, const float* const* grad
                    float* const* exp_avg_sq, const int64_t* numel, double lr, double beta1, double beta2, double eps,
                    int64_t step, void* stream);
 
+/* One whole CDE training step as a captured hipGraph (HIP graphs in place of a tracing compiler): the
+ * step's launches -- dmip_train_draws, the loss + gradients (dmip_loss_grad_f32's sequence, or the bf16
+ * kernel), dmip_adam_step -- recorded once for a fixed batch size with persistent scratch, and replayed
+ * per batch by one hipGraphLaunch after copying the batch into the plan's staging buffers. The per-step
+ * scalars live in a device counter pair the graph advances at its end: the draws' stream id is
+ * first_draw + (steps replayed), Adam's step is step0 + (steps replayed) + 1, with its bias corrections
+ * formed on the device in double. Replaces, per batch, the body of CDE.train_epoch's loop
+ * (models/diffusion.py:76-102: sample_t, base_sde.sample, loss_fn, backward, optimizer.step).
+ *   grads        consecutive views of one flat fp32 buffer in the reference parameter order (the
+ *                loss writes it); params / exp_avg / exp_avg_sq / numel as dmip_adam_step
+ *   cfg          as dmip_loss_grad_f32, with the built-in (linear-problem) initial condition only
+ *   t_dev [batch], eps_dev [batch][xdim], loss_dev [4] (loss, PDE, IC, DSM): caller-owned device buffers
+ *                the replays write (the latest step's draws and loss) */
+typedef struct dmip_train_plan dmip_train_plan;
+typedef struct {
+  int in_dim, out_dim, n_hidden;
+  const int* widths;
+  int xdim;
+  const float* const* weights_dev;
+  const float* const* biases_dev;
+  dmip_vpsde sde;
+  dmip_loss_cfg cfg;
+  int precision;                       /* DMIP_PREC_F32 (any width) or DMIP_PREC_BF16 (config-5 kernel) */
+  int64_t batch;
+  uint64_t seed, first_draw;           /* draws: (seed, sample, first_draw + step) */
+  int debias;
+  double t_epsilon;
+  float t_add;
+  int n_tensors;
+  float* const* params;
+  float* const* grads;
+  float* const* exp_avg;
+  float* const* exp_avg_sq;
+  const int64_t* numel;
+  double lr, beta1, beta2, eps;
+  int64_t step0;                       /* optimizer steps already taken */
+  float* t_dev;
+  float* eps_dev;
+  float* loss_dev;
+} dmip_train_plan_desc;
+int dmip_train_plan_create(const dmip_train_plan_desc* desc, dmip_train_plan** out);
+int dmip_train_plan_step(dmip_train_plan* plan, const float* x_dev, const float* y_dev, void* stream);
+/* set the counters (draws = the stream offset past first_draw, steps = optimizer steps taken), e.g. after
+ * steps taken outside the plan; synchronises the stream */
+int dmip_train_plan_set_counters(dmip_train_plan* plan, uint64_t draws_done, int64_t steps_done, void* stream);
+int dmip_train_plan_destroy(dmip_train_plan* plan);
+
 /* Non-zero when dmip_loss_grad has a kernel for this network shape. */
 int dmip_loss_grad_supported(int in_dim, int out_dim, int n_hidden, const int* widths, int xdim);
 

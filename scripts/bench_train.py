@@ -3,7 +3,8 @@ plus the exact-f32 engine at the reference configs' hidden_layers [512]*3.
 
 For each (width, precision) it times with HIP events on the launching stream:
   * ms_loss_grad   the fused loss + gradient launch sequence alone (dmip_loss_grad / _f32),
-  * ms_device_step the whole step on the device (training.DeviceTrainStep: dmip_train_draws ->
+  * ms_device_step the whole step on the device as one captured hipGraph (training.DeviceTrainStep ->
+                   dmip_train_plan; ms_device_step_no_graph: launch by launch: dmip_train_draws ->
                    loss + gradients -> dmip_adam_step, no host synchronisation),
   * ms_epoch_step  CDE.train_epoch's step (host t / eps draws, torch Adam, the reference's per-batch
                    loss.item()), host-timed,
@@ -71,11 +72,15 @@ def main():
             kern()
         ms_kernel = timed(kern, a.steps)
         opt = torch.optim.Adam(m.sde.a.parameters(), lr=1e-4)
-        dstep = tr.DeviceTrainStep(m, lf, opt, precision=prec)
-        run = lambda: dstep(x, y)
-        for _ in range(a.warmup):
-            run()
-        ms_dev = timed(run, a.steps)
+        ms_dev_modes = {}
+        for graph in ("0", "1"):  # launch by launch, then the captured hipGraph (dmip_train_plan)
+            os.environ["DMIP_TRAIN_GRAPH"] = graph
+            dstep = tr.DeviceTrainStep(m, lf, opt, precision=prec)
+            run = lambda: dstep(x, y)
+            for _ in range(a.warmup):
+                run()
+            ms_dev_modes[graph] = timed(run, a.steps)
+        ms_dev = ms_dev_modes["1"]
         step = lambda: m.train_epoch(opt, lf, loader)
         for _ in range(a.warmup):
             step()
@@ -87,7 +92,8 @@ def main():
         ms_epoch = (time.perf_counter() - t0) * 1e3 / a.steps
         F = 2 * (5 * width + 2 * width * width + width * 2)
         tf = 16.94 * F * B / (ms_kernel * 1e-3) / 1e12
-        rows[f"w{width}_{prec}"] = {"ms_loss_grad": ms_kernel, "ms_device_step": ms_dev, "ms_epoch_step": ms_epoch,
+        rows[f"w{width}_{prec}"] = {"ms_loss_grad": ms_kernel, "ms_device_step": ms_dev,
+                                    "ms_device_step_no_graph": ms_dev_modes["0"], "ms_epoch_step": ms_epoch,
                                     "device_step_samples_per_s": B / (ms_dev * 1e-3),
                                     "loss_grad_tflops": tf, "frac_of_dense_peak": tf / PEAK[prec]}
     os.environ.pop("DMIP_TRAIN_PRECISION", None)

@@ -109,8 +109,12 @@ def test_adam_step_matches_torch(dmip, foreach):
             assert err < 2e-6, err
 
 
+@pytest.mark.parametrize("graph", ["1", "0"])
 @pytest.mark.parametrize("precision,width", [("fp32", 512), ("fp32", 64), ("bf16", 64)])
-def test_device_step_equals_fused_then_torch_adam(dmip, precision, width):
+def test_device_step_equals_fused_then_torch_adam(dmip, precision, width, graph, monkeypatch):
+    """graph "1": the captured-graph step (dmip_train_plan; two batch sizes, so two plans and a
+    counter re-sync), "0": the launch-by-launch step."""
+    monkeypatch.setenv("DMIP_TRAIN_GRAPH", graph)
     tr = _tr()
     torch.manual_seed(11)
     a = dmip.CDE(2, 2, [width] * 3)
@@ -121,8 +125,10 @@ def test_device_step_equals_fused_then_torch_adam(dmip, precision, width):
     oa = torch.optim.Adam(a.sde.a.parameters(), lr=1e-3)
     ob = torch.optim.Adam(b.sde.a.parameters(), lr=1e-3)
     step = tr.DeviceTrainStep(a, lf, oa, precision=precision)
+    assert step.graph == (graph == "1")
     cfg = tr.fused_config(b, lf)
-    for k, n in enumerate((4096, 4096, 1000)):
+    n_plan = dmip._lib.calls.get("train_plan_step", 0)
+    for k, n in enumerate((4096, 4096, 1000, 4096)):
         x, y = _lin_data(n, k)
         out = step(x, y).clone()
         loss_b, _ = tr.fused_loss_grad(b, lf, cfg, x, y, step.t.clone(), step.eps.clone(), precision=precision)
@@ -131,7 +137,36 @@ def test_device_step_equals_fused_then_torch_adam(dmip, precision, width):
     for p, q in zip(a.sde.a.parameters(), b.sde.a.parameters()):
         err = float((p - q).abs().max() / q.abs().max())
         assert err < 1e-5, err
-    assert int(oa.state[next(a.sde.a.parameters())]["step"]) == 3
+    assert int(oa.state[next(a.sde.a.parameters())]["step"]) == 4
+    assert dmip._lib.calls.get("train_plan_step", 0) - n_plan == (4 if graph == "1" else 0)
+
+
+def test_graph_step_matches_launch_by_launch_step(dmip, monkeypatch):
+    """The captured step replays the launch-by-launch step: same draws (stream id from the device
+    counter), same loss, parameters equal to 1e-6 relative after 6 steps over two batch sizes (Adam's
+    bias corrections in device vs host double pow)."""
+    tr = _tr()
+    sp = dmip.LinearForwardProblem().score_posterior
+    lf = dmip.PINNLoss(sp, lam=1e-3, lam2=0.1, pde_loss="FPE", ic_metric="L2", pde_metric="L1")
+    runs = {}
+    for graph in ("1", "0"):
+        monkeypatch.setenv("DMIP_TRAIN_GRAPH", graph)
+        torch.manual_seed(3)
+        m = dmip.CDE(2, 2, [512] * 3)
+        opt = torch.optim.Adam(m.sde.a.parameters(), lr=1e-3)
+        st = tr.DeviceTrainStep(m, lf, opt)
+        losses, ts = [], []
+        for k, n in enumerate((1000, 1000, 1000, 357, 1000, 1000)):
+            x, y = _lin_data(n, 20 + k)
+            losses.append(st(x, y).clone())
+            ts.append(st.t.clone())
+        runs[graph] = (m, [float(v[0]) for v in losses], ts)
+    (ma, la, ta), (mb, lb, tb) = runs["1"], runs["0"]
+    assert all(torch.equal(u, v) for u, v in zip(ta, tb))
+    assert la[0] == lb[0]
+    np.testing.assert_allclose(la, lb, rtol=1e-5)
+    for p, q in zip(ma.sde.a.parameters(), mb.sde.a.parameters()):
+        assert float((p - q).abs().max() / q.abs().max()) < 1e-6
 
 
 def test_train_epoch_device_step(dmip, monkeypatch):
@@ -150,6 +185,7 @@ def test_train_epoch_device_step(dmip, monkeypatch):
     x, y = _lin_data(2048, 1)
     before = [p.detach().clone() for p in m.sde.a.parameters()]
     n0 = dmip._lib.calls.get("loss_grad_f32", 0)
+    p0 = dmip._lib.calls.get("train_plan_step", 0)
 
     def loader():
         for i in range(0, 2048, 512):
@@ -157,7 +193,8 @@ def test_train_epoch_device_step(dmip, monkeypatch):
     sp = dmip.LinearForwardProblem().score_posterior
     loss, info = m.train_epoch(opt, dmip.PINNLoss(sp, lam=1e-3, lam2=0.1, pde_loss="FPE", ic_metric="L2",
                                                   pde_metric="L1"), loader)
-    assert dmip._lib.calls["loss_grad_f32"] - n0 == 4 and calls["n"] == 0
+    n_fused = dmip._lib.calls.get("loss_grad_f32", 0) - n0 + dmip._lib.calls.get("train_plan_step", 0) - p0
+    assert n_fused == 4 and calls["n"] == 0
     assert np.isfinite(float(loss)) and set(info) == {"PDE-Loss", "Initial Condition", "DSM-Loss"}
     assert all(not torch.equal(p, q) for p, q in zip(m.sde.a.parameters(), before))
     assert int(opt.state[next(m.sde.a.parameters())]["step"]) == 4
