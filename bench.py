@@ -283,7 +283,7 @@ def other_configs(args, pkg, lib, dev):
     them (each: one warm-up launch, then timed launches with HIP events): configs[2] CDiffE
     predictor-corrector (the per-GPU share of 1M chains over 8 GPUs), configs[3] DPS (256k samples),
     configs[4] the PINNLoss training step (whole step on the device), and the reference configs'
-    own width [512]*3 for the CDE sampler. Not the headline; errors are reported, not raised."""
+    own width [512]*3 for the CDE and the two-network Posterior samplers. Not the headline; errors are reported, not raised."""
     import copy
     import torch
     out = {}
@@ -297,10 +297,17 @@ def other_configs(args, pkg, lib, dev):
             wl = Workload(a, pkg, dev, 0, 1)
             if workload == "cde" and kw.get("width"):
                 torch.manual_seed(0)
-                wl.model = pkg.CDE(XDIM, YDIM, [kw["width"]] * NH)
+                W = kw["width"]
+                if kw.get("posterior"):  # two networks: likelihood (x, y, t) + prior (x, t)
+                    wl.model = pkg.PosteriorDiffusionEstimator(XDIM, YDIM, [W] * NH)
+                    wl.flops_sample_step = flops_per_sample_step(w=W) + flops_per_sample_step(XDIM + 1, W, NH, XDIM)
+                    wl.kernel = f"em_sampler_kernel<1,{W},3,3,...> (output layers through the ring)"
+                    wl.workload = "PosteriorDiffusionEstimator at the reference width"
+                else:
+                    wl.model = pkg.CDE(XDIM, YDIM, [W] * NH)
+                    wl.flops_sample_step = flops_per_sample_step(w=W)
+                    wl.kernel, wl.workload = f"em_sampler_kernel<0,{W},3,3,...>", "CDE at the reference width"
                 wl.model.sde.a.to(dev)
-                wl.flops_sample_step = flops_per_sample_step(w=kw["width"])
-                wl.kernel, wl.workload = f"em_sampler_kernel<0,{kw['width']},3,3,...>", "CDE at the reference width"
                 wl.weights = "random-init"
             wl.step(3000)
             el, lm, x = timed(wl, reps, None, 1, dev, seed0=3100)
@@ -316,6 +323,7 @@ def other_configs(args, pkg, lib, dev):
     sampler("config3_cdiffe_pc_per_gpu", "cdiffe-pc", 125000, 2)
     sampler("config4_dps", "dps", 262144, 1)
     sampler("cde_reference_width_512", "cde", 100000, 2, width=512)
+    sampler("posterior_reference_width_512", "cde", 100000, 2, width=512, posterior=True)
     try:
         tr = importlib.import_module(PKG + ".training")
         torch.manual_seed(0)

@@ -418,6 +418,9 @@ int dmip_mlp_create(int in_dim, int out_dim, int n_hidden, const int* widths, in
   std::memcpy(ao_sb.data(), ao_s.data(), ao_sb.size());
   std::memcpy(ao_fb.data(), ao_f.data(), ao_fb.size());
   std::memcpy(a1f_b.data(), a1f.data(), a1f_b.size());
+  // the output image also follows the hidden chunks in one buffer: the two-network sampler at width 512
+  // streams it through the weight ring as the network's last chunk (dmip_kernels.hip Lay<AOR>)
+  hid_b.insert(hid_b.end(), ao_sb.begin(), ao_sb.end());
   std::vector<float> w1v(W1, W1 + (size_t)W * IN), b1v(b1, b1 + W);
   if ((rc = upload(&net->hidden, hid_b)) || (rc = upload(&net->ao_samp, ao_sb)) || (rc = upload(&net->ao_full, ao_fb)) ||
       (rc = upload(&net->bias_hidden, bh)) || (rc = upload(&net->bias_out_samp, bo_s)) ||

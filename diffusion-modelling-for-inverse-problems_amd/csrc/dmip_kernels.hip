@@ -22,21 +22,25 @@
 namespace dmip {
 
 // LDS layout of one workgroup: NNET networks (net 0 = the CDE / CDiffE / likelihood net, net 1 =
-// the prior net of the Posterior estimator) share one weight ring.
-template <int W, int NL, int K1S, int NNET, int R, bool RES>
+// the prior net of the Posterior estimator) share one weight ring. AOR: the output layers stream
+// through the ring too (one more chunk per network after its hidden chunks; the host appends the
+// output image to each network's hidden image) -- the two-network sampler at width 512, whose
+// resident output layers (2 x 32 KiB) would not leave room for the ring.
+template <int W, int NL, int K1S, int NNET, int R, bool RES, bool AOR = false>
 struct Lay {
   static constexpr int T = W / 32;            // 32-row tiles per layer
   static constexpr int KS = W / 16;           // 16-deep k-steps over a hidden layer
   static constexpr int CHUNK = KS * 1024;     // one row tile of a W x W layer, bf16 fragments
   static constexpr int NC = (NL - 1) * T;     // hidden chunks per network evaluation
-  static constexpr int NCT = NC * NNET;       // hidden chunks per step (all networks)
+  static constexpr int NCP = NC + (AOR ? 1 : 0);  // ring chunks per network evaluation
+  static constexpr int NCT = NCP * NNET;      // ring chunks per step (all networks)
   static constexpr int A1_BYTES = T * K1S * 1024;
   static constexpr int AO_BYTES = KS * 1024;
   static constexpr int BH_BYTES = (NL - 1) * T * 2 * 16 * 4;
   static constexpr int BO_BYTES = 2 * 16 * 4;  // output bias, summed over the networks
   static constexpr int A1_OFF = 0;
   static constexpr int AO_OFF = A1_OFF + NNET * A1_BYTES;
-  static constexpr int BH_OFF = AO_OFF + NNET * AO_BYTES;
+  static constexpr int BH_OFF = AO_OFF + (AOR ? 0 : NNET * AO_BYTES);
   static constexpr int BO_OFF = BH_OFF + NNET * BH_BYTES;
   static constexpr int W_OFF = BO_OFF + BO_BYTES;
   static constexpr int SLOTS = RES ? NCT : R;
@@ -112,9 +116,10 @@ __device__ __forceinline__ void mfma_row_tile(const char* a_lane_g, const bf16x8
 // compiler-visible lgkmcnt(0) covers it, so the first MFMA waits only for its own fragment.
 // DIAG (timing ablations only, never on the product path): bit 0 = no ring barrier/DMA,
 // bit 1 = hidden activations replaced by a cast, bit 2 = layer-1 activation replaced by a cast.
-template <int W, int NL, int K1S, int NNET, int NW, int R, bool RES, bool CONSERVATIVE, int DIAG = 0>
+template <int W, int NL, int K1S, int NNET, int NW, int R, bool RES, bool CONSERVATIVE, int DIAG = 0,
+          bool AOR = false>
 struct Engine {
-  using L = Lay<W, NL, K1S, NNET, R, RES>;
+  using L = Lay<W, NL, K1S, NNET, R, RES, AOR>;
   static constexpr int T = L::T;
   static constexpr int KS = L::KS;
   static constexpr int PPW = RES ? 1 : KS / NW;
@@ -135,13 +140,13 @@ struct Engine {
     // opaque wave-uniform base, re-materialised at every issue: otherwise the compiler hoists every
     // chunk's 64-bit source address out of the step loop and holds them all in registers (2 VGPRs
     // per chunk with a per-lane address, 2 SGPRs -- spilled to VGPR lanes -- with a constant one)
-    const char* base = c < L::NC ? hidden[0] : hidden[1];
+    const char* base = c < L::NCP ? hidden[0] : hidden[1];
     asm volatile("" : "+s"(base));
     char* dst = lds + L::W_OFF + slot * L::CHUNK;
 #pragma unroll
     for (int q = 0; q < PPW; ++q) {
       const int piece = w * PPW + q;
-      glds16(base + (size_t)(c % L::NC) * L::CHUNK + piece * 1024, dst + piece * 1024, lane);
+      glds16(base + (size_t)(c % L::NCP) * L::CHUNK + piece * 1024, dst + piece * 1024, lane);
     }
   }
 
@@ -227,7 +232,7 @@ struct Engine {
         acc = bias_tile(boff);
       } else {
         acc = bias_tile(boff);
-        wb = chunk_sync((NI * (NL - 1) + LI) * T + rt);
+        wb = chunk_sync(NI * L::NCP + LI * T + rt);
       }
       if (rt == 0) act_carry<TW>(carry, Hin);
       mfma_row_tile<KS, true>(wb + lane * 16, Hin, acc);
@@ -243,8 +248,14 @@ struct Engine {
                                                f32x16& out) {
     if constexpr (LI == NL - 1) {
       asm volatile("" ::: "memory");
-      act_carry<TW>(carry, Ha);
-      mfma_row_tile<KS, true>(lds + L::AO_OFF + NI * L::AO_BYTES + lane * 16, Ha, out);
+      if constexpr (AOR) {
+        const char* wb = chunk_sync(NI * L::NCP + L::NC);
+        act_carry<TW>(carry, Ha);
+        mfma_row_tile<KS, true>(wb + lane * 16, Ha, out);
+      } else {
+        act_carry<TW>(carry, Ha);
+        mfma_row_tile<KS, true>(lds + L::AO_OFF + NI * L::AO_BYTES + lane * 16, Ha, out);
+      }
     } else {
       const f32x16 c2 = hidden_layer<NI, LI, TW>(Ha, carry, Hb);
       hidden_stack<NI, LI + 1, false>(Hb, Ha, c2, out);
@@ -285,7 +296,7 @@ struct Engine {
 #pragma unroll
     for (int ni = 0; ni < NNET; ++ni) {
       stage_blocks<NW>(lds + L::A1_OFF + ni * L::A1_BYTES, a1[ni], T * K1S, w, lane);
-      stage_blocks<NW>(lds + L::AO_OFF + ni * L::AO_BYTES, ao[ni], KS, w, lane);
+      if constexpr (!AOR) stage_blocks<NW>(lds + L::AO_OFF + ni * L::AO_BYTES, ao[ni], KS, w, lane);
       if constexpr (RES) stage_blocks<NW>(lds + L::W_OFF + ni * L::NC * L::CHUNK, hidden[ni], L::NC * KS, w, lane);
       stage_floats((float*)(lds + L::BH_OFF + ni * L::BH_BYTES), bh[ni], L::BH_BYTES / 4, tid, NW * 64);
     }
@@ -379,7 +390,8 @@ struct SamplerLds {
   static constexpr int NNET = MODE == MODE_POSTERIOR ? 2 : 1;
   static constexpr int NV = MODE == MODE_CDIFFE ? D + M + 1 : D + 1;  // inputs that vary per chain
   static constexpr int K1S = k1s_of(3 * NV + 2);
-  using L = Lay<W, NL, K1S, NNET, R, RES>;
+  static constexpr bool AOR = NNET > 1 && W >= 512;  // output layers through the ring (Lay)
+  using L = Lay<W, NL, K1S, NNET, R, RES, AOR>;
   static constexpr int TOTAL = L::TOTAL;
 };
 
@@ -403,7 +415,7 @@ em_sampler_kernel(SamplerParams p) {
   const int h = lane >> 5;
   const int yi = blockIdx.y;
 
-  Engine<W, NL, K1S, NNET, NW, R, RES, NOISE, DIAG> eng{lds, {p.hidden, p.hidden2}, 0, w, lane};
+  Engine<W, NL, K1S, NNET, NW, R, RES, NOISE, DIAG, SL::AOR> eng{lds, {p.hidden, p.hidden2}, 0, w, lane};
   {
     const size_t a1_stride = (size_t)L::T * K1S * 1024;
     const char* const a1[2] = {p.a1 + (p.a1_per_y ? yi * a1_stride : 0), p.a1_2};
@@ -789,7 +801,8 @@ static hipError_t launch_forward_t(const ForwardParams& p, hipStream_t st) {
 }
 
 // Compiled shapes: widths 64 / 128 (hidden layers LDS-resident), 256 (4-slot ring) and 512 (4-wave
-// workgroups, 3 x 32 KiB ring slots; CDE only); 2 or 3 hidden layers; xdim 2 or 3. The CDE and
+// workgroups, 3 x 32 KiB ring slots; CDE, and Posterior with its output layers in the ring); 2 or 3
+// hidden layers; xdim 2 or 3. The CDE and
 // Posterior kernels take any ydim (y is folded into the per-y layer-1 bias, M = 0); CDiffE feeds y_t
 // through layer 1 and is compiled for the two problems' (xdim, ydim) = (2, 2) and (3, 23).
 #define DMIP_W_CASES(X, MODE, NL, D, M) \
@@ -804,7 +817,7 @@ static hipError_t launch_forward_t(const ForwardParams& p, hipStream_t st) {
   W512(X, MODE, 3, 2, M2) W512(X, MODE, 3, 3, M3) W512(X, MODE, 2, 2, M2) W512(X, MODE, 2, 3, M3)
 #define DMIP_ALL_SHAPES(X)                                \
   DMIP_SHAPES(X, MODE_CDE, DMIP_W512_CASE, 0, 0)          \
-  DMIP_SHAPES(X, MODE_POSTERIOR, DMIP_NO_W512, 0, 0)      \
+  DMIP_SHAPES(X, MODE_POSTERIOR, DMIP_W512_CASE, 0, 0)    \
   DMIP_SHAPES(X, MODE_CDIFFE, DMIP_NO_W512, 2, 23)
 
 // Development knob (not part of the ABI): DMIP_SAMPLER_VARIANT=10x runs the timing ablations

@@ -212,9 +212,10 @@ def test_f32_cdiffe_predictor_corrector_vs_oracle(dmip):
     assert np.abs(x - ref).max() < 1e-4 * max(1.0, np.abs(ref).max()), np.abs(x - ref).max()
 
 
-def test_bf16_request_at_width_512_runs_the_fused_f32_kernel(dmip):
-    """The Posterior / CDiffE samplers at the reference configs' width [512]*3 have no bf16 kernel:
-    a bf16 request runs the fused f32 kernel (never the per-step loop)."""
+def test_bf16_request_at_width_512_runs_a_fused_kernel(dmip):
+    """At the reference configs' width [512]*3 the Posterior sampler has a 16-bit kernel (output layers
+    through the weight ring) and CDiffE does not (its 27-input layer 1 alone is 96 KiB): a bf16 request
+    runs a fused kernel either way (never the per-step loop)."""
     torch.manual_seed(2)
     for cls, key in (("PosteriorDiffusionEstimator", "em_sample_posterior"), ("CDiffE", "em_sample_cdiffe")):
         m = getattr(dmip, cls)(3, 23, [512] * 3)

@@ -287,11 +287,12 @@ def _linear_params(net):
             for l in net if isinstance(l, torch.nn.Linear)]
 
 
-@pytest.mark.parametrize("W,NL", [(64, 3), (128, 3), (256, 3), (256, 2)])
+@pytest.mark.parametrize("W,NL", [(64, 3), (128, 3), (256, 3), (256, 2), (512, 3), (512, 2)])
 @pytest.mark.parametrize("xd,yd", [(2, 2), (3, 23)])
 def test_posterior_sampler_vs_oracle_product_rng(dmip, W, NL, xd, yd):
     """Fused two-network kernel (dmip_em_sample_posterior) against the oracle's restatement of the
-    PosteriorScore drift with the same chain-keyed RNG; 6 steps, tolerance as the CDE sampler test."""
+    PosteriorScore drift with the same chain-keyed RNG; 6 steps, tolerance as the CDE sampler test.
+    Width 512 (the reference configs'): both networks' output layers stream through the weight ring."""
     torch.manual_seed(W + xd + NL)
     m = dmip.PosteriorDiffusionEstimator(xd, yd, [W] * NL)
     prior, lik = _linear_params(m.sde.a.prior_net), _linear_params(m.sde.a.likelihood_net)
@@ -608,14 +609,15 @@ def test_balanced_schedule_injected_noise_vs_oracle(dmip, golden):
         assert np.abs(out[sl].cpu().numpy() - ref).max() < 0.05 * max(1.0, np.abs(ref).max())
 
 
-@pytest.mark.parametrize("cls", ["PosteriorDiffusionEstimator", "CDiffE"])
-def test_balanced_schedule_other_samplers(dmip, cls):
+@pytest.mark.parametrize("cls,W", [("PosteriorDiffusionEstimator", 256), ("CDiffE", 256),
+                                   ("PosteriorDiffusionEstimator", 512)])
+def test_balanced_schedule_other_samplers(dmip, cls, W):
     torch.manual_seed(21)
-    m = getattr(dmip, cls)(3, 23, [256] * 3)
+    m = getattr(dmip, cls)(3, 23, [W] * 3)
     y = torch.from_numpy(np.random.default_rng(2).uniform(0, 1, 23).astype(np.float32)).to(DEV)
-    n, S = 70001, 5
+    n, S = (70001, 5) if W == 256 else (40001, 5)  # above one GPU round either way
     full = m.sample_device(y, n, S, seed=3)[0]
-    for lo in (0, 40000, n - 500):
+    for lo in (0, n // 2 + 17, n - 500):
         part = m.sample_device(y, 500, S, seed=3, chain_offset=lo)[0]
         assert torch.equal(full[lo:lo + 500], part), lo
 
