@@ -220,9 +220,12 @@ class _TrainPlan:
         self.k, self.step = None, None  # the device counters' values (unknown until set)
 
     def __del__(self):
-        if getattr(self, "h", None):
-            self.lib.dmip_train_plan_destroy(self.h)
-            self.h = None
+        h, self.h = getattr(self, "h", None), None
+        if h:
+            try:
+                self.lib.dmip_train_plan_destroy(h)
+            except Exception:  # noqa: BLE001 -- interpreter shutdown: the runtime may already be gone
+                pass
 
 
 class DeviceTrainStep:
