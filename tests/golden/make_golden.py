@@ -458,6 +458,38 @@ def gen_posterior_loss(R):
     print("G10 loss", float(loss), {k: float(v) for k, v in info.items()})
 
 
+# ---------------------------------------------------------------------------------------- G12
+def gen_cdiffe_dsm(R):
+    """CDiffE's joint DSM batch loss + backward exactly as CDiffE.train_epoch computes it
+    (models/diffusion.py:128-136: z = [x, y], x_t / y_t from base_sde.sample, score = sde.a(x_t, y_t, t) / g,
+    DSMLoss(...).mean()), with the draws t and eps given (the reference's debiased sample_t needs the
+    un-vendored sdeflow-light). Reference networks, seeded; both problems' shapes."""
+    import torch
+    out = {}
+    for tag, xd, yd, W, seed in (("lin", 2, 2, 64, 51), ("scat", 3, 23, 128, 52)):
+        torch.manual_seed(seed)
+        m = R.diffusion.CDiffE(xd, yd, [W] * 3)
+        B = 512
+        g = torch.Generator().manual_seed(seed + 100)
+        z = torch.randn(B, xd + yd, generator=g)
+        t = (1e-4 + torch.rand(B, 1, generator=g) * (1 - 1e-4)).requires_grad_(True)
+        eps = torch.randn(B, xd + yd, generator=g)
+        sde = m.sde.base_sde
+        std = sde.var(t) ** 0.5
+        diffused = eps * std + sde.mean_weight(t) * z  # base_sde.sample (sdes.py:37-49) with the draw given
+        gt = sde.g(t, diffused)
+        score = m.sde.a(diffused[:, :xd], diffused[:, xd:], t) / gt
+        loss = R.losses.DSMLoss()(score, std, eps).mean()
+        loss.backward()
+        out.update({f"{tag}_z": z.numpy(), f"{tag}_t": t.detach().numpy(), f"{tag}_eps": eps.numpy(),
+                    f"{tag}_loss": float(loss)})
+        out.update(state_to_npz_dict(m.sde.a.state_dict(), f"{tag}_"))
+        for k, prm in m.sde.a.named_parameters():
+            out[f"{tag}_grad_{k.replace('.', '_')}"] = prm.grad.numpy().copy()
+        print("G12", tag, float(loss))
+    np.savez(os.path.join(OUT, "cdiffe_dsm.npz"), **out)
+
+
 # ---------------------------------------------------------------------------------------- G11
 def reference_weights(dims, seed):
     """Layer weights in nn.Linear's default range U(+-1/sqrt(fan_in)) from a numpy seed, so the tests can
@@ -557,6 +589,8 @@ def main():
         gen_surrogate(R)
     if w in ("all", "prior"):
         train_prior(R, a.minutes_prior)
+    if w in ("all", "cdiffe_dsm"):
+        gen_cdiffe_dsm(R)
 
 
 if __name__ == "__main__":

@@ -231,3 +231,21 @@ def test_cdiffe_train_epoch_fused_tracks_autograd(dmip, monkeypatch):
     la, na = run(False)
     assert nf == 4 and na == 0
     assert lf == pytest.approx(la, rel=1e-3)
+
+
+@pytest.mark.parametrize("tag,xd,yd,W", [("lin", 2, 2, 64), ("scat", 3, 23, 128)])
+def test_cdiffe_joint_dsm_vs_reference(dmip, golden, tag, xd, yd, W):
+    """G12: the fused engine's CDiffE DSM loss and gradients against the reference's own
+    (models/diffusion.py:128-136 on the same weights and draws); 1e-4 loss, 2e-3 gradient rel-L2."""
+    z = golden("cdiffe_dsm.npz")
+    m = dmip.CDiffE(xd, yd, [W] * 3)
+    m.sde.a.load_state_dict({k: torch.from_numpy(z[f"{tag}_{k.replace('.', '_')}"])
+                             for k in m.sde.a.state_dict().keys()})
+    lf = dmip.DSMLoss()
+    cfg = _tr().joint_fused_config(m, lf)
+    args = [torch.from_numpy(z[f"{tag}_{k}"]).to(DEV) for k in ("z", "t", "eps")]
+    loss, _ = _tr().fused_loss_grad(m, lf, cfg, args[0], None, args[1], args[2])
+    assert float(loss) == pytest.approx(float(z[f"{tag}_loss"]), rel=1e-4)
+    for name, p in m.sde.a.named_parameters():
+        ref = z[f"{tag}_grad_{name.replace('.', '_')}"]
+        assert _rel(p.grad.detach().cpu().numpy(), ref) < 2e-3, name

@@ -213,3 +213,20 @@ def test_loss_grad_oracle_matches_reference_at_reference_width(golden, tag):
     for li, (dW, db) in zip([0, 3, 5, 7], grads):
         for got, ref in ((dW, z[f"{tag}_grad_{li}_weight"]), (db, z[f"{tag}_grad_{li}_bias"])):
             assert np.linalg.norm(got - ref) < 1e-3 * np.linalg.norm(ref), (li, np.linalg.norm(got - ref) / np.linalg.norm(ref))
+
+
+def _g12_params(z, tag):
+    return [(z[f"{tag}_{k}_weight"], z[f"{tag}_{k}_bias"]) for k in (0, 3, 5, 7)]
+
+
+@pytest.mark.parametrize("tag", ["lin", "scat"])
+def test_cdiffe_joint_dsm_vs_reference(golden, tag):
+    """G12: the oracle's DSM on the joint state z = (x, y) with no condition input (ydim 0) reproduces
+    the reference's CDiffE training loss and every parameter gradient (models/diffusion.py:128-136)."""
+    z = golden("cdiffe_dsm.npz")
+    zz, t, eps = z[f"{tag}_z"], z[f"{tag}_t"], z[f"{tag}_eps"]
+    loss, _, grads = O.loss_grad(_g12_params(z, tag), zz, np.zeros((zz.shape[0], 0), np.float32), t, eps, kind="dsm")
+    assert loss == pytest.approx(float(z[f"{tag}_loss"]), rel=1e-5)
+    for (dW, db), k in zip(grads, (0, 3, 5, 7)):
+        for g, ref in ((dW, z[f"{tag}_grad_{k}_weight"]), (db, z[f"{tag}_grad_{k}_bias"])):
+            assert np.linalg.norm(g - ref) <= 1e-4 * np.linalg.norm(ref) + 1e-7
