@@ -167,6 +167,7 @@ struct dmip_mlp {
   float* bias_out_samp = nullptr; // [2][16]
   float* bias_out_full = nullptr; // [2][16]
   char* a1_full = nullptr;        // [W/32][k1s_full] KiB (every input column varying)
+  char* ring_l1 = nullptr;        // width 512: [layer-1 chunks (split image) | hidden | output] (CDiffE sampler)
   float* w1 = nullptr;            // layer-1 fp32 [W][in_dim] (per-y prep of the sampler's A1)
   float* b1 = nullptr;
   // exact-f32 images of a DPS prior (MLP2 (x, t), x 3, widths [256]*3): dmip_dps_sample
@@ -181,7 +182,7 @@ struct dmip_mlp {
   float* f32_bias = nullptr;      // [(L-1)][W] | [16 f32_ot]
   int f32_k1q = 0, f32_ot = 0;
   ~dmip_mlp() {
-    for (void* p : {(void*)hidden, (void*)ao_samp, (void*)ao_full, (void*)bias_hidden, (void*)bias_out_samp,
+    for (void* p : {(void*)ring_l1, (void*)hidden, (void*)ao_samp, (void*)ao_full, (void*)bias_hidden, (void*)bias_out_samp,
                     (void*)bias_out_full, (void*)a1_full, (void*)w1, (void*)b1, (void*)dps_l1, (void*)dps_w2,
                     (void*)dps_w3, (void*)dps_w4, (void*)dps_bias, (void*)f32_l1, (void*)f32_stream,
                     (void*)f32_bias})
@@ -364,7 +365,7 @@ int dmip_mlp_create(int in_dim, int out_dim, int n_hidden, const int* widths, in
   const int IN = in_dim;
   const bool split = dmip::forward_split(W, IN);
   net->k1s_full = split ? k1s_for(3 * IN + 2) : k1s_for(IN + 2);
-  const int K1S = net->k1s_full;
+  auto pack_a1 = [&](bool split, int K1S) {
   std::vector<uint16_t> a1f((size_t)T * K1S * 512, 0);
   for (int jr = 0; jr < W; ++jr) {
     const int rt = jr / 32, i = jr % 32;
@@ -390,6 +391,9 @@ int dmip_mlp_create(int in_dim, int out_dim, int n_hidden, const int* widths, in
       a1f[(((size_t)(rt * K1S + s)) * 64 + i + 32 * hh) * 8 + jj] = f2bf(val);
     }
   }
+  return a1f;
+  };
+  const std::vector<uint16_t> a1f = pack_a1(split, net->k1s_full);
 
   int rc = DMIP_OK;
   if (input_layout == DMIP_INPUT_X_T && xdim == 3 && in_dim == 4 && out_dim == 3 && L == 3 && W == dmip::kDpsPriorW) {
@@ -421,7 +425,27 @@ int dmip_mlp_create(int in_dim, int out_dim, int n_hidden, const int* widths, in
   // the output image also follows the hidden chunks in one buffer: the two-network sampler at width 512
   // streams it through the weight ring as the network's last chunk (dmip_kernels.hip Lay<AOR>)
   hid_b.insert(hid_b.end(), ao_sb.begin(), ao_sb.end());
+  // the CDiffE sampler at width 512 streams its split layer 1 (3 in + 2 slots, 6 KiB per row tile at
+  // in_dim 27) through the ring as well: [ceil(T / TPC) layer-1 chunks of TPC row tiles | hidden | output]
+  // (dmip_kernels.hip Lay<L1R>)
+  std::vector<char> ring_b;
+  if (W == 512 && input_layout == DMIP_INPUT_X_Y_T) {
+    const int k1s = k1s_for(3 * IN + 2), chunk = (W / 16) * 1024, tpc = chunk / (k1s * 1024);
+    if (tpc >= 1) {
+      const std::vector<uint16_t> a1s = pack_a1(true, k1s);
+      const int l1c = (T + tpc - 1) / tpc;
+      ring_b.assign((size_t)l1c * chunk, 0);
+      for (int rt = 0; rt < T; ++rt)
+        std::memcpy(ring_b.data() + (size_t)(rt / tpc) * chunk + (size_t)(rt % tpc) * k1s * 1024,
+                    (const char*)a1s.data() + (size_t)rt * k1s * 1024, (size_t)k1s * 1024);
+      ring_b.insert(ring_b.end(), hid_b.begin(), hid_b.end());
+    }
+  }
   std::vector<float> w1v(W1, W1 + (size_t)W * IN), b1v(b1, b1 + W);
+  if (!ring_b.empty() && (rc = upload(&net->ring_l1, ring_b))) {
+    delete net;
+    return rc;
+  }
   if ((rc = upload(&net->hidden, hid_b)) || (rc = upload(&net->ao_samp, ao_sb)) || (rc = upload(&net->ao_full, ao_fb)) ||
       (rc = upload(&net->bias_hidden, bh)) || (rc = upload(&net->bias_out_samp, bo_s)) ||
       (rc = upload(&net->bias_out_full, bo_f)) || (rc = upload(&net->a1_full, a1f_b)) ||
@@ -610,10 +634,16 @@ static int em_sample_impl(int mode, const dmip_mlp* net0, const dmip_mlp* net1, 
   hipStream_t st = (hipStream_t)a.stream;
   dmip::SamplerParams p{};
   char* a1 = nullptr;
+  p.hidden = net0->hidden;
   if (mode == DMIP_SAMPLER_CDIFFE) {
-    // y_t varies per chain: layer 1 takes every input column (the forward kernel's image)
+    // y_t varies per chain: layer 1 takes every input column (the forward kernel's image); at width 512
+    // the split layer-1 image streams through the ring ahead of the hidden chunks
     p.a1 = net0->a1_full;
     p.a1_per_y = 0;
+    if (net0->width == 512) {
+      if (!net0->ring_l1) return fail(DMIP_ERR_UNSUPPORTED, "no ring image for this network");
+      p.hidden = net0->ring_l1;
+    }
   } else {
     // y is constant per y index: fold W1_y y + b1 into a per-y layer-1 bias
     const int T = net0->width / 32;
@@ -640,7 +670,6 @@ static int em_sample_impl(int mode, const dmip_mlp* net0, const dmip_mlp* net1, 
     p.a1 = a1;
     p.a1_per_y = 1;
   }
-  p.hidden = net0->hidden;
   p.ao = net0->ao_samp;
   p.bias_hidden = net0->bias_hidden;
   p.bias_out = net0->bias_out_samp;

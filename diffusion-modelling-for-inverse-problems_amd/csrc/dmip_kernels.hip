@@ -25,21 +25,25 @@ namespace dmip {
 // the prior net of the Posterior estimator) share one weight ring. AOR: the output layers stream
 // through the ring too (one more chunk per network after its hidden chunks; the host appends the
 // output image to each network's hidden image) -- the two-network sampler at width 512, whose
-// resident output layers (2 x 32 KiB) would not leave room for the ring.
-template <int W, int NL, int K1S, int NNET, int R, bool RES, bool AOR = false>
+// resident output layers (2 x 32 KiB) would not leave room for the ring. L1R: layer 1 streams through
+// the ring ahead of the hidden chunks, TPC row tiles (K1S KiB each) per chunk -- CDiffE at width 512,
+// whose 27-input split layer 1 is 96 KiB.
+template <int W, int NL, int K1S, int NNET, int R, bool RES, bool AOR = false, bool L1R = false>
 struct Lay {
   static constexpr int T = W / 32;            // 32-row tiles per layer
   static constexpr int KS = W / 16;           // 16-deep k-steps over a hidden layer
   static constexpr int CHUNK = KS * 1024;     // one row tile of a W x W layer, bf16 fragments
   static constexpr int NC = (NL - 1) * T;     // hidden chunks per network evaluation
-  static constexpr int NCP = NC + (AOR ? 1 : 0);  // ring chunks per network evaluation
+  static constexpr int TPC = L1R ? KS / K1S : 1;        // layer-1 row tiles per ring chunk (L1R)
+  static constexpr int L1C = L1R ? (T + TPC - 1) / TPC : 0;  // layer-1 chunks per network evaluation
+  static constexpr int NCP = L1C + NC + (AOR ? 1 : 0);  // ring chunks per network evaluation
   static constexpr int NCT = NCP * NNET;      // ring chunks per step (all networks)
   static constexpr int A1_BYTES = T * K1S * 1024;
   static constexpr int AO_BYTES = KS * 1024;
   static constexpr int BH_BYTES = (NL - 1) * T * 2 * 16 * 4;
   static constexpr int BO_BYTES = 2 * 16 * 4;  // output bias, summed over the networks
   static constexpr int A1_OFF = 0;
-  static constexpr int AO_OFF = A1_OFF + NNET * A1_BYTES;
+  static constexpr int AO_OFF = A1_OFF + (L1R ? 0 : NNET * A1_BYTES);
   static constexpr int BH_OFF = AO_OFF + (AOR ? 0 : NNET * AO_BYTES);
   static constexpr int BO_OFF = BH_OFF + NNET * BH_BYTES;
   static constexpr int W_OFF = BO_OFF + BO_BYTES;
@@ -117,9 +121,9 @@ __device__ __forceinline__ void mfma_row_tile(const char* a_lane_g, const bf16x8
 // DIAG (timing ablations only, never on the product path): bit 0 = no ring barrier/DMA,
 // bit 1 = hidden activations replaced by a cast, bit 2 = layer-1 activation replaced by a cast.
 template <int W, int NL, int K1S, int NNET, int NW, int R, bool RES, bool CONSERVATIVE, int DIAG = 0,
-          bool AOR = false>
+          bool AOR = false, bool L1R = false>
 struct Engine {
-  using L = Lay<W, NL, K1S, NNET, R, RES, AOR>;
+  using L = Lay<W, NL, K1S, NNET, R, RES, AOR, L1R>;
   static constexpr int T = L::T;
   static constexpr int KS = L::KS;
   static constexpr int PPW = RES ? 1 : KS / NW;
@@ -198,13 +202,19 @@ struct Engine {
   template <int NI>
   __device__ __forceinline__ f32x16 layer1(const bf16x8 (&B1)[K1S], bf16x8 (&H)[KS]) {
     f32x16 pend;
+    const char* a1c = nullptr;  // L1R: the ring slot holding this row tile's layer-1 chunk
 #pragma unroll
     for (int rt = 0; rt < T; ++rt) {
       asm volatile("" ::: "memory");
       f32x16 acc = {};
+      if constexpr (L1R) {
+        if (rt % L::TPC == 0) a1c = chunk_sync(NI * L::NCP + rt / L::TPC);
+      }
 #pragma unroll
       for (int s = 0; s < K1S; ++s) {
-        const bf16x8 a = *(const bf16x8*)(lds + L::A1_OFF + NI * L::A1_BYTES + (rt * K1S + s) * 1024 + lane * 16);
+        const char* src = L1R ? a1c + ((rt % L::TPC) * K1S + s) * 1024
+                              : lds + L::A1_OFF + NI * L::A1_BYTES + (rt * K1S + s) * 1024;
+        const bf16x8 a = *(const bf16x8*)(src + lane * 16);
         acc = mfma32(a, B1[s], acc);
       }
       if (rt > 0) act_pack<true, (DIAG & 4) != 0>(pend, H[2 * (rt - 1)], H[2 * (rt - 1) + 1]);
@@ -232,7 +242,7 @@ struct Engine {
         acc = bias_tile(boff);
       } else {
         acc = bias_tile(boff);
-        wb = chunk_sync(NI * L::NCP + LI * T + rt);
+        wb = chunk_sync(NI * L::NCP + L::L1C + LI * T + rt);
       }
       if (rt == 0) act_carry<TW>(carry, Hin);
       mfma_row_tile<KS, true>(wb + lane * 16, Hin, acc);
@@ -249,7 +259,7 @@ struct Engine {
     if constexpr (LI == NL - 1) {
       asm volatile("" ::: "memory");
       if constexpr (AOR) {
-        const char* wb = chunk_sync(NI * L::NCP + L::NC);
+        const char* wb = chunk_sync(NI * L::NCP + L::L1C + L::NC);
         act_carry<TW>(carry, Ha);
         mfma_row_tile<KS, true>(wb + lane * 16, Ha, out);
       } else {
@@ -295,7 +305,7 @@ struct Engine {
     const int tid = threadIdx.x;
 #pragma unroll
     for (int ni = 0; ni < NNET; ++ni) {
-      stage_blocks<NW>(lds + L::A1_OFF + ni * L::A1_BYTES, a1[ni], T * K1S, w, lane);
+      if constexpr (!L1R) stage_blocks<NW>(lds + L::A1_OFF + ni * L::A1_BYTES, a1[ni], T * K1S, w, lane);
       if constexpr (!AOR) stage_blocks<NW>(lds + L::AO_OFF + ni * L::AO_BYTES, ao[ni], KS, w, lane);
       if constexpr (RES) stage_blocks<NW>(lds + L::W_OFF + ni * L::NC * L::CHUNK, hidden[ni], L::NC * KS, w, lane);
       stage_floats((float*)(lds + L::BH_OFF + ni * L::BH_BYTES), bh[ni], L::BH_BYTES / 4, tid, NW * 64);
@@ -391,7 +401,8 @@ struct SamplerLds {
   static constexpr int NV = MODE == MODE_CDIFFE ? D + M + 1 : D + 1;  // inputs that vary per chain
   static constexpr int K1S = k1s_of(3 * NV + 2);
   static constexpr bool AOR = NNET > 1 && W >= 512;  // output layers through the ring (Lay)
-  using L = Lay<W, NL, K1S, NNET, R, RES, AOR>;
+  static constexpr bool L1R = MODE == MODE_CDIFFE && W >= 512;  // layer 1 through the ring (Lay)
+  using L = Lay<W, NL, K1S, NNET, R, RES, AOR, L1R>;
   static constexpr int TOTAL = L::TOTAL;
 };
 
@@ -415,7 +426,7 @@ em_sampler_kernel(SamplerParams p) {
   const int h = lane >> 5;
   const int yi = blockIdx.y;
 
-  Engine<W, NL, K1S, NNET, NW, R, RES, NOISE, DIAG, SL::AOR> eng{lds, {p.hidden, p.hidden2}, 0, w, lane};
+  Engine<W, NL, K1S, NNET, NW, R, RES, NOISE, DIAG, SL::AOR, SL::L1R> eng{lds, {p.hidden, p.hidden2}, 0, w, lane};
   {
     const size_t a1_stride = (size_t)L::T * K1S * 1024;
     const char* const a1[2] = {p.a1 + (p.a1_per_y ? yi * a1_stride : 0), p.a1_2};
@@ -801,8 +812,8 @@ static hipError_t launch_forward_t(const ForwardParams& p, hipStream_t st) {
 }
 
 // Compiled shapes: widths 64 / 128 (hidden layers LDS-resident), 256 (4-slot ring) and 512 (4-wave
-// workgroups, 3 x 32 KiB ring slots; CDE, and Posterior with its output layers in the ring); 2 or 3
-// hidden layers; xdim 2 or 3. The CDE and
+// workgroups, 3 x 32 KiB ring slots; Posterior with its output layers and CDiffE with its layer 1 in
+// the ring); 2 or 3 hidden layers; xdim 2 or 3. The CDE and
 // Posterior kernels take any ydim (y is folded into the per-y layer-1 bias, M = 0); CDiffE feeds y_t
 // through layer 1 and is compiled for the two problems' (xdim, ydim) = (2, 2) and (3, 23).
 #define DMIP_W_CASES(X, MODE, NL, D, M) \
@@ -810,7 +821,6 @@ static hipError_t launch_forward_t(const ForwardParams& p, hipStream_t st) {
   X(MODE, 128, NL, D, M, 8, 0, true)    \
   X(MODE, 256, NL, D, M, 8, 4, false)
 #define DMIP_W512_CASE(X, MODE, NL, D, M) X(MODE, 512, NL, D, M, 4, 3, false)
-#define DMIP_NO_W512(X, MODE, NL, D, M)
 #define DMIP_SHAPES(X, MODE, W512, M2, M3)                              \
   DMIP_W_CASES(X, MODE, 3, 2, M2) DMIP_W_CASES(X, MODE, 3, 3, M3)      \
   DMIP_W_CASES(X, MODE, 2, 2, M2) DMIP_W_CASES(X, MODE, 2, 3, M3)      \
@@ -818,7 +828,7 @@ static hipError_t launch_forward_t(const ForwardParams& p, hipStream_t st) {
 #define DMIP_ALL_SHAPES(X)                                \
   DMIP_SHAPES(X, MODE_CDE, DMIP_W512_CASE, 0, 0)          \
   DMIP_SHAPES(X, MODE_POSTERIOR, DMIP_W512_CASE, 0, 0)    \
-  DMIP_SHAPES(X, MODE_CDIFFE, DMIP_NO_W512, 2, 23)
+  DMIP_SHAPES(X, MODE_CDIFFE, DMIP_W512_CASE, 2, 23)
 
 // Development knob (not part of the ABI): DMIP_SAMPLER_VARIANT=10x runs the timing ablations
 // (DIAG = x) of the width-256 CDE sampler; see profiles/README.md.

@@ -43,7 +43,7 @@ def test_supported_shapes(lib, dmip):
     assert sup(512, 3, 3, 23) and sup(256, 3, 3, 5)  # CDE: any ydim
     P, C = dmip._lib.DMIP_SAMPLER_POSTERIOR, dmip._lib.DMIP_SAMPLER_CDIFFE
     assert sup(256, 3, 2, 2, P) and sup(64, 2, 3, 23, P) and sup(512, 3, 3, 23, P)  # 512: output layers in the ring
-    assert not sup(512, 3, 3, 23, C)  # CDiffE at 512: the exact-f32 engine only
+    assert sup(512, 3, 3, 23, C) and sup(512, 2, 2, 2, C)  # CDiffE at 512: layer 1 through the ring
     assert sup(256, 3, 3, 23, C) and sup(128, 3, 2, 2, C)
     assert not sup(256, 3, 3, 5, C)  # CDiffE feeds y_t through layer 1: compiled ydim only
     # exact f32: every mode at widths 64..512 and 1..3 hidden layers (the reference configs' [512]*3)

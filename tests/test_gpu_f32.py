@@ -213,9 +213,9 @@ def test_f32_cdiffe_predictor_corrector_vs_oracle(dmip):
 
 
 def test_bf16_request_at_width_512_runs_a_fused_kernel(dmip):
-    """At the reference configs' width [512]*3 the Posterior sampler has a 16-bit kernel (output layers
-    through the weight ring) and CDiffE does not (its 27-input layer 1 alone is 96 KiB): a bf16 request
-    runs a fused kernel either way (never the per-step loop)."""
+    """At the reference configs' width [512]*3 both the Posterior sampler (output layers through the
+    weight ring) and CDiffE (its 96 KiB split layer 1 through the ring) run a fused 16-bit kernel for a
+    bf16 request (never the per-step loop)."""
     torch.manual_seed(2)
     for cls, key in (("PosteriorDiffusionEstimator", "em_sample_posterior"), ("CDiffE", "em_sample_cdiffe")):
         m = getattr(dmip, cls)(3, 23, [512] * 3)

@@ -307,7 +307,7 @@ def test_posterior_sampler_vs_oracle_product_rng(dmip, W, NL, xd, yd):
     assert err.max() < 0.02 * max(1.0, np.abs(ref).max()), err.max()
 
 
-@pytest.mark.parametrize("W,NL", [(64, 3), (128, 3), (256, 3), (256, 2)])
+@pytest.mark.parametrize("W,NL", [(64, 3), (128, 3), (256, 3), (256, 2), (512, 3), (512, 2)])
 @pytest.mark.parametrize("xd,yd", [(2, 2), (3, 23)])
 def test_cdiffe_sampler_vs_oracle_product_rng(dmip, W, NL, xd, yd):
     """Fused CDiffE kernel (dmip_em_sample_cdiffe): per-step re-diffused y_t through layer 1, the
@@ -610,7 +610,7 @@ def test_balanced_schedule_injected_noise_vs_oracle(dmip, golden):
 
 
 @pytest.mark.parametrize("cls,W", [("PosteriorDiffusionEstimator", 256), ("CDiffE", 256),
-                                   ("PosteriorDiffusionEstimator", 512)])
+                                   ("PosteriorDiffusionEstimator", 512), ("CDiffE", 512)])
 def test_balanced_schedule_other_samplers(dmip, cls, W):
     torch.manual_seed(21)
     m = getattr(dmip, cls)(3, 23, [W] * 3)
