@@ -311,7 +311,8 @@ def test_posterior_sampler_vs_oracle_product_rng(dmip, W, NL, xd, yd):
 @pytest.mark.parametrize("xd,yd", [(2, 2), (3, 23)])
 def test_cdiffe_sampler_vs_oracle_product_rng(dmip, W, NL, xd, yd):
     """Fused CDiffE kernel (dmip_em_sample_cdiffe): per-step re-diffused y_t through layer 1, the
-    joint net's x rows drive the update. Same RNG consumption as oracle.cdiffe_sample; 6 steps."""
+    joint net's x rows drive the update. Same RNG consumption as oracle.cdiffe_sample; 6 steps.
+    Width 512 (the reference configs'): the split layer 1 streams through the weight ring."""
     torch.manual_seed(3 * W + xd + NL)
     m = dmip.CDiffE(xd, yd, [W] * NL)
     params = _linear_params(m.sde.a)
