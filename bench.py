@@ -283,7 +283,7 @@ def other_configs(args, pkg, lib, dev):
     them (each: one warm-up launch, then timed launches with HIP events): configs[2] CDiffE
     predictor-corrector (the per-GPU share of 1M chains over 8 GPUs), configs[3] DPS (256k samples),
     configs[4] the PINNLoss training step (whole step on the device), and the reference configs'
-    own width [512]*3 for the CDE and the two-network Posterior samplers. Not the headline; errors are reported, not raised."""
+    own width [512]*3 for the CDE, the two-network Posterior and the CDiffE predictor-corrector samplers. Not the headline; errors are reported, not raised."""
     import copy
     import torch
     out = {}
@@ -309,6 +309,14 @@ def other_configs(args, pkg, lib, dev):
                     wl.kernel, wl.workload = f"em_sampler_kernel<0,{W},3,3,...>", "CDE at the reference width"
                 wl.model.sde.a.to(dev)
                 wl.weights = "random-init"
+            if workload == "cdiffe-pc" and kw.get("width"):
+                torch.manual_seed(0)
+                W = kw["width"]
+                wl.model = pkg.CDiffE(XDIM, YDIM, [W] * NH)
+                wl.model.sde.a.to(dev)
+                wl.flops_sample_step = 2 * flops_per_sample_step(XDIM + YDIM + 1, W, NH, XDIM + YDIM)
+                wl.kernel = f"em_sampler_kernel<2,{W},3,3,23,...> (layer 1 through the ring)"
+                wl.workload = "CDiffE predictor-corrector at the reference width"
             wl.step(3000)
             el, lm, x = timed(wl, reps, None, 1, dev, seed0=3100)
             lib.device_status(dev)
@@ -324,6 +332,7 @@ def other_configs(args, pkg, lib, dev):
     sampler("config4_dps", "dps", 262144, 1)
     sampler("cde_reference_width_512", "cde", 100000, 2, width=512)
     sampler("posterior_reference_width_512", "cde", 100000, 2, width=512, posterior=True)
+    sampler("cdiffe_pc_reference_width_512", "cdiffe-pc", 100000, 1, width=512)
     try:
         tr = importlib.import_module(PKG + ".training")
         torch.manual_seed(0)
