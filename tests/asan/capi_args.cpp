@@ -69,6 +69,20 @@ int main() {
   expect(dmip_schedule(0, &sde, nullptr, nullptr), DMIP_ERR_INVALID, "schedule: steps");
   expect(dmip_sampler_supported(0, 256, 3, 3, 23), 1, "supported bf16");
   expect(dmip_sampler_supported_f32(2, 512, 3, 3, 23), 1, "supported f32");
+  expect(dmip_sampler_supported(2, 512, 3, 3, 23), 1, "supported bf16 CDiffE width 512");
+  float dummy[4];
+  expect(dmip_em_sample_snapshots(0, nullptr, nullptr, &sde, nullptr, 1, 2, 2, 10, 0, 10, 0.f, 1.f, 1, 0, 0, 0.16f,
+                                  0, dummy, nullptr, nullptr),
+         DMIP_ERR_INVALID, "snapshots: every");
+  expect(dmip_em_sample_snapshots(0, nullptr, nullptr, &sde, nullptr, 1, 2, 2, 10, 0, 10, 0.f, 1.f, 1, 0, 0, 0.16f,
+                                  2, nullptr, nullptr, nullptr),
+         DMIP_ERR_INVALID, "snapshots: null buffer");
+  dmip_train_plan* plan = nullptr;
+  expect(dmip_train_plan_create(nullptr, &plan), DMIP_ERR_INVALID, "train_plan: null desc");
+  dmip_train_plan_desc d{};
+  expect(dmip_train_plan_create(&d, &plan), DMIP_ERR_INVALID, "train_plan: null pointers");
+  expect(dmip_train_plan_step(nullptr, nullptr, nullptr, nullptr), DMIP_ERR_INVALID, "train_plan: null step");
+  expect(dmip_train_plan_destroy(nullptr), DMIP_OK, "train_plan: destroy null");
   // the error buffer is thread-local: concurrent failures keep their own messages
   std::string a, b;
   std::thread t1([&] {
