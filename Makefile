@@ -5,7 +5,8 @@ HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-parameter
 F32OBJS := $(CSRC)/dmip_f32.o $(CSRC)/dmip_f32_cde.o $(CSRC)/dmip_f32_post.o $(CSRC)/dmip_f32_cdiffe.o
-OBJS := $(CSRC)/dmip_kernels.o $(CSRC)/dmip_train.o $(CSRC)/dmip_eval.o $(CSRC)/dmip_surrogate.o $(CSRC)/dmip_gemm.o $(CSRC)/dmip_jets.o $(CSRC)/dmip_step.o $(F32OBJS) $(CSRC)/dmip_capi.o
+X3OBJS := $(CSRC)/dmip_x3.o $(CSRC)/dmip_x3_cde.o $(CSRC)/dmip_x3_post.o $(CSRC)/dmip_x3_cdiffe.o
+OBJS := $(CSRC)/dmip_kernels.o $(CSRC)/dmip_train.o $(CSRC)/dmip_eval.o $(CSRC)/dmip_surrogate.o $(CSRC)/dmip_gemm.o $(CSRC)/dmip_jets.o $(CSRC)/dmip_step.o $(F32OBJS) $(X3OBJS) $(CSRC)/dmip_capi.o
 HDRS := $(CSRC)/dmip_device.h $(CSRC)/dmip_internal.h include/dmip.h
 
 all: $(PKG)/libdmip.so
@@ -38,6 +39,13 @@ $(CSRC)/dmip_f32.o: $(CSRC)/dmip_f32.hip $(CSRC)/dmip_f32.h $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(CSRC)/dmip_f32_%.o: $(CSRC)/dmip_f32_%.hip $(CSRC)/dmip_f32.h $(HDRS)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+# fp32-accurate split-fp16 engine (DMIP_PREC_F32X3): one header, four translation units
+$(CSRC)/dmip_x3.o: $(CSRC)/dmip_x3.hip $(CSRC)/dmip_x3.h $(HDRS)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(CSRC)/dmip_x3_%.o: $(CSRC)/dmip_x3_%.hip $(CSRC)/dmip_x3.h $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(CSRC)/dmip_capi.o: $(CSRC)/dmip_capi.cpp $(HDRS)

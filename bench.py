@@ -57,7 +57,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="cde", choices=["cde", "cdiffe-pc", "dps"])
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32x3", "fp32"])
     ap.add_argument("--chains", type=int, default=100000, help="chains per GPU (weak scaling)")
     ap.add_argument("--chains-total", type=int, default=0, help="total chains over all GPUs (strong scaling)")
     ap.add_argument("--num-steps", type=int, default=1000, help="SDE steps per sample")
@@ -207,9 +207,10 @@ class Workload:
         if args.workload == "cde":
             self.model, self.weights = load_model(pkg, dev)
             self.flops_sample_step = flops_per_sample_step()
-            self.peak = PEAK_BF16_TFLOPS if args.precision == "bf16" else PEAK_F32_TFLOPS
-            self.kernel = ("em_sampler_kernel<0,256,3,3,0,8,4,false> (+a1_prep, inside the events)"
-                           if args.precision == "bf16" else "f32_sampler_kernel<0,256,3,0,false> (+l1_prep)")
+            self.peak = PEAK_F32_TFLOPS if args.precision == "fp32" else PEAK_BF16_TFLOPS
+            self.kernel = {"bf16": "em_sampler_kernel<0,256,3,3,0,8,4,false> (+a1_prep, inside the events)",
+                           "fp32x3": "x3_sampler_kernel<0,256,3,0,false> (+x3_bias_prep)",
+                           "fp32": "f32_sampler_kernel<0,256,3,0,false> (+l1_prep)"}[args.precision]
             self.workload = "scatterometry CDE posterior sampling (BASELINE configs[1])"
             self.kw = {"precision": args.precision}
         elif args.workload == "cdiffe-pc":

@@ -18,10 +18,10 @@ LIB_PATH = os.environ.get("DMIP_LIB", os.path.join(_HERE, "libdmip.so"))
 DMIP_OK, DMIP_ERR_INVALID, DMIP_ERR_UNSUPPORTED, DMIP_ERR_HIP, DMIP_ERR_ALLOC = range(5)
 DMIP_INPUT_X_Y_T, DMIP_INPUT_X_T = 0, 1
 DMIP_ACT_TANH_TWICE_FIRST, DMIP_ACT_TANH = 0, 1
-DMIP_PREC_BF16, DMIP_PREC_F32 = 0, 1
-PRECISIONS = {"bf16": DMIP_PREC_BF16, "fp32": DMIP_PREC_F32}
+DMIP_PREC_BF16, DMIP_PREC_F32, DMIP_PREC_F32X3 = 0, 1, 2
+PRECISIONS = {"bf16": DMIP_PREC_BF16, "fp32": DMIP_PREC_F32, "fp32x3": DMIP_PREC_F32X3}
 DMIP_SAMPLER_CDE, DMIP_SAMPLER_POSTERIOR, DMIP_SAMPLER_CDIFFE = 0, 1, 2
-ABI_VERSION = 5
+ABI_VERSION = 6
 DMIP_LOSS_DSM, DMIP_LOSS_DSM_PDE, DMIP_LOSS_PINN, DMIP_LOSS_PINN2 = 0, 1, 2, 3
 DMIP_PDE_NONE, DMIP_PDE_FPE, DMIP_PDE_CFPE = 0, 1, 2
 DMIP_METRIC_L1, DMIP_METRIC_L2 = 0, 1
@@ -35,7 +35,7 @@ EXPORTED = (
     "dmip_surrogate_forward", "dmip_log_posterior", "dmip_mh_sample", "dmip_dps_sample", "dmip_device_status",
     "dmip_sampler_supported_f32", "dmip_posterior_loss_grad", "dmip_loss_grad_f32", "dmip_train_draws",
     "dmip_adam_step", "dmip_em_sample_snapshots", "dmip_train_plan_create", "dmip_train_plan_step",
-    "dmip_train_plan_set_counters", "dmip_train_plan_destroy",
+    "dmip_train_plan_set_counters", "dmip_train_plan_destroy", "dmip_sampler_supported_precision",
 )
 DMIP_DPS_NLL, DMIP_DPS_NORM = 0, 1
 
@@ -82,6 +82,9 @@ def _declare(lib):
     lib.dmip_abi_version.restype = _i32
     lib.dmip_sampler_supported.argtypes = [_i32, _i32, _i32, _i32, _i32]
     lib.dmip_sampler_supported_f32.argtypes = [_i32, _i32, _i32, _i32, _i32]
+    if hasattr(lib, "dmip_sampler_supported_precision"):
+        lib.dmip_sampler_supported_precision.argtypes = [_i32, _i32, _i32, _i32, _i32, _i32]
+        lib.dmip_sampler_supported_precision.restype = _i32
     lib.dmip_device_status.argtypes = [_c_void_p]
     lib.dmip_train_draws.argtypes = [_u64, _u64, _i64, _i32, _i32, ctypes.POINTER(DmipVpsde), ctypes.c_double, _f32,
                                      _c_void_p, _c_void_p, _c_void_p]
@@ -227,7 +230,8 @@ class MlpHandle:
 
 
 def precision_code(precision):
-    """'bf16' (bf16 MFMA operands, the throughput mode) or 'fp32' (exact f32, the reference's arithmetic)."""
+    """'bf16' (16-bit MFMA operands, the fastest mode), 'fp32x3' (fp32-accurate products as three fp16 MFMAs,
+    the reference-precision throughput mode) or 'fp32' (exact f32 MFMA, bit-level parity mode)."""
     if precision not in PRECISIONS:
         raise ValueError(f"precision must be one of {sorted(PRECISIONS)}, got {precision!r}")
     return PRECISIONS[precision]
@@ -284,8 +288,7 @@ def em_sample_snapshots(mode, net, prior, sde, y, n_chains, chain_offset, num_st
 
 
 def sampler_supported(width, n_hidden, xdim, ydim=0, mode=DMIP_SAMPLER_CDE, precision="bf16"):
-    fn = lib().dmip_sampler_supported_f32 if precision_code(precision) == DMIP_PREC_F32 else lib().dmip_sampler_supported
-    return bool(fn(mode, width, n_hidden, xdim, ydim))
+    return bool(lib().dmip_sampler_supported_precision(precision_code(precision), mode, width, n_hidden, xdim, ydim))
 
 
 def device_status(device):

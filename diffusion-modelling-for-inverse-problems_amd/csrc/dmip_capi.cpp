@@ -181,11 +181,16 @@ struct dmip_mlp {
   char* f32_stream = nullptr;     // [(L-1) W/16 + f32_ot chunks][W/16][64][4]
   float* f32_bias = nullptr;      // [(L-1)][W] | [16 f32_ot]
   int f32_k1q = 0, f32_ot = 0;
+  // fp32-accurate split-fp16 images (DMIP_PREC_F32X3, dmip_x3.h)
+  char* x3_l1 = nullptr;          // [W/16][K1Q][64][8] fp16 over (x, t)
+  char* x3_l1_full = nullptr;     // the same over every input column (X_Y_T networks: CDiffE)
+  char* x3_stream = nullptr;      // hidden chunks | output chunk
+  float* x3_bias = nullptr;       // [L W + 16]
   ~dmip_mlp() {
     for (void* p : {(void*)ring_l1, (void*)hidden, (void*)ao_samp, (void*)ao_full, (void*)bias_hidden, (void*)bias_out_samp,
                     (void*)bias_out_full, (void*)a1_full, (void*)w1, (void*)b1, (void*)dps_l1, (void*)dps_w2,
                     (void*)dps_w3, (void*)dps_w4, (void*)dps_bias, (void*)f32_l1, (void*)f32_stream,
-                    (void*)f32_bias})
+                    (void*)f32_bias, (void*)x3_l1, (void*)x3_l1_full, (void*)x3_stream, (void*)x3_bias})
       if (p) (void)hipFree(p);
   }
 };
@@ -228,6 +233,99 @@ int pack_f32_net(dmip_mlp* net, const float* const* weights, const float* const*
 
 dmip::F32Net f32_net(const dmip_mlp* n) { return dmip::F32Net{n->f32_l1, n->f32_stream, n->f32_bias}; }
 
+// ---- fp32-accurate split-fp16 images (DMIP_PREC_F32X3, dmip_x3.h). A 16x16x32 f16 fragment block:
+// lane l = i + 16 g holds A[row i][k-slot 8 g + m], m = 0..7. Hidden-layer k-slots follow the previous
+// layer's accumulator tiles: slot (q, g, m) is unit kperm16(q, g, m).
+inline int kperm16(int q, int g, int m) { return 32 * q + 16 * (m >> 2) + 4 * g + (m & 3); }
+inline int x3_k1q(int nv) { return (3 * nv + 31) / 32; }
+
+// v = hi + lo in fp16 (hi = fp16(v), lo = fp16(v - hi))
+void split_h(double v, uint16_t& hi, uint16_t& lo) {
+  hi = f2h((float)v);
+  lo = f2h((float)(v - (double)h2f(hi)));
+}
+
+// layer-1 image over the input columns `cols` (scaled by c): input n at k-slots 3n, 3n+1, 3n+2 with
+// A = [W_hi, W_hi, W_lo] (the kernel's B = [v_hi, v_lo, v_hi])
+std::vector<uint16_t> pack_x3_l1(const float* W1, int W, int in_dim, const std::vector<int>& cols) {
+  const int NV = (int)cols.size(), K1Q = x3_k1q(NV), ST = W / 16;
+  std::vector<uint16_t> img((size_t)ST * K1Q * 512, 0);
+  for (int o = 0; o < ST; ++o)
+    for (int q = 0; q < K1Q; ++q)
+      for (int l = 0; l < 64; ++l)
+        for (int m = 0; m < 8; ++m) {
+          const int i = l & 15, g = l >> 4, s = 32 * q + 8 * g + m, n = s / 3, p = s % 3;
+          if (n >= NV) continue;
+          uint16_t hi, lo;
+          split_h(kC * (double)W1[(size_t)(16 * o + i) * in_dim + cols[n]], hi, lo);
+          img[(((size_t)o * K1Q + q) * 64 + l) * 8 + m] = p < 2 ? hi : lo;
+        }
+  return img;
+}
+
+// [n_tiles][KQ][2][64][8] image of an r-form-input layer: A = scale * (-2 W), init = scale b - 0.5 sum_k A
+// (with A = hi + lo as the kernel applies it); rows >= n_rows zero
+void pack_x3_layer(const float* Wl, const float* bl, int n_rows, int W, int n_tiles, double scale,
+                   std::vector<uint16_t>& img, float* init) {
+  const int KQ = W / 32;
+  img.assign((size_t)n_tiles * KQ * 2 * 512, 0);
+  std::vector<uint16_t> hi((size_t)n_rows * W), lo((size_t)n_rows * W);
+  for (int r = 0; r < n_rows; ++r) {
+    double acc = 0.0;
+    for (int k = 0; k < W; ++k) {
+      split_h(-2.0 * scale * (double)Wl[(size_t)r * W + k], hi[(size_t)r * W + k], lo[(size_t)r * W + k]);
+      acc += (double)h2f(hi[(size_t)r * W + k]) + (double)h2f(lo[(size_t)r * W + k]);
+    }
+    init[r] = (float)(scale * (double)bl[r] - 0.5 * acc);
+  }
+  for (int o = 0; o < n_tiles; ++o)
+    for (int q = 0; q < KQ; ++q)
+      for (int p = 0; p < 2; ++p)
+        for (int l = 0; l < 64; ++l)
+          for (int m = 0; m < 8; ++m) {
+            const int row = 16 * o + (l & 15);
+            if (row >= n_rows) continue;
+            const size_t src = (size_t)row * W + kperm16(q, l >> 4, m);
+            img[((((size_t)o * KQ + q) * 2 + p) * 64 + l) * 8 + m] = p == 0 ? hi[src] : lo[src];
+          }
+}
+
+int pack_x3_net(dmip_mlp* net, const float* const* weights, const float* const* biases) {
+  const int W = net->width, L = net->n_hidden, IN = net->in_dim, OUT = net->out_dim, ST = W / 16;
+  const int chunk = dmip::x3_chunk_bytes(W);
+  if (chunk == 0) return DMIP_OK;  // no x3 kernels at this width
+  std::vector<int> xt;
+  for (int k = 0; k < net->xdim; ++k) xt.push_back(k);
+  xt.push_back(IN - 1);
+  std::vector<int> full;
+  for (int k = 0; k < IN; ++k) full.push_back(k);
+  const std::vector<uint16_t> l1 = pack_x3_l1(weights[0], W, IN, xt);
+  std::vector<uint16_t> l1f;
+  if (net->layout == DMIP_INPUT_X_Y_T) l1f = pack_x3_l1(weights[0], W, IN, full);
+  std::vector<float> bias((size_t)L * W + 16, 0.0f);
+  for (int u = 0; u < W; ++u) bias[u] = (float)(kC * (double)biases[0][u]);
+  std::vector<char> stream;
+  std::vector<uint16_t> img;
+  for (int li = 1; li < L; ++li) {
+    pack_x3_layer(weights[li], biases[li], W, W, ST, kC, img, bias.data() + (size_t)li * W);
+    const char* b = (const char*)img.data();
+    stream.insert(stream.end(), b, b + img.size() * 2);
+  }
+  const int orows = OUT < 16 ? OUT : 16;  // the samplers read output rows 0..15 (the x rows)
+  pack_x3_layer(weights[L], biases[L], orows, W, 1, 1.0, img, bias.data() + (size_t)L * W);
+  std::vector<char> ochunk((size_t)chunk, 0);
+  std::memcpy(ochunk.data(), img.data(), img.size() * 2);
+  stream.insert(stream.end(), ochunk.begin(), ochunk.end());
+  std::vector<char> l1b(l1.size() * 2), l1fb(l1f.size() * 2);
+  std::memcpy(l1b.data(), l1.data(), l1b.size());
+  if (!l1f.empty()) std::memcpy(l1fb.data(), l1f.data(), l1fb.size());
+  int rc = DMIP_OK;
+  if ((rc = upload(&net->x3_l1, l1b)) || (rc = upload(&net->x3_l1_full, l1fb)) || (rc = upload(&net->x3_stream, stream)) ||
+      (rc = upload(&net->x3_bias, bias)))
+    return rc;
+  return DMIP_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -258,6 +356,15 @@ int dmip_sampler_supported(int mode, int width, int n_hidden, int xdim, int ydim
 
 int dmip_sampler_supported_f32(int mode, int width, int n_hidden, int xdim, int ydim) {
   return dmip::f32_sampler_supported(mode, width, n_hidden, xdim, ydim) ? 1 : 0;
+}
+
+int dmip_sampler_supported_precision(int precision, int mode, int width, int n_hidden, int xdim, int ydim) {
+  switch (precision) {
+    case DMIP_PREC_BF16: return dmip::sampler_shape_supported(mode, width, n_hidden, xdim, ydim) ? 1 : 0;
+    case DMIP_PREC_F32: return dmip::f32_sampler_supported(mode, width, n_hidden, xdim, ydim) ? 1 : 0;
+    case DMIP_PREC_F32X3: return dmip::x3_sampler_supported(mode, width, n_hidden, xdim, ydim) ? 1 : 0;
+    default: return 0;
+  }
 }
 
 int dmip_mlp_create(int in_dim, int out_dim, int n_hidden, const int* widths, int act_mode, int input_layout,
@@ -449,7 +556,8 @@ int dmip_mlp_create(int in_dim, int out_dim, int n_hidden, const int* widths, in
   if ((rc = upload(&net->hidden, hid_b)) || (rc = upload(&net->ao_samp, ao_sb)) || (rc = upload(&net->ao_full, ao_fb)) ||
       (rc = upload(&net->bias_hidden, bh)) || (rc = upload(&net->bias_out_samp, bo_s)) ||
       (rc = upload(&net->bias_out_full, bo_f)) || (rc = upload(&net->a1_full, a1f_b)) ||
-      (rc = upload(&net->w1, w1v)) || (rc = upload(&net->b1, b1v)) || (rc = pack_f32_net(net, weights, biases))) {
+      (rc = upload(&net->w1, w1v)) || (rc = upload(&net->b1, b1v)) || (rc = pack_f32_net(net, weights, biases)) ||
+      (rc = pack_x3_net(net, weights, biases))) {
     delete net;
     return rc;
   }
@@ -465,14 +573,15 @@ int dmip_mlp_destroy(dmip_mlp* net) {
 int dmip_mlp_forward(const dmip_mlp* net, const float* x_dev, const float* y_dev, int64_t y_stride,
                      const float* t_dev, int t_stride, int64_t n, float* out_dev, int precision, void* stream) {
   if (!net || !x_dev || !t_dev || !out_dev) return fail(DMIP_ERR_INVALID, "null argument");
-  if (precision != DMIP_PREC_BF16 && precision != DMIP_PREC_F32) return fail(DMIP_ERR_INVALID, "unknown precision");
+  if (precision != DMIP_PREC_BF16 && precision != DMIP_PREC_F32 && precision != DMIP_PREC_F32X3)
+    return fail(DMIP_ERR_INVALID, "unknown precision");
   if (n < 0) return fail(DMIP_ERR_INVALID, "n < 0");
   if (n == 0) return DMIP_OK;
   const int ydim = net->layout == DMIP_INPUT_X_Y_T ? net->in_dim - net->xdim - 1 : 0;
   if (ydim > 0 && !y_dev) return fail(DMIP_ERR_INVALID, "y required for an X_Y_T network");
   if (ydim > 0 && y_stride != 0 && y_stride != ydim) return fail(DMIP_ERR_INVALID, "y_stride must be 0 or ydim");
   if (t_stride != 0 && t_stride != 1) return fail(DMIP_ERR_INVALID, "t_stride must be 0 or 1");
-  if (precision == DMIP_PREC_F32) {
+  if (precision == DMIP_PREC_F32 || precision == DMIP_PREC_F32X3) {  // F32X3: the exact-f32 forward (fp32 either way)
     dmip::F32ForwardParams q{};
     q.net = f32_net(net);
     q.n_hidden = net->n_hidden;
@@ -603,12 +712,68 @@ static int em_sample_f32(int mode, const dmip_mlp* net0, const dmip_mlp* net1, c
   return DMIP_OK;
 }
 
+// fp32-accurate split-fp16 samplers (dmip_x3.h): same loop, RNG and sharding as the other engines;
+// arguments already validated by em_sample_impl
+static int em_sample_x3(int mode, const dmip_mlp* net0, const dmip_mlp* net1, const SampleArgs& a) {
+  const int xdim = a.xdim, ydim = a.ydim;
+  if (!dmip::x3_sampler_supported(mode, net0->width, net0->n_hidden, xdim, ydim) || !net0->x3_stream ||
+      (mode == DMIP_SAMPLER_CDIFFE && !net0->x3_l1_full) || (net1 && !net1->x3_stream))
+    return fail(DMIP_ERR_UNSUPPORTED, "no compiled f32x3 sampler (mode " + std::to_string(mode) + ") for width " +
+                                          std::to_string(net0->width) + ", layers " + std::to_string(net0->n_hidden) +
+                                          ", xdim " + std::to_string(xdim) + ", ydim " + std::to_string(ydim));
+  hipStream_t st = (hipStream_t)a.stream;
+  dmip::X3SamplerParams p{};
+  p.net[0] = dmip::X3Net{mode == DMIP_SAMPLER_CDIFFE ? net0->x3_l1_full : net0->x3_l1, net0->x3_stream, net0->x3_bias};
+  if (net1) p.net[1] = dmip::X3Net{net1->x3_l1, net1->x3_stream, net1->x3_bias};
+  p.n_hidden = net0->n_hidden;
+  float* bias_y = nullptr;
+  if (mode != DMIP_SAMPLER_CDIFFE) {
+    // y is constant per y index: c (b1 + W1_y y) becomes layer 1's per-y bias (f64 prep)
+    hipError_t e = hipMallocAsync((void**)&bias_y, (size_t)a.n_y * net0->width * sizeof(float), st);
+    if (e != hipSuccess) return fail(DMIP_ERR_ALLOC, std::string("hipMallocAsync: ") + hipGetErrorString(e));
+    dmip::X3BiasPrepParams bp{net0->w1, net0->b1, a.y_dev, bias_y, net0->width, net0->in_dim, xdim, ydim};
+    if ((e = dmip::launch_x3_bias_prep(bp, a.n_y, st)) != hipSuccess) {
+      (void)hipFreeAsync(bias_y, st);
+      return hip_fail(e, "x3 bias prep launch");
+    }
+  }
+  p.bias_y = bias_y;
+  p.y_obs = a.y_dev;
+  p.n_corr = a.n_corr;
+  p.snr = a.snr;
+  p.noise = a.noise_dev;
+  p.x_out = a.x_out_dev;
+  p.snap_out = a.snap_out_dev;
+  p.snap_every = a.snap_every;
+  p.n_chains = a.n_chains;
+  p.chain_offset = a.chain_offset;
+  p.num_steps = a.num_steps;
+  fill_schedule(a, p.T, p.bmin, p.bdiff, p.delta, p.sqrt_delta);
+  p.mean = a.mean;
+  p.stdv = a.stdv;
+  p.seed = a.seed;
+  p.err = status_word(dmip::stream_device(st));
+  if (!p.err) {
+    if (bias_y) (void)hipFreeAsync(bias_y, st);
+    return fail(DMIP_ERR_ALLOC, "device status word");
+  }
+  p.debug_flags = debug_no_handover();
+  p.spin_limit = p.debug_flags ? (1u << 10) : (1u << 22);
+  bool ok = false;
+  hipError_t e = dmip::launch_x3_sampler(p, mode, net0->width, net0->n_hidden, xdim, ydim, a.n_y, st, &ok);
+  if (bias_y) (void)hipFreeAsync(bias_y, st);
+  if (!ok) return fail(DMIP_ERR_UNSUPPORTED, "no compiled f32x3 sampler");
+  if (e != hipSuccess) return hip_fail(e, "f32x3 sampler launch");
+  return DMIP_OK;
+}
+
 // net0: the CDE / CDiffE network or the Posterior likelihood; net1: the Posterior prior (else null)
 static int em_sample_impl(int mode, const dmip_mlp* net0, const dmip_mlp* net1, const SampleArgs& a) {
   const int xdim = a.xdim, ydim = a.ydim;
   if (!net0 || !a.sde || !a.y_dev || !a.x_out_dev || (mode == DMIP_SAMPLER_POSTERIOR && !net1))
     return fail(DMIP_ERR_INVALID, "null argument");
-  if (a.precision != DMIP_PREC_BF16 && a.precision != DMIP_PREC_F32) return fail(DMIP_ERR_INVALID, "unknown precision");
+  if (a.precision != DMIP_PREC_BF16 && a.precision != DMIP_PREC_F32 && a.precision != DMIP_PREC_F32X3)
+    return fail(DMIP_ERR_INVALID, "unknown precision");
   if (a.noise_dev && mode != DMIP_SAMPLER_CDE) return fail(DMIP_ERR_INVALID, "noise injection: CDE sampler only");
   if (net0->layout != DMIP_INPUT_X_Y_T) return fail(DMIP_ERR_INVALID, "sampler needs an x,y,t network");
   const int out_expected = mode == DMIP_SAMPLER_CDIFFE ? xdim + ydim : xdim;
@@ -627,6 +792,7 @@ static int em_sample_impl(int mode, const dmip_mlp* net0, const dmip_mlp* net1, 
   if (!(a.sde->T > 0.0)) return fail(DMIP_ERR_INVALID, "T must be > 0");
   if (a.n_chains == 0) return DMIP_OK;
   if (a.precision == DMIP_PREC_F32) return em_sample_f32(mode, net0, net1, a);
+  if (a.precision == DMIP_PREC_F32X3) return em_sample_x3(mode, net0, net1, a);
   if (!dmip::sampler_shape_supported(mode, net0->width, net0->n_hidden, xdim, ydim))
     return fail(DMIP_ERR_UNSUPPORTED, "no compiled sampler (mode " + std::to_string(mode) + ") for width " +
                                           std::to_string(net0->width) + ", layers " + std::to_string(net0->n_hidden) +

@@ -240,6 +240,51 @@ bool f32_sampler_supported(int mode, int width, int n_hidden, int xdim, int ydim
 hipError_t launch_f32_forward(const F32ForwardParams& p, int width, int ot, hipStream_t st, bool* supported);
 hipError_t launch_f32_l1_prep(const F32L1PrepParams& p, int n_y, hipStream_t st);
 
+// fp32-accurate split-fp16 networks (dmip_x3.h, DMIP_PREC_F32X3): images packed by dmip_capi.cpp pack_x3_net.
+struct X3Net {
+  const char* l1;      // [W/16 tiles][K1Q][64 lanes][8 fp16]: layer-1 image (x, t columns -- or every column, CDiffE)
+  const char* stream;  // [(L-1) NCH hidden chunks + 1 output chunk][CHUNK bytes] (dmip_x3.h Shape)
+  const float* bias;   // [L W + 16]: c b1 | folded hidden biases | folded output bias (rows 0..15)
+};
+
+struct X3SamplerParams {
+  X3Net net[2];               // net 0: CDE / CDiffE / likelihood; net 1: the Posterior prior
+  const float* bias_y;        // CDE / likelihood: per-y layer-1 bias c (b1 + W1_y y) [n_y][W]
+  int n_hidden;
+  const float* y_obs;         // CDiffE observations [n_y][ydim]
+  int n_corr;
+  float snr;
+  const float* noise;         // CDE: injected normals [S+1][n_y][n_chains][D] or null
+  float* x_out;               // [n_y][n_chains][D]
+  float* snap_out;            // trajectory snapshots or null
+  int snap_every;
+  long long n_chains, chain_offset;
+  int num_steps;
+  float T, bmin, bdiff, delta, sqrt_delta, mean, stdv;
+  unsigned long long seed;
+  float* xfer;                // balanced schedule hand-over (as SamplerParams)
+  unsigned int* xflag;
+  unsigned int* err;
+  unsigned int spin_limit;
+  int debug_flags;
+};
+
+struct X3BiasPrepParams {
+  const float* w1;  // [width][in_dim] (nn.Linear layout)
+  const float* b1;
+  const float* y;   // [n_y][ydim]
+  float* bias_y;    // out: [n_y][width] = c (b1 + W1_y y), f64 accumulation
+  int width, in_dim, xdim, ydim;
+};
+
+hipError_t launch_x3_sampler(const X3SamplerParams& p, int mode, int width, int n_hidden, int xdim, int ydim, int n_y,
+                             hipStream_t st, bool* supported);
+bool x3_sampler_supported(int mode, int width, int n_hidden, int xdim, int ydim);
+hipError_t launch_x3_bias_prep(const X3BiasPrepParams& p, int n_y, hipStream_t st);
+// geometry of the x3 images (dmip_x3.h Shape) for the host packer
+int x3_chunk_bytes(int width);
+int x3_tiles_per_chunk(int width);
+
 // ---- exact-f32 training engine (dmip_gemm.hip): MFMA GEMM with fused epilogues
 enum {
   GEMM_EPI_NONE = 0,      // C = acc

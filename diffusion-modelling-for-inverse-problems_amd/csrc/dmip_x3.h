@@ -1,0 +1,504 @@
+// fp32-accurate score networks at the fp16 matrix rate: the DMIP_PREC_F32X3 reverse-SDE samplers.
+//
+// The reference computes its score network in fp32 (nets.py:32-35, models/diffusion.py:38-42). Every
+// product here is formed as a three-term fp16 split on v_mfma_f32_16x16x32_f16 (fp32 accumulation):
+//     W h  ~  W_hi h_hi + W_hi h_lo + W_lo h_hi,   v_hi = fp16(v), v_lo = fp16(v - v_hi)
+// The dropped W_lo h_lo is <= 2^-24 |W h|, and the lo parts are held to ~2^-24 absolute (fp16 subnormals
+// are honoured by the f16 MFMAs on gfx950): measured on the device, the split product's error is
+// 2^-23.2 of sum |w h| against 2^-23.0 for an f32 fmaf chain (profiles/r3_mfma_f16_check.txt,
+// scripts/ubench/mfma_f16_check.hip). Three fp16 MFMAs cost 3/16 of one f32 MFMA of the same work:
+// this engine runs the reference's fp32 arithmetic at ~5x the exact-f32 engine's (dmip_f32.h) rate.
+//
+// Layout (one wave = 16 chains, v_mfma_f32_16x16x32_f16):
+//   * a layer's output tile is 16 units x 16 chains: lane (g = l >> 4, j = l & 15) holds units
+//     16 o + 4 g + r (r = 0..3) of chain j. Two consecutive tiles 2q, 2q + 1 are the B operand of
+//     k-step q of the next layer with no lane movement: lane (g, j) supplies k-slots 8 g + m, which
+//     the host maps to unit kperm16(q, g, m) = 32 q + 16 (m >> 2) + 4 g + (m & 3) of the weight image.
+//   * activations stay in registers as (hi, lo) fp16 pairs: W/32 B fragments each (W = 256: 64 VGPRs
+//     for a layer's input, 64 for its output), so a 512-thread workgroup keeps 2 waves per SIMD.
+//   * weight images (dmip_capi.cpp pack_x3_net): output tile o, k-step q, part p (hi / lo), lane
+//     l = i + 16 g holds A[16 o + i][kperm16(q, g, 0..7)] -- one ds_read_b128 per lane per fragment;
+//     a tile is W/16 KiB (both parts). The W x W layers and the output layer stream from L2 through
+//     an R-slot LDS ring by LDS-DMA (the protocol of dmip_f32.h), CHUNK = CT tiles (<= 32 KiB);
+//     layer 1 and the biases are LDS-resident.
+//   * layer 1 (x, tau -- or every input for CDiffE -- plus its bias in the accumulator init): input n
+//     takes k-slots 3n, 3n+1, 3n+2 with B = [v_hi, v_lo, v_hi] against A = [W_hi, W_hi, W_lo].
+//   * activations in r-form, r = 1 / (1 + 2^zs) = (1 - tanh z) / 2 (zs = 2 log2(e) z, the scale folded
+//     into the weights); "1 - 2r" is folded into the next layer's weights (-2 W) and bias (b + sum W).
+//     Layer 1's double tanh (nets.py:21-26) is r1 = act_r(zs), r2 = act_r(c (1 - 2 r1)) -- exp2 + rcp
+//     at ~1 ulp each, no polynomial (the 16-bit engine's degree-4 fit is 1.7e-5 off).
+// The chain state, schedule, RNG, EM update, snapshots, hand-over and predictor-corrector are those of
+// the other two engines (dmip_device.h): all three precisions draw identical noise chain by chain.
+#pragma once
+#include "dmip_device.h"
+#include "dmip_internal.h"
+
+namespace dmip {
+namespace x3 {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 mfma16(const u32x4& a, const u32x4& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0,
+                                                0);
+}
+
+template <int W>
+struct Shape {
+  static constexpr int ST = W / 16;                        // 16-row output tiles per layer
+  static constexpr int KQ = W / 32;                        // 32-deep k-steps over a W-wide input
+  static constexpr int TILE = KQ * 2048;                   // one output tile: hi + lo fragments per k-step
+  static constexpr int CT0 = 32768 / TILE;
+  static constexpr int CT = CT0 < 1 ? 1 : (CT0 > ST ? ST : CT0);  // tiles per ring chunk
+  static constexpr int CHUNK = CT * TILE;
+  static constexpr int NCH = ST / CT;                      // chunks per W x W layer
+  static constexpr int NW = W == 512 ? 4 : 8;              // W = 512: one wave per SIMD (2 x 128 VGPR activations)
+  static constexpr int PPW = CHUNK / 1024 / NW;            // LDS-DMA pieces per wave per chunk
+  static_assert(ST % CT == 0 && PPW >= 1 && CHUNK % (1024 * NW) == 0, "ring geometry");
+};
+
+constexpr int kLdsBudget = 160 * 1024;
+constexpr int kMaxHidden = 3;
+constexpr int k1q_of(int nv) { return (3 * nv + 31) / 32; }
+constexpr int align16(int v) { return (v + 15) / 16 * 16; }
+
+// LDS: layer-1 images, biases (per network: layer 1 | hidden layers | output rows 0..15), the
+// observation (CDiffE), the ring.
+template <int W, int NNET, int K1Q, int M>
+struct XLay {
+  using S = Shape<W>;
+  static constexpr int L1_BYTES = S::ST * K1Q * 1024;
+  static constexpr int BF = kMaxHidden * W + 16;  // bias floats per network
+  static constexpr int L1 = 0;
+  static constexpr int BIAS = L1 + NNET * L1_BYTES;
+  static constexpr int BIAS_BYTES = align16(BF * 4);
+  static constexpr int YOBS = BIAS + NNET * BIAS_BYTES;
+  static constexpr int RING = align16(YOBS + (M > 0 ? M : 1) * 4);
+  static constexpr int R0 = (kLdsBudget - RING) / S::CHUNK;
+  static constexpr int R = R0 > 4 ? 4 : R0;
+  static constexpr int TOTAL = RING + R * S::CHUNK;
+  static_assert(R >= 2, "LDS budget: fewer than two ring slots");
+};
+
+// split a pair of f32 values into an (hi, lo) pair of packed fp16 dwords: v = hi + lo to ~2^-22 |v|
+__device__ __forceinline__ void split_pair(float a, float b, uint32_t& hi, uint32_t& lo) {
+  hi = cvt_pk_f16(a, b);
+  const f16x2 h = __builtin_bit_cast(f16x2, hi);
+  lo = cvt_pk_f16(a - (float)h[0], b - (float)h[1]);
+}
+
+// r-form activation r = 1 / (1 + 2^zs) (v_exp_f32 + v_rcp_f32, ~1 ulp each)
+__device__ __forceinline__ float x3_act_r(float zs) {
+  return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(zs));
+}
+
+// layer 1's tanh(tanh(z)) in r-form: r1 = (1 - tanh z)/2, then r2 = (1 - tanh(tanh z))/2 with
+// tanh z = 1 - 2 r1 (both tanh arguments pre-scaled by c = 2 log2(e))
+__device__ __forceinline__ float x3_act_r2(float zs) {
+  const float r1 = x3_act_r(zs);
+  return x3_act_r(__builtin_fmaf(-2.0f * kTanhScale, r1, kTanhScale));
+}
+
+// The network engine: NNET networks of nl layers (runtime, 1..3) of width W share one weight ring;
+// each evaluation streams (nl - 1) NCH hidden chunks then one output chunk, in the host image's order.
+template <int W, int NNET, int K1Q, int R, int RING_OFF>
+struct XEngine {
+  using S = Shape<W>;
+  static constexpr int ST = S::ST, KQ = S::KQ, CT = S::CT, NCH = S::NCH, NW = S::NW, PPW = S::PPW;
+  static constexpr int CHUNK = S::CHUNK, TILE = S::TILE;
+
+  char* lds;
+  const char* img[2];
+  int l1_off[2];
+  int bias_off[2];
+  int nl;       // hidden layers (layer 1 + nl - 1 W x W layers)
+  int ncn;      // chunks per network evaluation
+  int c_issue;  // next chunk to issue, in [0, NNET ncn)
+  int s_issue;  // its ring slot
+  int s_read;   // ring slot of the next chunk to consume
+  int w, lane, g;
+
+  __device__ __forceinline__ void init(int n_hidden) {
+    nl = n_hidden;
+    ncn = (nl - 1) * NCH + 1;
+    c_issue = s_issue = s_read = 0;
+  }
+
+  __device__ __forceinline__ void ring_issue() {
+    const int c = __builtin_amdgcn_readfirstlane(c_issue);
+    const int n = __builtin_amdgcn_readfirstlane(ncn);
+    const uint64_t addr = (uint64_t)((c < n ? img[0] : img[1]) + (size_t)(c < n ? c : c - n) * CHUNK);
+    const char* base = (const char*)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(addr >> 32)) << 32) |
+                                     (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)addr));
+    asm volatile("" : "+s"(base));  // keep the per-chunk address out of the loop-invariant hoist
+    char* dst = lds + RING_OFF + __builtin_amdgcn_readfirstlane(s_issue) * CHUNK;
+#pragma unroll
+    for (int q = 0; q < PPW; ++q) {
+      const int piece = w * PPW + q;
+      glds16(base + piece * 1024, dst + piece * 1024, lane);
+    }
+    c_issue = c_issue + 1 == NNET * ncn ? 0 : c_issue + 1;
+    s_issue = s_issue + 1 == R ? 0 : s_issue + 1;
+  }
+
+  // the next chunk of the stream, landed (own pieces counted, the others' by the barrier); the slot
+  // read one chunk ago is refilled R - 1 chunks ahead
+  __device__ __forceinline__ const char* chunk_sync() {
+    wait_vmcnt<(R - 2) * PPW>();
+    lds_barrier();
+    ring_issue();
+    const char* slot = lds + RING_OFF + s_read * CHUNK;
+    s_read = s_read + 1 == R ? 0 : s_read + 1;
+    return slot;
+  }
+
+  __device__ __forceinline__ void stage(char* dst, const char* src, int bytes) {
+    for (int blk = w; blk < bytes / 1024; blk += NW) glds16(src + blk * 1024, dst + blk * 1024, lane);
+  }
+
+  __device__ __forceinline__ void start() {
+    wait_vmcnt<0>();
+    __syncthreads();
+    for (int q = 0; q < R - 1; ++q) ring_issue();
+  }
+
+  __device__ __forceinline__ void finish() { wait_vmcnt<0>(); }
+
+  // accumulator init of tile `tile` of layer li (0 = layer 1; nl = the output layer)
+  __device__ __forceinline__ f32x4 bias4(int ni, int li, int tile) const {
+    return *(const f32x4*)((const float*)(lds + bias_off[ni]) + li * W + 16 * tile + 4 * g);
+  }
+
+  // acc += W_hi h_hi + W_hi h_lo + W_lo h_hi over one output tile (image at tp)
+  __device__ __forceinline__ f32x4 tile_product(const char* tp, const u32x4 (&Hh)[KQ], const u32x4 (&Hl)[KQ],
+                                                f32x4 acc) const {
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) {
+      const u32x4 ah = *(const u32x4*)(tp + ((2 * q + 0) * 64 + lane) * 16);
+      const u32x4 al = *(const u32x4*)(tp + ((2 * q + 1) * 64 + lane) * 16);
+      acc = mfma16(ah, Hl[q], acc);
+      acc = mfma16(al, Hh[q], acc);
+      acc = mfma16(ah, Hh[q], acc);
+    }
+    return acc;
+  }
+
+  // activate tile o (compile-time after unrolling) into the (hi, lo) B operands of the next layer
+  template <bool L1>
+  __device__ __forceinline__ void act_store(const f32x4& z, int o, u32x4 (&Oh)[KQ], u32x4 (&Ol)[KQ]) const {
+    float r[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) r[k] = L1 ? x3_act_r2(z[k]) : x3_act_r(z[k]);
+    uint32_t h0, l0, h1, l1;
+    split_pair(r[0], r[1], h0, l0);
+    split_pair(r[2], r[3], h1, l1);
+    const int q = o >> 1, d = (o & 1) * 2;
+    Oh[q][d] = h0, Oh[q][d + 1] = h1;
+    Ol[q][d] = l0, Ol[q][d + 1] = l1;
+  }
+
+  // layer 1 from the resident image and the B operand b1; the activation of tile o - 1 is issued in
+  // tile o's block so it overlaps the MFMAs
+  __device__ __forceinline__ void layer1(int ni, const u32x4 (&b1)[K1Q], u32x4 (&Oh)[KQ], u32x4 (&Ol)[KQ]) {
+    asm volatile("" ::: "memory");
+    const char* l1 = lds + l1_off[ni];
+    f32x4 pend;
+#pragma unroll
+    for (int o = 0; o < ST; ++o) {
+      f32x4 acc = bias4(ni, 0, o);
+#pragma unroll
+      for (int q = 0; q < K1Q; ++q) acc = mfma16(*(const u32x4*)(l1 + ((o * K1Q + q) * 64 + lane) * 16), b1[q], acc);
+      if (o > 0) act_store<true>(pend, o - 1, Oh, Ol);
+      pend = acc;
+    }
+    act_store<true>(pend, ST - 1, Oh, Ol);
+  }
+
+  __device__ __forceinline__ void hidden(int ni, int li, const u32x4 (&Hh)[KQ], const u32x4 (&Hl)[KQ],
+                                         u32x4 (&Oh)[KQ], u32x4 (&Ol)[KQ]) {
+    f32x4 pend;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const char* ch = chunk_sync();
+#pragma unroll
+      for (int t = 0; t < CT; ++t) {
+        const int o = c * CT + t;
+        const f32x4 acc = tile_product(ch + t * TILE, Hh, Hl, bias4(ni, li, o));
+        if (o > 0) act_store<false>(pend, o - 1, Oh, Ol);
+        pend = acc;
+      }
+    }
+    act_store<false>(pend, ST - 1, Oh, Ol);
+  }
+
+  // output rows 0..15 (tile 0 of the output chunk)
+  __device__ __forceinline__ f32x4 output(int ni, const u32x4 (&Hh)[KQ], const u32x4 (&Hl)[KQ]) {
+    const char* ch = chunk_sync();
+    return tile_product(ch, Hh, Hl, bias4(ni, nl, 0));
+  }
+
+  // one network: layer 1, the nl - 1 hidden layers (ping-pong), the output tile
+  __device__ __forceinline__ f32x4 eval(int ni, const u32x4 (&b1)[K1Q]) {
+    u32x4 Ah[KQ], Al[KQ], Bh[KQ], Bl[KQ];
+    layer1(ni, b1, Ah, Al);
+    for (int li = 1; li < nl; li += 2) {
+      hidden(ni, li, Ah, Al, Bh, Bl);
+      if (li + 1 < nl) hidden(ni, li + 1, Bh, Bl, Ah, Al);
+    }
+    if (((nl - 1) & 1) != 0) return output(ni, Bh, Bl);
+    return output(ni, Ah, Al);
+  }
+};
+
+// layer-1 B operand: input n at k-slots 3n (hi), 3n+1 (lo), 3n+2 (hi); lane group g supplies slots
+// 32 q + 8 g + m of its chain
+template <int NV, int K1Q>
+__device__ __forceinline__ void l1_operand(const float (&v)[NV], int g, u32x4 (&b)[K1Q]) {
+  _Float16 vh[NV], vl[NV];
+#pragma unroll
+  for (int n = 0; n < NV; ++n) {
+    vh[n] = (_Float16)v[n];
+    vl[n] = (_Float16)(v[n] - (float)vh[n]);
+  }
+  auto slot = [&](int s) -> _Float16 {
+    const int n = s / 3, p = s % 3;
+    if (n >= NV) return (_Float16)0.0f;
+    return p == 1 ? vl[n] : vh[n];
+  };
+#pragma unroll
+  for (int q = 0; q < K1Q; ++q) {
+    f16x8 e;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const _Float16 c0 = slot(32 * q + m), c1 = slot(32 * q + 8 + m), c2 = slot(32 * q + 16 + m),
+                     c3 = slot(32 * q + 24 + m);
+      e[m] = g == 0 ? c0 : (g == 1 ? c1 : (g == 2 ? c2 : c3));
+    }
+    b[q] = __builtin_bit_cast(u32x4, e);
+  }
+}
+
+// ---------------------------------------------------------------------------- sampler kernel
+// The reverse-SDE loop (models/diffusion.py:27-46) with fp32-accurate networks:
+//   MODE_CDE        a = net(x, y, tau), y folded into the per-y layer-1 bias (f64 prep)
+//   MODE_POSTERIOR  a = g (lik(x, y, tau) + prior(x, tau))            (nets.py:155-157)
+//   MODE_CDIFFE     y_t = eps std(tau) + mean_weight(tau) y, a = net(x, y_t, tau)[:D]   (+ Langevin
+//                   corrector steps before each predictor step)
+// then mu = g a + 0.5 beta x, x <- x + delta mu + sqrt(delta) g xi (dmip_device.h em_update). Work
+// distribution: the balanced WaveSchedule over 16-chain tiles (as dmip_f32.h).
+template <int MODE, int W, int D, int M>
+struct SamplerCfg {
+  static constexpr int NNET = MODE == SAMPLER_POSTERIOR ? 2 : 1;
+  static constexpr int NV = MODE == SAMPLER_CDIFFE ? D + M + 1 : D + 1;  // layer-1 inputs (y folded for CDE)
+  static constexpr int K1Q = k1q_of(NV);
+  using L = XLay<W, NNET, K1Q, M>;
+  using E = XEngine<W, NNET, K1Q, L::R, L::RING>;
+};
+
+template <int MODE, int W, int D, int M, bool NOISE>
+__global__ void __launch_bounds__(Shape<W>::NW * 64, Shape<W>::NW / 4) x3_sampler_kernel(X3SamplerParams p) {
+  using C = SamplerCfg<MODE, W, D, M>;
+  using L = typename C::L;
+  using E = typename C::E;
+  constexpr int NW = Shape<W>::NW, ST = Shape<W>::ST, K1Q = C::K1Q;
+  static_assert(L::TOTAL <= kLdsBudget, "LDS budget");
+  static_assert(D <= 4, "output rows of a chain sit in lane group 0 (D <= 4)");
+  __shared__ __attribute__((aligned(16))) char lds[L::TOTAL];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, j = lane & 15;
+  const int yi = blockIdx.y;
+
+  E eng{lds, {p.net[0].stream, p.net[1].stream}, {L::L1, L::L1 + L::L1_BYTES}, {L::BIAS, L::BIAS + L::BIAS_BYTES}};
+  eng.w = w, eng.lane = lane, eng.g = g;
+  eng.init(p.n_hidden);
+  {
+    const int bf = p.n_hidden * W + 16;
+    for (int ni = 0; ni < C::NNET; ++ni) {
+      eng.stage(lds + L::L1 + ni * L::L1_BYTES, p.net[ni].l1, L::L1_BYTES);
+      float* bl = (float*)(lds + L::BIAS + ni * L::BIAS_BYTES);
+      // CDE / likelihood: layer 1's bias is the per-y c (b1 + W1_y y) (x3_bias_prep_kernel)
+      const bool per_y = ni == 0 && MODE != SAMPLER_CDIFFE;
+      for (int i = threadIdx.x; i < bf; i += NW * 64)
+        bl[i] = (per_y && i < W) ? p.bias_y[(size_t)yi * W + i] : p.net[ni].bias[i];
+    }
+    if constexpr (MODE == SAMPLER_CDIFFE) {
+      float* yo = (float*)(lds + L::YOBS);
+      for (int i = threadIdx.x; i < M; i += NW * 64) yo[i] = p.y_obs[(size_t)yi * M + i];
+    }
+    eng.start();
+  }
+  const float* yobs = (const float*)(lds + L::YOBS);
+
+  const int S = p.num_steps;
+  const long long tiles_y = (p.n_chains + 15) / 16;
+  const long long n_waves = (long long)gridDim.x * NW;  // waves sharing this y
+  const long long gw = (long long)blockIdx.x * NW + w;  // this wave among them
+  constexpr int XW = sampler_xfer_words(D);
+  const WaveSchedule sched(tiles_y, S, n_waves, gw);
+  const size_t noise_step = (size_t)gridDim.y * p.n_chains * D;
+  (void)ST;
+
+  for (int sgi = 0; sgi < sched.n_seg; ++sgi) {
+    const Seg sg = sched.segment(sgi);
+    const long long c_local = (long long)(sg.job >= 0 ? sg.job : 0) * 16 + j;
+    const bool valid = sg.job >= 0 && c_local < p.n_chains;
+    const long long c_rd = valid ? c_local : 0;
+    Rng rng;
+    float x[D];
+    if (sg.kind == 2) {  // resume the tile the previous wave of the grid handed over
+      const size_t slot = (size_t)yi * n_waves + gw - 1;
+      const bool lost = handover_wait(p.xflag + slot, p.spin_limit, p.err, kErrHandover, lane);
+      const float* src = p.xfer + slot * XW;
+#pragma unroll
+      for (int k = 0; k < D; ++k) x[k] = lost ? __builtin_nanf("") : src[k * 64 + lane];
+      rng.s0 = __float_as_uint(src[(D + 0) * 64 + lane]);
+      rng.s1 = __float_as_uint(src[(D + 1) * 64 + lane]);
+      rng.s2 = __float_as_uint(src[(D + 2) * 64 + lane]);
+      rng.s3 = __float_as_uint(src[(D + 3) * 64 + lane]);
+    } else {
+      rng = rng_init(p.seed, (uint64_t)(p.chain_offset + c_local), (uint64_t)yi);
+      float n0[D];
+      if constexpr (NOISE) {
+        const float* src = p.noise + ((size_t)yi * p.n_chains + c_rd) * D;
+#pragma unroll
+        for (int k = 0; k < D; ++k) n0[k] = src[k];
+      } else {
+        rng_normals<D>(rng, n0);
+      }
+#pragma unroll
+      for (int k = 0; k < D; ++k) x[k] = __fadd_rn(__fmul_rn(n0[k], p.stdv), p.mean);
+    }
+
+    SnapCursor snap(p.snap_every, sg.s0);
+    for (int i0 = sg.s0; i0 < sg.s1; ++i0) {
+      const int i = sg.kind == 3 ? 0 : i0;  // idle steps: a dummy tile at step 0, discarded
+      const StepCoef cf = step_coef(i, S, p.T, p.bmin, p.bdiff);
+      float v[C::NV];
+#pragma unroll
+      for (int k = 0; k < D; ++k) v[k] = x[k];
+      if constexpr (MODE == SAMPLER_CDIFFE) {
+        // y_t = eps * std(T-t) + mean_weight(T-t) * y  (sdes.py:37-44)
+        const float mw = vp_mean_weight(cf.tau, p.bmin, p.bdiff);
+        const float sd = vp_std(cf.tau, p.bmin, p.bdiff);
+        float eps[M];
+        rng_normals<M>(rng, eps);
+#pragma unroll
+        for (int k = 0; k < M; ++k) v[D + k] = __fadd_rn(__fmul_rn(eps[k], sd), __fmul_rn(mw, yobs[k]));
+      }
+      v[C::NV - 1] = cf.tau;
+
+      // a(x) at this step's time (and y_t): output rows 0..D-1 of every chain, on all its lanes. Always
+      // inlined: an outlined call would put the activation arrays on the scratch stack.
+      auto score = [&](const float (&vin)[C::NV], float (&a)[D]) __attribute__((always_inline)) {
+        u32x4 b1[K1Q];
+        l1_operand<C::NV, K1Q>(vin, g, b1);
+        f32x4 out = eng.eval(0, b1);
+        if constexpr (C::NNET > 1) out = out + eng.eval(1, b1);  // likelihood + prior, then g * (...)
+#pragma unroll
+        for (int k = 0; k < D; ++k) a[k] = __shfl(out[k], j, 64);
+      };
+
+      if constexpr (MODE == SAMPLER_CDIFFE) {
+        // Langevin corrector steps (dmip_kernels.hip's definition): s = a / g, eps = 2 alpha
+        // (snr |z| / |s|)^2, x <- x + eps s + sqrt(2 eps) z, alpha = exp(-beta delta)
+        for (int c = 0; c < p.n_corr; ++c) {
+          float oc[D];
+          score(v, oc);
+          float z[D], sc[D];
+          rng_normals<D>(rng, z);
+          float zn = 0.0f, sn = 0.0f;
+#pragma unroll
+          for (int k = 0; k < D; ++k) {
+            sc[k] = oc[k] / cf.g;
+            zn += z[k] * z[k];
+            sn += sc[k] * sc[k];
+          }
+          const float alpha = __expf(-cf.beta * p.delta);
+          const float r = p.snr * p.snr * zn / fmaxf(sn, 1e-30f);
+          const float es = 2.0f * alpha * r;
+          const float ns = __fsqrt_rn(2.0f * es);
+#pragma unroll
+          for (int k = 0; k < D; ++k) {
+            x[k] = x[k] + es * sc[k] + ns * z[k];
+            v[k] = x[k];
+          }
+        }
+      }
+
+      float a[D];
+      score(v, a);
+      float xi[D];
+      if constexpr (NOISE) {
+        const float* src = p.noise + noise_step * (i + 1) + ((size_t)yi * p.n_chains + c_rd) * D;
+#pragma unroll
+        for (int k = 0; k < D; ++k) xi[k] = src[k];
+      } else {
+        rng_normals<D>(rng, xi);
+      }
+#pragma unroll
+      for (int k = 0; k < D; ++k) {
+        const float ak = MODE == SAMPLER_POSTERIOR ? __fmul_rn(cf.g, a[k]) : a[k];
+        x[k] = em_update(x[k], ak, xi[k], cf, p.delta, p.sqrt_delta);
+      }
+      snap.at_step<D>(i0, p.snap_every, p.snap_out, gridDim.y, yi, p.n_chains, c_local,
+                      sg.kind != 3 && valid && g == 0, x);
+    }
+    if (sg.kind == 1) {  // hand the tile over to the next wave of the grid
+      const size_t slot = (size_t)yi * n_waves + gw;
+      float* dst = p.xfer + slot * XW;
+#pragma unroll
+      for (int k = 0; k < D; ++k) dst[k * 64 + lane] = x[k];
+      dst[(D + 0) * 64 + lane] = __uint_as_float(rng.s0);
+      dst[(D + 1) * 64 + lane] = __uint_as_float(rng.s1);
+      dst[(D + 2) * 64 + lane] = __uint_as_float(rng.s2);
+      dst[(D + 3) * 64 + lane] = __uint_as_float(rng.s3);
+      handover_publish(p.xflag + slot, lane, p.debug_flags);
+    } else if (sg.kind != 3 && valid && g == 0) {
+      float* dst = p.x_out + ((size_t)yi * p.n_chains + c_local) * D;
+#pragma unroll
+      for (int k = 0; k < D; ++k) dst[k] = x[k];
+    }
+  }
+  eng.finish();
+}
+
+}  // namespace x3
+
+// ----------------------------------------------------------------- launch helpers (per TU)
+template <int MODE, int W, int D, int M, bool NOISE>
+inline hipError_t launch_x3_sampler_t(const X3SamplerParams& p, int n_y, hipStream_t st) {
+  constexpr int NW = x3::Shape<W>::NW;
+  auto kern = x3::x3_sampler_kernel<MODE, W, D, M, NOISE>;
+  const long long tiles = (p.n_chains + 15) / 16;
+  long long g = resident_slots(kern, NW * 64, st) / (n_y > 0 ? n_y : 1);
+  const long long cap = (tiles + NW - 1) / NW;
+  if (g > cap) g = cap;
+  if (g < 1) g = 1;
+  // the balanced schedule's hand-over needs every workgroup of the grid resident at once: g is
+  // capped by the stream device's occupancy above
+  X3SamplerParams q = p;
+  char* buf = nullptr;
+  hipError_t e = alloc_handover((size_t)g * n_y * NW, D, st, &buf, &q.xfer, &q.xflag);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(kern, dim3((unsigned)g, (unsigned)n_y), dim3(NW * 64), 0, st, q);
+  e = hipGetLastError();
+  (void)hipFreeAsync(buf, st);
+  return e;
+}
+
+template <int MODE, int W, int D, int M>
+inline hipError_t launch_x3_sampler_n(const X3SamplerParams& p, int n_y, hipStream_t st) {
+  if constexpr (MODE == SAMPLER_CDE) {
+    if (p.noise) return launch_x3_sampler_t<MODE, W, D, M, true>(p, n_y, st);
+  }
+  return launch_x3_sampler_t<MODE, W, D, M, false>(p, n_y, st);
+}
+
+// per-mode instantiations (dmip_x3_{cde,post,cdiffe}.hip)
+hipError_t launch_x3_sampler_cde(const X3SamplerParams& p, int width, int xdim, int n_y, hipStream_t st, bool* ok);
+hipError_t launch_x3_sampler_post(const X3SamplerParams& p, int width, int xdim, int n_y, hipStream_t st, bool* ok);
+hipError_t launch_x3_sampler_cdiffe(const X3SamplerParams& p, int width, int xdim, int ydim, int n_y, hipStream_t st,
+                                    bool* ok);
+
+}  // namespace dmip

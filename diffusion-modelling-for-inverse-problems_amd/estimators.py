@@ -7,12 +7,16 @@ reverse-SDE kernel for all num_steps, the chain state never leaving the register
   * PosteriorDiffusionEstimator: dmip_em_sample_posterior (prior + likelihood networks in one kernel);
   * CDiffE (repaired sampler): dmip_em_sample_cdiffe;
   * DPS (BASELINE config 4, prior score net + forward-model guidance): dmip_dps_sample.
-Precision (`model.precision`, or `precision=` per call; default from $DMIP_PRECISION, else "bf16"):
-"bf16" runs the network GEMMs with bf16 MFMA operands (the throughput mode, BASELINE headline);
-"fp32" runs them in exact f32 (v_mfma_f32_16x16x4_f32), the reference's own arithmetic (the parity
-mode). A shape with a fused f32 kernel but no fused bf16 one (the Posterior / CDiffE samplers at width
-512) runs the f32 kernel. Shapes with no fused kernel at all step through per-step launches of the
-network kernel (dmip_mlp_forward) with the SDE update as device tensor ops and the kernels'
+Precision (`model.precision`, or `precision=` per call; default from $DMIP_PRECISION, else "fp32x3"):
+  "fp32x3" -- the reference's fp32 arithmetic at the fp16 matrix rate: every product as three fp16 MFMAs
+             (W_hi h_hi + W_hi h_lo + W_lo h_hi, fp32 accumulation; csrc/dmip_x3.h), tanh by exp2 + rcp.
+             Error per product 2^-23 of sum |w h|, as an fp32 fmaf chain. The default.
+  "fp32"   -- exact f32 (v_mfma_f32_16x16x4_f32, an fmaf chain, libm tanh): the bit-level parity mode.
+  "bf16"   -- 16-bit MFMA operands (fp16 hidden and output layers, split-bf16 layer 1): the fastest
+             mode, ~1e-3 relative per network evaluation.
+A shape without a fused kernel in the requested precision runs the next more accurate one that has one
+(bf16 -> fp32x3 -> fp32). Shapes with no fused kernel at all step through per-step launches of the
+network kernel (dmip_mlp_forward, exact f32) with the SDE update as device tensor ops and the kernels'
 chain-keyed RNG (so sharding stays bit-identical there too).
 There is no CPU sampling path: without a HIP device the samplers raise.
 
@@ -47,17 +51,21 @@ def _draw_seed():
 
 
 def default_precision():
-    return os.environ.get("DMIP_PRECISION", "bf16")
+    return os.environ.get("DMIP_PRECISION", "fp32x3")
+
+
+# a precision whose fused kernel is missing for a shape falls back to a more accurate one, never a less
+# accurate one: bf16 -> fp32x3 -> fp32
+_MORE_ACCURATE = {"bf16": ("fp32x3", "fp32"), "fp32x3": ("fp32",), "fp32": ()}
 
 
 def _fused_precision(precision, mode, width, n_hidden, xdim, ydim):
-    """The precision a fused kernel runs this shape in: the requested one, else exact f32 when only
-    that is compiled (bf16 -> fp32 never loses accuracy); None when neither is (per-step loop)."""
+    """The precision a fused kernel runs this shape in: the requested one, else the next more accurate
+    one that is compiled (_MORE_ACCURATE); None when none is (per-step loop)."""
     _lib.precision_code(precision)
-    if _lib.sampler_supported(width, n_hidden, xdim, ydim, mode, precision):
-        return precision
-    if precision == "bf16" and _lib.sampler_supported(width, n_hidden, xdim, ydim, mode, "fp32"):
-        return "fp32"
+    for prec in (precision,) + _MORE_ACCURATE[precision]:
+        if _lib.sampler_supported(width, n_hidden, xdim, ydim, mode, prec):
+            return prec
     return None
 
 
@@ -68,7 +76,7 @@ class BaseClassDiffusionModel:
         self.xdim = xdim
         self.ydim = ydim
         self.sde = None
-        self.precision = default_precision()  # "bf16" | "fp32": arithmetic of the sampler's network GEMMs
+        self.precision = default_precision()  # "fp32x3" | "fp32" | "bf16": arithmetic of the sampler's networks
 
     def __call__(self, *args, **kwargs):
         return self.forward(*args, **kwargs)
@@ -135,7 +143,7 @@ class BaseClassDiffusionModel:
         """Device-resident samples (n_y, num_samples, xdim) for ys (n_y, ydim) -- no host copy.
         `chain_offset` selects a shard of a larger run; `noise` injects standard normals
         (num_steps + 1, n_y, num_samples, xdim) (slot 0 -> x0) in place of the internal RNG;
-        `precision` ("bf16" | "fp32") overrides self.precision."""
+        `precision` ("fp32x3" | "fp32" | "bf16") overrides self.precision."""
         raise NotImplementedError
 
     def _prepare(self, y, num_samples, num_steps, nets):

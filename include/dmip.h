@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define DMIP_ABI_VERSION 5
+#define DMIP_ABI_VERSION 6
 
 typedef enum {
   DMIP_OK = 0,
@@ -44,9 +44,14 @@ typedef enum { DMIP_ACT_TANH_TWICE_FIRST = 0, DMIP_ACT_TANH = 1 } dmip_act;
  *                   layer 1's double tanh in packed fp16. The throughput mode (BASELINE headline).
  *   DMIP_PREC_F32   exact f32: every product and sum in f32 (v_mfma_f32_16x16x4_f32, an fmaf chain),
  *                   libm-accurate tanh -- the reference's own arithmetic (nets.py:32-35 in fp32).
- *                   The parity mode; ~1/6 of the bf16 throughput. Same RNG stream per chain as bf16,
- *                   so the two modes are comparable chain by chain. */
-typedef enum { DMIP_PREC_BF16 = 0, DMIP_PREC_F32 = 1 } dmip_precision;
+ *                   The bit-level parity mode; ~1/10 of the bf16 throughput.
+ *   DMIP_PREC_F32X3 fp32-accurate at the fp16 matrix rate: every product as the three-term fp16 split
+ *                   W_hi h_hi + W_hi h_lo + W_lo h_hi on v_mfma_f32_16x16x32_f16 (fp32 accumulation; error
+ *                   2^-23.2 of sum |w h| measured against 2^-23.0 for an f32 fmaf chain), tanh by exp2 + rcp
+ *                   at ~1 ulp (no polynomial). The reference-precision throughput mode (samplers; the
+ *                   network forward runs the exact-f32 kernel).
+ * All three draw the same RNG stream per chain, so the modes are comparable chain by chain. */
+typedef enum { DMIP_PREC_BF16 = 0, DMIP_PREC_F32 = 1, DMIP_PREC_F32X3 = 2 } dmip_precision;
 
 /* VariancePreservingSDE (sdes.py:9-19): beta(t) = beta_min + (beta_max - beta_min) t. */
 typedef struct {
@@ -385,6 +390,9 @@ int dmip_device_status(void* stream);
  * hidden layers, xdim 2 or 3; CDiffE for (xdim, ydim) = (2, 2) and (3, 23)). */
 int dmip_sampler_supported(int mode, int width, int n_hidden, int xdim, int ydim);
 int dmip_sampler_supported_f32(int mode, int width, int n_hidden, int xdim, int ydim);
+/* The same question for any dmip_precision (DMIP_PREC_F32X3: widths 64/128/256/512, 1-3 hidden layers,
+ * xdim 2 or 3; CDiffE for (xdim, ydim) = (2, 2), and (3, 23) up to width 256). */
+int dmip_sampler_supported_precision(int precision, int mode, int width, int n_hidden, int xdim, int ydim);
 
 #ifdef __cplusplus
 }

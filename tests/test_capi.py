@@ -32,7 +32,7 @@ def test_exports_every_declared_symbol(lib, dmip):
 
 
 def test_abi_version(lib, dmip):
-    assert lib.dmip_abi_version() == dmip._lib.ABI_VERSION == 5
+    assert lib.dmip_abi_version() == dmip._lib.ABI_VERSION == 6
 
 
 def test_supported_shapes(lib, dmip):
@@ -50,6 +50,13 @@ def test_supported_shapes(lib, dmip):
     for mode in (0, P, C):
         assert sup(512, 3, 3, 23, mode, "fp32") and sup(64, 2, 2, 2, mode, "fp32") and sup(256, 1, 3, 23, mode, "fp32")
     assert not sup(96, 3, 3, 23, 0, "fp32") and not sup(256, 4, 3, 23, 0, "fp32") and not sup(256, 3, 3, 5, C, "fp32")
+    # fp32x3 (split fp16): every mode at widths 64..512 and 1..3 hidden layers; CDiffE scatterometry to 256
+    for mode in (0, P, C):
+        assert sup(256, 3, 3, 23, mode, "fp32x3") and sup(64, 1, 2, 2, mode, "fp32x3")
+        assert sup(512, 3, 2, 2, mode, "fp32x3")
+    assert sup(512, 3, 3, 23, 0, "fp32x3") and sup(512, 3, 3, 23, P, "fp32x3") and sup(256, 3, 3, 9, 0, "fp32x3")
+    assert not sup(512, 3, 3, 23, C, "fp32x3") and not sup(256, 4, 3, 23, 0, "fp32x3")
+    assert not sup(96, 3, 3, 23, 0, "fp32x3") and not sup(256, 3, 3, 5, C, "fp32x3")
     with pytest.raises(ValueError):
         sup(256, 3, 3, 23, 0, "fp16")
 

@@ -1,0 +1,262 @@
+"""The fp32-accurate split-fp16 sampler (DMIP_PREC_F32X3, csrc/dmip_x3.h) -- the package's default
+precision -- against the reference's own trajectories and draws, the oracle, and the exact-f32 engine.
+Every test here needs an MI355X: run with `pytest -m gpu`.
+
+The engine claims the reference's fp32 arithmetic, so it is held to the exact-f32 engine's gates
+(test_gpu_f32.py), not the 16-bit engine's:
+  * injected-noise trajectories (fixture G3, the reference's own x0 and per-step noise): final samples
+    within 1e-3 max|x| after all steps (1e-4 for the short runs) -- the oracle's own bound;
+  * product-RNG samplers vs the float32 oracle (same chains): 1e-4 max(1, |x|) after 6 steps;
+  * posteriors at 100k samples vs the reference's draws: KS (alpha = 0.01) against the 20k draws and the
+    100k-run quantiles, per-dimension and sliced W1 <= 3x the null level (metrics.parity_report);
+  * against the exact-f32 engine on the same chains over 1000 steps: the two fp32 engines agree to
+    within the G3 bound too.
+Observed values are printed (pytest -s) and recorded in DESIGN.md §3c.
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+from conftest import state_from_npz
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+PREC = "fp32x3"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+
+
+def _cde(dmip, tag, z):
+    xd, yd, hl = {"lin": (2, 2, [64] * 3), "scat": (3, 23, [256] * 3)}[tag]
+    m = dmip.CDE(xd, yd, hl)
+    m.sde.a.load_state_dict(state_from_npz(z))
+    return m
+
+
+def _linear_params(net):
+    return [(l.weight.detach().cpu().numpy(), l.bias.detach().cpu().numpy())
+            for l in net if isinstance(l, torch.nn.Linear)]
+
+
+def _rel(out, ref):
+    return float(np.abs(out - ref).max() / max(1.0, np.abs(ref).max()))
+
+
+def test_default_precision_is_fp32x3(dmip):
+    m = dmip.CDE(3, 23, [256] * 3)
+    assert m.precision == PREC
+    assert dmip._lib.sampler_supported(256, 3, 3, 23, dmip._lib.DMIP_SAMPLER_CDE, PREC)
+
+
+# ------------------------------------------------------------- injected-noise trajectories (A2)
+@pytest.mark.parametrize("tag", ["lin", "scat"])
+def test_x3_trajectory_injected_noise_matches_reference(dmip, golden, tag):
+    """The reference's own x0 and per-step noise (G3) through the fused f32x3 sampler."""
+    tr = golden(f"traj_{tag}.npz")
+    m = _cde(dmip, tag, golden(f"ckpt_{tag}.npz"))
+    S = int(tr["num_steps"])
+    noise = np.concatenate([tr["x0"][None], tr["xi"]], 0)[:, None]
+    n = tr["x0"].shape[0]
+    before = dmip._lib.calls["em_sample"]
+    out = m.sample_device(torch.from_numpy(tr["y"]).to(DEV), n, S, noise=torch.from_numpy(noise).to(DEV),
+                          precision=PREC)[0].cpu().numpy()
+    assert dmip._lib.calls["em_sample"] == before + 1
+    ref = tr["x_final"]
+    assert np.all(np.isfinite(out))
+    err = _rel(out, ref)
+    print(f"\n[x3] G3 {tag}: {S} steps, max err / max|x| = {err:.3e}")
+    assert err < 1e-3, err
+    Ss = int(tr["steps_short"])
+    ns = np.concatenate([tr["x0_short"][None], tr["xi_short"]], 0)[:, None]
+    out_s = m.sample_device(torch.from_numpy(tr["y"]).to(DEV), n, Ss, noise=torch.from_numpy(ns).to(DEV),
+                            precision=PREC)[0].cpu().numpy()
+    err_s = _rel(out_s, tr["x_final_short"])
+    print(f"[x3] G3 {tag}: {Ss} steps, max err / max|x| = {err_s:.3e}")
+    assert err_s < 1e-4, err_s
+
+
+# ------------------------------------------------------------------- product-RNG samplers vs the oracle
+@pytest.mark.parametrize("W", [64, 128, 256, 512])
+@pytest.mark.parametrize("NL", [1, 2, 3])
+@pytest.mark.parametrize("xd,yd", [(2, 2), (3, 23)])
+def test_x3_cde_sampler_vs_oracle(dmip, W, NL, xd, yd):
+    torch.manual_seed(W + NL + xd)
+    m = dmip.CDE(xd, yd, [W] * NL)
+    params = _linear_params(m.sde.a)
+    y = np.random.default_rng(5).uniform(0, 1, yd).astype(np.float32)
+    n, S, seed = 700, 6, 99
+    x = m.sample_device(torch.from_numpy(y).to(DEV), n, S, seed=seed, precision=PREC)[0].cpu().numpy()
+    ref = O.cde_sample(params, y, n, S, seed)
+    err = _rel(x, ref)
+    print(f"\n[x3] CDE W={W} L={NL} x{xd}: {err:.3e}")
+    assert err < 1e-4, err
+
+
+@pytest.mark.parametrize("W", [64, 256, 512])
+@pytest.mark.parametrize("NL", [2, 3])
+@pytest.mark.parametrize("xd,yd", [(2, 2), (3, 23)])
+def test_x3_posterior_sampler_vs_oracle(dmip, W, NL, xd, yd):
+    torch.manual_seed(W + xd + NL)
+    m = dmip.PosteriorDiffusionEstimator(xd, yd, [W] * NL)
+    prior, lik = _linear_params(m.sde.a.prior_net), _linear_params(m.sde.a.likelihood_net)
+    y = np.random.default_rng(7).uniform(0, 1, yd).astype(np.float32)
+    n, S, seed = 700, 6, 31
+    before = dmip._lib.calls["em_sample_posterior"]
+    x = m.sample_device(torch.from_numpy(y).to(DEV), n, S, seed=seed, precision=PREC)[0].cpu().numpy()
+    assert dmip._lib.calls["em_sample_posterior"] == before + 1
+    ref = O.posterior_sample(prior, lik, y, n, S, seed)
+    err = _rel(x, ref)
+    print(f"\n[x3] Posterior W={W} L={NL} x{xd}: {err:.3e}")
+    assert err < 1e-4, err
+
+
+@pytest.mark.parametrize("W,xd,yd", [(64, 2, 2), (256, 2, 2), (512, 2, 2), (64, 3, 23), (128, 3, 23), (256, 3, 23)])
+def test_x3_cdiffe_sampler_vs_oracle(dmip, W, xd, yd):
+    torch.manual_seed(3 * W + xd)
+    m = dmip.CDiffE(xd, yd, [W] * 3)
+    params = _linear_params(m.sde.a)
+    y = np.random.default_rng(8).uniform(0, 1, yd).astype(np.float32)
+    n, S, seed = 700, 6, 57
+    before = dmip._lib.calls["em_sample_cdiffe"]
+    x = m.sample_device(torch.from_numpy(y).to(DEV), n, S, seed=seed, precision=PREC)[0].cpu().numpy()
+    assert dmip._lib.calls["em_sample_cdiffe"] == before + 1
+    ref = O.cdiffe_sample(params, y, n, S, seed)
+    err = _rel(x, ref)
+    print(f"\n[x3] CDiffE W={W} x{xd}: {err:.3e}")
+    assert err < 1e-4, err
+
+
+def test_x3_cdiffe_predictor_corrector_vs_oracle(dmip):
+    torch.manual_seed(11)
+    m = dmip.CDiffE(3, 23, [256] * 3)
+    with torch.no_grad():
+        last = [l for l in m.sde.a if isinstance(l, torch.nn.Linear)][-1]
+        last.weight.mul_(0.05)
+        last.bias.fill_(0.5)
+    params = _linear_params(m.sde.a)
+    y = np.random.default_rng(8).uniform(0, 1, 23).astype(np.float32)
+    n, S, seed = 700, 5, 77
+    x = m.sample_device(torch.from_numpy(y).to(DEV), n, S, seed=seed, corrector_steps=2, snr=0.16,
+                        precision=PREC)[0].cpu().numpy()
+    ref = O.cdiffe_sample(params, y, n, S, seed, corrector_steps=2, snr=0.16)
+    x0 = O.cdiffe_sample(params, y, n, S, seed)
+    assert np.abs(ref - x0).max() > 1e-2  # the corrector moves the chains
+    err = _rel(x, ref)
+    print(f"\n[x3] CDiffE PC: {err:.3e}")
+    assert err < 1e-4, err
+
+
+def test_x3_cdiffe_scat_width512_falls_back_to_exact_f32(dmip):
+    """CDiffE scatterometry at width 512 has no f32x3 kernel (layer-1 image too large): a fp32x3 request
+    runs the exact-f32 kernel (more accurate, never less)."""
+    est = __import__("importlib").import_module("diffusion-modelling-for-inverse-problems_amd.estimators")
+    assert not dmip._lib.sampler_supported(512, 3, 3, 23, dmip._lib.DMIP_SAMPLER_CDIFFE, PREC)
+    assert est._fused_precision(PREC, dmip._lib.DMIP_SAMPLER_CDIFFE, 512, 3, 3, 23) == "fp32"
+    assert est._fused_precision("bf16", dmip._lib.DMIP_SAMPLER_CDIFFE, 512, 3, 3, 23) == "bf16"
+
+
+# ------------------------------------------------------- the two fp32 engines over a long trajectory
+@pytest.mark.parametrize("tag", ["lin", "scat"])
+def test_x3_matches_exact_f32_engine_over_1000_steps(dmip, golden, tag):
+    """Same chains (same RNG stream), 1000 steps, trained fixture weights: f32x3 vs exact f32."""
+    m = _cde(dmip, tag, golden(f"ckpt_{tag}.npz"))
+    y = torch.from_numpy(golden(f"samples_{tag}.npz")["y"]).to(DEV)
+    a = m.sample_device(y, 20000, 1000, seed=123, precision=PREC)[0].cpu().numpy()
+    b = m.sample_device(y, 20000, 1000, seed=123, precision="fp32")[0].cpu().numpy()
+    err = _rel(a, b)
+    q = np.quantile(np.abs(a - b).max(1), [0.5, 0.99])
+    print(f"\n[x3] vs exact f32, {tag}, 1000 steps: max {err:.3e}, per-chain median {q[0]:.2e}, p99 {q[1]:.2e}")
+    assert err < 1e-3, err
+
+
+# ------------------------------------------------------------------- sharding / schedule / snapshots
+@pytest.mark.parametrize("cls", ["CDE", "PosteriorDiffusionEstimator", "CDiffE"])
+def test_x3_shards_and_batches_bit_identical(dmip, cls):
+    torch.manual_seed(13)
+    m = getattr(dmip, cls)(3, 23, [256] * 3)
+    ys = torch.from_numpy(np.random.default_rng(9).uniform(0, 1, (3, 23)).astype(np.float32)).to(DEV)
+    n, S, seed = 1000, 10, 5
+    full = m.sample_device(ys, n, S, seed=seed, precision=PREC)
+    shard = m.sample_device(ys, 300, S, seed=seed, chain_offset=500, precision=PREC)
+    assert torch.equal(full[:, 500:800], shard)
+    assert torch.equal(m.sample_device(ys, n, S, seed=seed, precision=PREC), full)
+    assert not torch.equal(full[0], full[1])
+
+
+@pytest.mark.parametrize("cls,W,n", [("CDE", 256, 70001), ("CDE", 512, 40001), ("PosteriorDiffusionEstimator", 256, 70001),
+                                     ("CDiffE", 256, 70001)])
+def test_x3_balanced_schedule_matches_unsplit_runs(dmip, cls, W, n):
+    """More chains than one GPU round: tiles split between waves through the balanced schedule; every
+    chain equals a launch small enough to run each tile whole."""
+    torch.manual_seed(W + n)
+    m = getattr(dmip, cls)(3, 23, [W] * 3)
+    y = torch.from_numpy(np.random.default_rng(5).uniform(0, 1, 23).astype(np.float32)).to(DEV)
+    S = 6
+    full = m.sample_device(y, n, S, seed=11, precision=PREC)[0]
+    for lo in (0, n // 2 + 5, n - 333):
+        part = m.sample_device(y, 333, S, seed=11, chain_offset=lo, precision=PREC)[0]
+        assert torch.equal(full[lo:lo + 333], part), lo
+    assert torch.isfinite(full).all()
+
+
+def test_x3_handover_timeout_is_reported_not_silent(dmip, golden, monkeypatch):
+    m = _cde(dmip, "scat", golden("ckpt_scat.npz"))
+    y = torch.from_numpy(golden("data_scat.npz")["y_test"][0]).to(DEV)
+    monkeypatch.setenv("DMIP_DEBUG_NO_HANDOVER", "1")
+    x = m.sample_device(y, 50000, 4, seed=1, precision=PREC)
+    with pytest.raises(RuntimeError, match="hand-over"):
+        dmip._lib.device_status(x.device)
+    assert torch.isnan(x).any() and torch.isfinite(x).any()
+    monkeypatch.delenv("DMIP_DEBUG_NO_HANDOVER")
+    x = m.sample_device(y, 50000, 4, seed=1, precision=PREC)
+    dmip._lib.device_status(x.device)
+    assert torch.isfinite(x).all()
+
+
+@pytest.mark.parametrize("cls", ["CDE", "PosteriorDiffusionEstimator", "CDiffE"])
+def test_x3_snapshots(dmip, cls):
+    """Trajectory snapshots through the balanced schedule: last snapshot = output = plain sampler, and a
+    shard's snapshots are slices of the whole run's; CDE's snapshots against the oracle's loop states."""
+    xd, yd = (3, 23) if cls != "CDiffE" else (2, 2)
+    torch.manual_seed(1)
+    m = getattr(dmip, cls)(xd, yd, [64] * 3)
+    y = torch.from_numpy(np.random.default_rng(2).uniform(0, 1, (2, yd)).astype(np.float32)).to(DEV)
+    n, S, every, seed = 90000, 40, 8, 7
+    x, snaps = m.sample_trajectory(y, n, S, every, seed=seed, precision=PREC)
+    assert tuple(snaps.shape) == (S // every, 2, n, xd)
+    assert torch.equal(snaps[-1], x) and torch.isfinite(snaps).all()
+    assert torch.equal(m.sample_device(y, n, S, seed=seed, precision=PREC), x)
+    lo, hi = 30011, 61000
+    xs, ss = m.sample_trajectory(y, hi - lo, S, every, seed=seed, chain_offset=lo, precision=PREC)
+    assert torch.equal(ss, snaps[:, :, lo:hi]) and torch.equal(xs, x[:, lo:hi])
+    if cls == "CDE":
+        params = _linear_params(m.sde.a)
+        yy = y[0].cpu().numpy()
+        xs1, sn1 = m.sample_trajectory(y[:1], 700, 6, 2, seed=99, precision=PREC)
+        _, ref_snaps = O.cde_sample(params, yy, 700, 6, 99, snapshots={2, 4, 6})
+        for k in range(3):
+            r = ref_snaps[(k + 1) * 2]
+            assert _rel(sn1[k, 0].cpu().numpy(), r) < 1e-4
+
+
+# ---------------------------------------------- distributional parity vs the reference (§8c)
+@pytest.mark.parametrize("tag", ["lin", "scat"])
+def test_x3_posterior_parity_fp32_gate(dmip, golden, tag):
+    """100k samples against the reference sampler's draws on the same weights and y: the fp32 gate."""
+    import importlib
+    M = importlib.import_module("diffusion-modelling-for-inverse-problems_amd.metrics")
+    smp = golden(f"samples_{tag}.npz")
+    m = _cde(dmip, tag, golden(f"ckpt_{tag}.npz"))
+    S = int(smp["num_steps"])
+    torch.manual_seed(0)
+    x = m(torch.from_numpy(smp["y"]).to(DEV), num_samples=100000, num_steps=S)  # the default precision
+    assert x.shape == (100000, smp["samples"].shape[1]) and np.all(np.isfinite(x))
+    r = M.parity_report(x, smp["samples"], smp["quantiles"], int(smp["n_total"]))
+    print(f"\n[x3] parity {tag}: {r}")
+    assert r["pass"], r
