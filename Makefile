@@ -41,12 +41,13 @@ $(CSRC)/dmip_f32.o: $(CSRC)/dmip_f32.hip $(CSRC)/dmip_f32.h $(HDRS)
 $(CSRC)/dmip_f32_%.o: $(CSRC)/dmip_f32_%.hip $(CSRC)/dmip_f32.h $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-# fp32-accurate split-fp16 engine (DMIP_PREC_F32X3): one header, four translation units
+# fp32-accurate split-fp16 engine (DMIP_PREC_F32X3): one header, four translation units; no SLP
+# vectorisation (it packs the split's f32 subtractions into v_pk_add_f32, an anti-lever beside MFMAs)
 $(CSRC)/dmip_x3.o: $(CSRC)/dmip_x3.hip $(CSRC)/dmip_x3.h $(HDRS)
-	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) -fno-slp-vectorize -c $< -o $@
 
 $(CSRC)/dmip_x3_%.o: $(CSRC)/dmip_x3_%.hip $(CSRC)/dmip_x3.h $(HDRS)
-	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) -fno-slp-vectorize -c $< -o $@
 
 $(CSRC)/dmip_capi.o: $(CSRC)/dmip_capi.cpp $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@

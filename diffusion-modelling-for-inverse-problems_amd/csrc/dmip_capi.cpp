@@ -1236,6 +1236,27 @@ struct dmip_train_plan {
   int device = 0;
 };
 
+// makes `dev` the current device for the guard's scope (and restores the caller's)
+struct DeviceGuard {
+  int prev = -1, dev = -1;
+  explicit DeviceGuard(int d) : dev(d) {
+    if (hipGetDevice(&prev) == hipSuccess && prev != dev && dev >= 0) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    if (prev >= 0 && prev != dev && dev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+// the device that owns a device pointer (the current device if the runtime cannot tell)
+static int pointer_device(const void* p) {
+  hipPointerAttribute_t a{};
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  if (p && hipPointerGetAttributes(&a, p) == hipSuccess && a.device >= 0) return a.device;
+  (void)hipGetLastError();  // clear a sticky error from a non-device pointer
+  return cur;
+}
+
 static void plan_free(dmip_train_plan* pl) {
   if (!pl) return;
   if (pl->exec) (void)hipGraphExecDestroy(pl->exec);
@@ -1286,6 +1307,9 @@ int dmip_train_plan_create(const dmip_train_plan_desc* d, dmip_train_plan** out)
   for (int k = 1; k < d->n_tensors; ++k)
     if (d->grads[k] != d->grads[0] + ap.off[k])
       return fail(DMIP_ERR_INVALID, "grads must be consecutive views of one flat buffer (reference parameter order)");
+  // everything the plan allocates, and its capture stream, live on the parameters' device, whatever the
+  // caller's current device is (the weights, optimizer state and the replay stream are that device's)
+  const DeviceGuard guard(pointer_device(d->weights_dev[0]));
   auto* pl = new dmip_train_plan();
   pl->batch = d->batch;
   pl->xdim = d->xdim;
@@ -1293,7 +1317,7 @@ int dmip_train_plan_create(const dmip_train_plan_desc* d, dmip_train_plan** out)
   pl->t = d->t_dev;
   pl->eps = d->eps_dev;
   pl->loss = d->loss_dev;
-  (void)hipGetDevice(&pl->device);
+  pl->device = guard.dev;
   const int64_t B = d->batch;
   auto alloc = [&](void** q, size_t bytes) { return hipMalloc(q, bytes < 4 ? 4 : bytes); };
   hipError_t e = hipSuccess;
@@ -1366,6 +1390,7 @@ int dmip_train_plan_create(const dmip_train_plan_desc* d, dmip_train_plan** out)
 int dmip_train_plan_step(dmip_train_plan* pl, const float* x_dev, const float* y_dev, void* stream) {
   if (!pl || !x_dev || (pl->ydim > 0 && !y_dev)) return fail(DMIP_ERR_INVALID, "null argument");
   hipStream_t st = (hipStream_t)stream;
+  const DeviceGuard guard(pl->device);
   hipError_t e = hipMemcpyAsync(pl->x, x_dev, (size_t)pl->batch * pl->xdim * 4, hipMemcpyDeviceToDevice, st);
   if (e == hipSuccess && pl->ydim > 0)
     e = hipMemcpyAsync(pl->y, y_dev, (size_t)pl->batch * pl->ydim * 4, hipMemcpyDeviceToDevice, st);
@@ -1384,7 +1409,9 @@ int dmip_train_plan_set_counters(dmip_train_plan* pl, uint64_t draws_done, int64
 }
 
 int dmip_train_plan_destroy(dmip_train_plan* pl) {
-  if (pl) (void)hipDeviceSynchronize();  // no replay may still be running
+  if (!pl) return DMIP_OK;
+  const DeviceGuard guard(pl->device);
+  (void)hipDeviceSynchronize();  // no replay may still be running on the plan's device
   plan_free(pl);
   return DMIP_OK;
 }

@@ -80,11 +80,88 @@ struct XLay {
   static_assert(R >= 2, "LDS budget: fewer than two ring slots");
 };
 
-// split a pair of f32 values into an (hi, lo) pair of packed fp16 dwords: v = hi + lo to ~2^-22 |v|
+// split a pair of f32 values into an (hi, lo) pair of packed fp16 dwords: v = hi + lo to ~2^-22 |v|.
+// lo = fp16(v - hi) in one instruction per half: v_fma_mix{lo,hi}_f16 takes hi as an fp16 operand,
+// forms v - hi exactly and rounds once (3 instructions per pair instead of cvt, 2 cvt back, 2 sub, cvt;
+// bit-identical, scripts/ubench/fma_mix_check.hip)
 __device__ __forceinline__ void split_pair(float a, float b, uint32_t& hi, uint32_t& lo) {
   hi = cvt_pk_f16(a, b);
-  const f16x2 h = __builtin_bit_cast(f16x2, hi);
-  lo = cvt_pk_f16(a - (float)h[0], b - (float)h[1]);
+  asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(lo) : "v"(hi), "v"(a));
+  asm("v_fma_mixhi_f16 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(lo) : "v"(hi), "v"(b));
+}
+
+// A-fragment reads of the MFMA chains: explicit ds_read_b128 kept PF k-steps ahead with counted
+// lgkmcnt waits (left to itself the compiler reads each fragment right before its MFMA behind an
+// lgkmcnt(0)). A wait names the fragments it guards ("+v"), so their MFMAs cannot move above it;
+// LDS returns in order, so younger LDS operations only make a counted wait stricter.
+typedef __attribute__((address_space(3))) const char* lds_cptr;
+
+template <int OFF>
+__device__ __forceinline__ u32x4 lds_rd(lds_cptr p) {
+  u32x4 r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(p), "i"(OFF));
+  return r;
+}
+
+template <int N>
+__device__ __forceinline__ void lds_wait2(u32x4& a, u32x4& b) {
+  asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "i"(N));
+}
+
+template <int N>
+__device__ __forceinline__ void lds_wait1(u32x4& a) {
+  asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(a) : "i"(N));
+}
+
+// compiler-visible lgkmcnt(0): the compiler's own LDS reads (biases) are known complete after it
+__device__ __forceinline__ void lgkm_drain() { __builtin_amdgcn_s_waitcnt(0xC07F); }
+
+constexpr int cmin(int a, int b) { return a < b ? a : b; }
+
+// acc[u / KQ] += W_hi h_hi + W_hi h_lo + W_lo h_hi over the NU = n_tiles KQ k-steps of a chunk: k-step u
+// has its hi / lo fragments at (2u, 2u + 1) KiB from `base` (per-lane address); PF k-steps prefetched
+template <int KQ, int NU, int PF, int U = 0>
+__device__ __forceinline__ void split_chain(lds_cptr base, const u32x4 (&Hh)[KQ], const u32x4 (&Hl)[KQ],
+                                            f32x4 (&acc)[(NU + KQ - 1) / KQ], u32x4 (&fa)[PF + 1][2]) {
+  if constexpr (U < NU) {
+    if constexpr (U + PF < NU) {
+      fa[(U + PF) % (PF + 1)][0] = lds_rd<(2 * (U + PF)) * 1024>(base);
+      fa[(U + PF) % (PF + 1)][1] = lds_rd<(2 * (U + PF) + 1) * 1024>(base);
+    }
+    lds_wait2<2 * cmin(NU - 1 - U, PF)>(fa[U % (PF + 1)][0], fa[U % (PF + 1)][1]);
+    constexpr int t = U / KQ, q = U % KQ;
+    acc[t] = mfma16(fa[U % (PF + 1)][0], Hl[q], acc[t]);
+    acc[t] = mfma16(fa[U % (PF + 1)][1], Hh[q], acc[t]);
+    acc[t] = mfma16(fa[U % (PF + 1)][0], Hh[q], acc[t]);
+    split_chain<KQ, NU, PF, U + 1>(base, Hh, Hl, acc, fa);
+  }
+}
+
+template <int KQ, int NU, int PF>
+__device__ __forceinline__ void split_product(lds_cptr base, const u32x4 (&Hh)[KQ], const u32x4 (&Hl)[KQ],
+                                              f32x4 (&acc)[(NU + KQ - 1) / KQ]) {
+  u32x4 fa[PF + 1][2];
+#pragma unroll
+  for (int u = 0; u < cmin(PF, NU); ++u) {
+    // (unrolled: u is a constant) the first PF k-steps' fragments
+    if (u == 0) fa[0][0] = lds_rd<0>(base), fa[0][1] = lds_rd<1024>(base);
+    if (u == 1) fa[1][0] = lds_rd<2048>(base), fa[1][1] = lds_rd<3072>(base);
+    if (u == 2) fa[2][0] = lds_rd<4096>(base), fa[2][1] = lds_rd<5120>(base);
+  }
+  static_assert(PF >= 1 && PF <= 3, "prefetch depth");
+  split_chain<KQ, NU, PF>(base, Hh, Hl, acc, fa);
+}
+
+// layer 1: one fragment per k-step (the split lives in the k-slots), NU = n_tiles K1Q k-steps in tile order
+template <int K1Q, int NU, int PF, int F = 0>
+__device__ __forceinline__ void l1_chain(lds_cptr base, const u32x4 (&b1)[K1Q], f32x4 (&acc)[NU / K1Q],
+                                         u32x4 (&fa)[PF + 1]) {
+  if constexpr (F < NU) {
+    if constexpr (F + PF < NU) fa[(F + PF) % (PF + 1)] = lds_rd<(F + PF) * 1024>(base);
+    lds_wait1<cmin(NU - 1 - F, PF)>(fa[F % (PF + 1)]);
+    acc[F / K1Q] = mfma16(fa[F % (PF + 1)], b1[F % K1Q], acc[F / K1Q]);
+    l1_chain<K1Q, NU, PF, F + 1>(base, b1, acc, fa);
+  }
 }
 
 // r-form activation r = 1 / (1 + 2^zs) (v_exp_f32 + v_rcp_f32, ~1 ulp each)
@@ -101,7 +178,10 @@ __device__ __forceinline__ float x3_act_r2(float zs) {
 
 // The network engine: NNET networks of nl layers (runtime, 1..3) of width W share one weight ring;
 // each evaluation streams (nl - 1) NCH hidden chunks then one output chunk, in the host image's order.
-template <int W, int NNET, int K1Q, int R, int RING_OFF>
+// DIAG (timing ablations only, never on the product path; DMIP_X3_DIAG): bit 0 = no ring (no DMA, no
+// barrier: stale weights), bit 1 = hidden activations replaced by the split alone, bit 2 = the same for
+// layer 1's double tanh
+template <int W, int NNET, int K1Q, int R, int RING_OFF, int DIAG = 0>
 struct XEngine {
   using S = Shape<W>;
   static constexpr int ST = S::ST, KQ = S::KQ, CT = S::CT, NCH = S::NCH, NW = S::NW, PPW = S::PPW;
@@ -144,6 +224,12 @@ struct XEngine {
   // the next chunk of the stream, landed (own pieces counted, the others' by the barrier); the slot
   // read one chunk ago is refilled R - 1 chunks ahead
   __device__ __forceinline__ const char* chunk_sync() {
+    if constexpr (DIAG & 1) {
+      asm volatile("" ::: "memory");
+      const char* slot = lds + RING_OFF + s_read * CHUNK;
+      s_read = s_read + 1 == R ? 0 : s_read + 1;
+      return slot;
+    }
     wait_vmcnt<(R - 2) * PPW>();
     lds_barrier();
     ring_issue();
@@ -169,26 +255,15 @@ struct XEngine {
     return *(const f32x4*)((const float*)(lds + bias_off[ni]) + li * W + 16 * tile + 4 * g);
   }
 
-  // acc += W_hi h_hi + W_hi h_lo + W_lo h_hi over one output tile (image at tp)
-  __device__ __forceinline__ f32x4 tile_product(const char* tp, const u32x4 (&Hh)[KQ], const u32x4 (&Hl)[KQ],
-                                                f32x4 acc) const {
-#pragma unroll
-    for (int q = 0; q < KQ; ++q) {
-      const u32x4 ah = *(const u32x4*)(tp + ((2 * q + 0) * 64 + lane) * 16);
-      const u32x4 al = *(const u32x4*)(tp + ((2 * q + 1) * 64 + lane) * 16);
-      acc = mfma16(ah, Hl[q], acc);
-      acc = mfma16(al, Hh[q], acc);
-      acc = mfma16(ah, Hh[q], acc);
-    }
-    return acc;
-  }
-
   // activate tile o (compile-time after unrolling) into the (hi, lo) B operands of the next layer
   template <bool L1>
   __device__ __forceinline__ void act_store(const f32x4& z, int o, u32x4 (&Oh)[KQ], u32x4 (&Ol)[KQ]) const {
     float r[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) r[k] = L1 ? x3_act_r2(z[k]) : x3_act_r(z[k]);
+    for (int k = 0; k < 4; ++k) {
+      if constexpr (L1 ? (DIAG & 4) != 0 : (DIAG & 2) != 0) r[k] = z[k];
+      else r[k] = L1 ? x3_act_r2(z[k]) : x3_act_r(z[k]);
+    }
     uint32_t h0, l0, h1, l1;
     split_pair(r[0], r[1], h0, l0);
     split_pair(r[2], r[3], h1, l1);
@@ -197,44 +272,55 @@ struct XEngine {
     Ol[q][d] = l0, Ol[q][d + 1] = l1;
   }
 
-  // layer 1 from the resident image and the B operand b1; the activation of tile o - 1 is issued in
-  // tile o's block so it overlaps the MFMAs
+  // layer 1 from the resident image and the B operand b1 (all ST tiles' pre-activations in one prefetched
+  // MFMA chain), then the double tanh of every tile
   __device__ __forceinline__ void layer1(int ni, const u32x4 (&b1)[K1Q], u32x4 (&Oh)[KQ], u32x4 (&Ol)[KQ]) {
     asm volatile("" ::: "memory");
-    const char* l1 = lds + l1_off[ni];
-    f32x4 pend;
+    f32x4 acc[ST];
 #pragma unroll
-    for (int o = 0; o < ST; ++o) {
-      f32x4 acc = bias4(ni, 0, o);
+    for (int o = 0; o < ST; ++o) acc[o] = bias4(ni, 0, o);
+    lgkm_drain();
+    const lds_cptr base = (lds_cptr)(lds + l1_off[ni] + lane * 16);
+    constexpr int NU = ST * K1Q;
+    u32x4 fa[4];
+    fa[0] = lds_rd<0>(base);
+    if constexpr (NU > 1) fa[1] = lds_rd<1024>(base);
+    if constexpr (NU > 2) fa[2] = lds_rd<2048>(base);
+    l1_chain<K1Q, NU, 3>(base, b1, acc, fa);
 #pragma unroll
-      for (int q = 0; q < K1Q; ++q) acc = mfma16(*(const u32x4*)(l1 + ((o * K1Q + q) * 64 + lane) * 16), b1[q], acc);
-      if (o > 0) act_store<true>(pend, o - 1, Oh, Ol);
-      pend = acc;
-    }
-    act_store<true>(pend, ST - 1, Oh, Ol);
+    for (int o = 0; o < ST; ++o) act_store<true>(acc[o], o, Oh, Ol);
   }
 
   __device__ __forceinline__ void hidden(int ni, int li, const u32x4 (&Hh)[KQ], const u32x4 (&Hl)[KQ],
                                          u32x4 (&Oh)[KQ], u32x4 (&Ol)[KQ]) {
-    f32x4 pend;
+    f32x4 pend[CT];
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
-      const char* ch = chunk_sync();
+      f32x4 acc[CT];
 #pragma unroll
-      for (int t = 0; t < CT; ++t) {
-        const int o = c * CT + t;
-        const f32x4 acc = tile_product(ch + t * TILE, Hh, Hl, bias4(ni, li, o));
-        if (o > 0) act_store<false>(pend, o - 1, Oh, Ol);
-        pend = acc;
+      for (int t = 0; t < CT; ++t) acc[t] = bias4(ni, li, c * CT + t);
+      lgkm_drain();
+      const char* ch = chunk_sync();
+      split_product<KQ, CT * KQ, 2>((lds_cptr)(ch + lane * 16), Hh, Hl, acc);
+      // the previous chunk's tiles are activated beside this chunk's MFMAs
+      if (c > 0) {
+#pragma unroll
+        for (int t = 0; t < CT; ++t) act_store<false>(pend[t], (c - 1) * CT + t, Oh, Ol);
       }
+#pragma unroll
+      for (int t = 0; t < CT; ++t) pend[t] = acc[t];
     }
-    act_store<false>(pend, ST - 1, Oh, Ol);
+#pragma unroll
+    for (int t = 0; t < CT; ++t) act_store<false>(pend[t], (NCH - 1) * CT + t, Oh, Ol);
   }
 
   // output rows 0..15 (tile 0 of the output chunk)
   __device__ __forceinline__ f32x4 output(int ni, const u32x4 (&Hh)[KQ], const u32x4 (&Hl)[KQ]) {
+    f32x4 acc[1] = {bias4(ni, nl, 0)};
+    lgkm_drain();
     const char* ch = chunk_sync();
-    return tile_product(ch, Hh, Hl, bias4(ni, nl, 0));
+    split_product<KQ, KQ, 2>((lds_cptr)(ch + lane * 16), Hh, Hl, acc);
+    return acc[0];
   }
 
   // one network: layer 1, the nl - 1 hidden layers (ping-pong), the output tile
@@ -286,18 +372,18 @@ __device__ __forceinline__ void l1_operand(const float (&v)[NV], int g, u32x4 (&
 //                   corrector steps before each predictor step)
 // then mu = g a + 0.5 beta x, x <- x + delta mu + sqrt(delta) g xi (dmip_device.h em_update). Work
 // distribution: the balanced WaveSchedule over 16-chain tiles (as dmip_f32.h).
-template <int MODE, int W, int D, int M>
+template <int MODE, int W, int D, int M, int DIAG = 0>
 struct SamplerCfg {
   static constexpr int NNET = MODE == SAMPLER_POSTERIOR ? 2 : 1;
   static constexpr int NV = MODE == SAMPLER_CDIFFE ? D + M + 1 : D + 1;  // layer-1 inputs (y folded for CDE)
   static constexpr int K1Q = k1q_of(NV);
   using L = XLay<W, NNET, K1Q, M>;
-  using E = XEngine<W, NNET, K1Q, L::R, L::RING>;
+  using E = XEngine<W, NNET, K1Q, L::R, L::RING, DIAG>;
 };
 
-template <int MODE, int W, int D, int M, bool NOISE>
+template <int MODE, int W, int D, int M, bool NOISE, int DIAG = 0>
 __global__ void __launch_bounds__(Shape<W>::NW * 64, Shape<W>::NW / 4) x3_sampler_kernel(X3SamplerParams p) {
-  using C = SamplerCfg<MODE, W, D, M>;
+  using C = SamplerCfg<MODE, W, D, M, DIAG>;
   using L = typename C::L;
   using E = typename C::E;
   constexpr int NW = Shape<W>::NW, ST = Shape<W>::ST, K1Q = C::K1Q;
@@ -466,10 +552,10 @@ __global__ void __launch_bounds__(Shape<W>::NW * 64, Shape<W>::NW / 4) x3_sample
 }  // namespace x3
 
 // ----------------------------------------------------------------- launch helpers (per TU)
-template <int MODE, int W, int D, int M, bool NOISE>
+template <int MODE, int W, int D, int M, bool NOISE, int DIAG = 0>
 inline hipError_t launch_x3_sampler_t(const X3SamplerParams& p, int n_y, hipStream_t st) {
   constexpr int NW = x3::Shape<W>::NW;
-  auto kern = x3::x3_sampler_kernel<MODE, W, D, M, NOISE>;
+  auto kern = x3::x3_sampler_kernel<MODE, W, D, M, NOISE, DIAG>;
   const long long tiles = (p.n_chains + 15) / 16;
   long long g = resident_slots(kern, NW * 64, st) / (n_y > 0 ? n_y : 1);
   const long long cap = (tiles + NW - 1) / NW;

@@ -1,10 +1,28 @@
 // fp32-accurate split-fp16 sampler instantiations: SAMPLER_CDE (dmip_x3.h).
 #include "dmip_x3.h"
 
+#include <cstdlib>
+
 namespace dmip {
+
+// Development knob (not part of the ABI): DMIP_X3_DIAG=d (1..7) runs the timing ablation DIAG = d of the
+// width-256, xdim-3 CDE kernel (dmip_x3.h XEngine); see profiles/README.md.
+static int x3_diag() {
+  const char* e = getenv("DMIP_X3_DIAG");
+  return e ? atoi(e) : 0;
+}
 
 hipError_t launch_x3_sampler_cde(const X3SamplerParams& p, int width, int xdim, int n_y, hipStream_t st, bool* ok) {
   *ok = true;
+  if (width == 256 && xdim == 3 && !p.noise) {
+    switch (x3_diag()) {
+#define DG(d) \
+  case d: return launch_x3_sampler_t<SAMPLER_CDE, 256, 3, 0, false, d>(p, n_y, st);
+      DG(1) DG(2) DG(3) DG(4) DG(6) DG(7)
+#undef DG
+      default: break;
+    }
+  }
 #define X(Wv, Dv) \
   if (width == Wv && xdim == Dv) return launch_x3_sampler_n<SAMPLER_CDE, Wv, Dv, 0>(p, n_y, st);
   X(64, 2) X(128, 2) X(256, 2) X(512, 2) X(64, 3) X(128, 3) X(256, 3) X(512, 3)

@@ -232,12 +232,13 @@ class CDE(BaseClassDiffusionModel):
         return out
 
     def train_epoch(self, optimizer, loss_fn, epoch_data_loader):
-        from .training import DeviceTrainStep, _plain_adam, device_step_enabled, fused_config, fused_loss_grad, \
-            loss_info
+        from .training import DeviceTrainStep, _plain_adam, device_step_enabled, device_step_ok, fused_config, \
+            fused_loss_grad, loss_info
         cfg = fused_config(self, loss_fn)
         # $DMIP_TRAIN_DEVICE_STEP=1: t, eps and Adam on the device too (training.DeviceTrainStep)
         dstep = DeviceTrainStep(self, loss_fn, optimizer) \
-            if cfg is not None and device_step_enabled() and _plain_adam(optimizer) is not None else None
+            if cfg is not None and device_step_enabled() and _plain_adam(optimizer) is not None \
+            and device_step_ok(self) else None
 
         def batch_loss(x, y):
             if dstep is not None:
@@ -268,7 +269,8 @@ def _loop_normals(seed, chain_offset, stream_id, n, d, dev):
 def _em_device_loop(model, ys, num_samples, num_steps, mean, std, seed, chain_offset, drift, zdim,
                     keep, y_resample=None):
     """Reverse-SDE EM loop on device tensors for shapes without a compiled fused sampler: the
-    network evaluations are dmip_mlp_forward launches (model precision), the update follows
+    network evaluations are dmip_mlp_forward launches in the networks' own forward precision
+    (nets.MLP.dmip_precision, exact f32 unless set otherwise), the update follows
     models/diffusion.py:40-42 (same rounding order as the fused kernel). Noise comes from the
     kernels' counter-keyed generator, keyed by (seed, global chain index, stream = (y index, step)),
     so a shard of a run draws exactly the chains of the full run (bit-identical union)."""

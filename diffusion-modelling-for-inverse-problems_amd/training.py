@@ -215,7 +215,8 @@ class _TrainPlan:
         d.t_dev, d.eps_dev, d.loss_dev = self.t.data_ptr(), self.eps.data_ptr(), self.out.data_ptr()
         self.hyper = (d.lr, d.beta1, d.beta2, d.eps)
         h = ctypes.c_void_p()
-        _lib.check(self.lib.dmip_train_plan_create(ctypes.byref(d), ctypes.byref(h)))
+        with torch.cuda.device(ds.dev):  # the plan's buffers and capture stream on the parameters' device
+            _lib.check(self.lib.dmip_train_plan_create(ctypes.byref(d), ctypes.byref(h)))
         self.h = h
         self.k, self.step = None, None  # the device counters' values (unknown until set)
 
@@ -226,6 +227,15 @@ class _TrainPlan:
                 self.lib.dmip_train_plan_destroy(h)
             except Exception:  # noqa: BLE001 -- interpreter shutdown: the runtime may already be gone
                 pass
+
+
+ADAM_MAX_TENSORS = 16  # dmip_adam_step / dmip_train_plan (csrc dmip_internal.h kAdamMaxTensors)
+
+
+def device_step_ok(model):
+    """The whole-step device path handles this network (at most ADAM_MAX_TENSORS parameter tensors, i.e. up
+    to 7 hidden layers); otherwise train_epoch keeps the fused loss + torch Adam path."""
+    return len(list(model.sde.a.parameters())) <= ADAM_MAX_TENSORS
 
 
 class DeviceTrainStep:
@@ -246,6 +256,9 @@ class DeviceTrainStep:
             raise ValueError("no fused loss path for this network / loss")
         net = model.sde.a
         self.params = list(net.parameters())
+        if len(self.params) > ADAM_MAX_TENSORS:
+            raise ValueError(f"DeviceTrainStep: dmip_adam_step takes at most {ADAM_MAX_TENSORS} parameter tensors "
+                             f"(this network has {len(self.params)})")
         if {id(p) for p in self.opt.param_groups[0]["params"]} != {id(p) for p in self.params}:
             raise ValueError("DeviceTrainStep: the optimizer must hold exactly the score network's parameters")
         p0 = self.params[0]
@@ -302,7 +315,12 @@ class DeviceTrainStep:
 
     def __call__(self, x, y):
         """One step on a batch (x, y) (device fp32): returns the [4] loss tensor (loss, PDE, IC, DSM)
-        without synchronising; the parameters and the optimizer state are updated in place."""
+        without synchronising; the parameters and the optimizer state are updated in place. Runs with the
+        parameters' device current (the launches and the captured plan belong to it)."""
+        with torch.cuda.device(self.dev):
+            return self._step(x, y)
+
+    def _step(self, x, y):
         import ctypes
         L, P, lib = self.L, self.ptr, self.lib
         B = int(x.shape[0])
