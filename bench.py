@@ -3,28 +3,33 @@
 Default workload (BASELINE.json configs[1]): scatterometry CDE, MLP 27 -> [256]*3 -> 3 (tanh, double
 tanh on layer 1), 1000 Euler-Maruyama steps, 100,000 chains per GPU for one y (y_test[0] of the
 reference's seeded test set, tests/golden/data_scat.npz), weights = the fixture-trained checkpoint
-(tests/golden/ckpt_scat.npz; random init if absent -- timing does not depend on the weights), bf16
-MFMA operands (north_star: "MFMA bf16 GEMMs"). One "step" = one full sampling call (x0 draw + 1000
-SDE steps + output in HBM). With --gpus N the chains are sharded by global chain index (weak
-scaling: 100k chains per GPU) and the shards are gathered to every rank with one RCCL all_gather
-inside the timed region.
+(tests/golden/ckpt_scat.npz; random init if absent -- timing does not depend on the weights).
+Headline arithmetic: the reference's fp32 (models/diffusion.py:38-42, nets.py:32-35), computed by the
+fp32x3 engine (every product as three fp16 MFMAs, W_hi h_hi + W_hi h_lo + W_lo h_hi, fp32 accumulation:
+csrc/dmip_x3.h). One "step" = one full sampling call (x0 draw + 1000 SDE steps + output in HBM). With
+--gpus N the chains are sharded by global chain index (weak scaling: 100k chains per GPU) and the shards
+are gathered to every rank with one RCCL all_gather inside the timed region.
 
 Launch: `python bench.py --gpus N` starts N rank processes itself (one per GPU, RCCL over xGMI) when
-it is not already running under torch.distributed.run; the parent never touches the GPU.
+it is not already running under torch.distributed.run; the parent never touches the GPU, polls its
+children and terminates the others as soon as one fails.
 
 Prints ONE JSON line on rank 0 (driver contract) with
-  * `roofline`: MFMA-bound; algorithmic flops per launch / HIP-event-timed average launch;
+  * `roofline`: MFMA-bound; algorithmic flops per launch / HIP-event-timed average launch, against the
+    matrix pipe the kernel runs on (fp16 for fp32x3 -- `executed_frac` counts its three products);
   * `cpu_baseline`: reference-order torch-CPU sampler on a bounded sample (rank 0, N = 1 only);
   * `ks_vs_ref` / `w1_vs_ref` / `parity`: the timed run's samples against the reference sampler's own
     draws (tests/golden/samples_scat.npz: 20k draws and the 1001 quantiles of its 100k-chain run, same
     y and weights): per-dimension KS (alpha = 0.01), per-dimension and sliced W1 with their null levels;
-  * `fp32_mode`: the same workload in the exact-f32 parity mode (DMIP_PREC_F32), timed after the
-    headline with its own parity report.
+  * `fast_mode`: the same workload on the 16-bit engine (fp16 hidden layers), `fp32_mode`: on the
+    exact-f32 engine (v_mfma_f32_16x16x4_f32) -- each timed after the headline with its own parity report;
+  * `dist`: the world size torch.distributed reports after init and every rank's device (PCI bus id).
 Other workloads (not the headline): --workload cdiffe-pc (BASELINE config 3: CDiffE + 1 Langevin
 corrector step, --chains-total 1000000 sharded over the ranks: strong scaling) and --workload dps
 (config 4: DPS with surrogate guidance, exact f32, --chains-total 262144).
 """
 import argparse
+import datetime
 import importlib
 import json
 import os
@@ -39,7 +44,7 @@ sys.path.insert(0, ROOT)
 PKG = "diffusion-modelling-for-inverse-problems_amd"
 
 XDIM, YDIM, WIDTH, NH = 3, 23, 256, 3
-PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, no sparsity)
+PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 / fp16 MFMA (MI355X_MICROARCH.md, no sparsity)
 PEAK_F32_TFLOPS = 157.3    # MI355X f32 MFMA (= the f32 vector rate)
 
 
@@ -48,6 +53,28 @@ def flops_per_sample_step(in_dim=XDIM + YDIM + 1, w=WIDTH, nh=NH, out=XDIM):
 
 
 F_PRIOR = flops_per_sample_step(XDIM + 1, WIDTH, NH, XDIM)
+
+# the headline workload's sampler kernel per precision (+ its per-y prep kernel, inside the HIP events)
+KERNELS = {"fp32x3": "x3_sampler_kernel<0,256,3,0,false> (+x3_bias_prep)",
+           "bf16": "em_sampler_kernel<0,256,3,3,0,8,4,false> (+a1_prep)",
+           "fp32": "f32_sampler_kernel<0,256,3,0,false> (+f32_l1_prep)"}
+KERNEL_MATCH = {"fp32x3": "x3_sampler", "bf16": "em_sampler", "fp32": "f32_sampler"}
+ARITH = {
+    "fp32x3": "fp32-accurate: every product as three fp16 MFMAs W_hi h_hi + W_hi h_lo + W_lo h_hi "
+              "(v_mfma_f32_16x16x32_f16, fp32 accumulation; 2^-23.2 of sum|w h| per product vs 2^-23.0 for an fp32 "
+              "fmaf chain, profiles/r3_mfma_f16_check.txt), tanh by exp2 + rcp (~1 ulp); fp32 chain state / SDE update",
+    "bf16": "16-bit MFMA operands (layer 1: bf16 over split hi+lo inputs, ~fp32; hidden and output layers: fp16 "
+            "weights and activations), fp32 accumulate; fp32 chain state / SDE update",
+    "fp32": "exact f32 MFMA (v_mfma_f32_16x16x4_f32, an fmaf chain), libm tanh; fp32 chain state / SDE update"}
+DTYPE = {"fp32x3": "fp32", "bf16": "fp16", "fp32": "fp32"}
+
+
+def executed_flops_per_sample_step(precision, in_dim=XDIM + YDIM + 1, w=WIDTH, nh=NH, out=XDIM):
+    """MFMA work the kernel issues per chain-step: fp32x3 runs every hidden/output product three times
+    (layer 1 carries its split in the k-slots: 3 slots per input); the other engines one."""
+    if precision != "fp32x3":
+        return flops_per_sample_step(in_dim, w, nh, out)
+    return 2 * (3 * (XDIM + 1) * w + 3 * ((nh - 1) * w * w + w * out))
 F_SUR = 2 * (3 * 256 + 2 * 256 * 256 + 256 * 23)
 
 
@@ -57,7 +84,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="cde", choices=["cde", "cdiffe-pc", "dps"])
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32x3", "fp32"])
+    ap.add_argument("--precision", default="fp32x3", choices=["fp32x3", "bf16", "fp32"],
+                    help="headline arithmetic (default: fp32x3, the reference's fp32 at the fp16 matrix rate)")
     ap.add_argument("--chains", type=int, default=100000, help="chains per GPU (weak scaling)")
     ap.add_argument("--chains-total", type=int, default=0, help="total chains over all GPUs (strong scaling)")
     ap.add_argument("--num-steps", type=int, default=1000, help="SDE steps per sample")
@@ -65,17 +93,24 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fp32", action="store_true", help="skip the exact-f32 run beside the headline")
     ap.add_argument("--fp32-steps", type=int, default=2)
+    ap.add_argument("--no-fast", action="store_true", help="skip the 16-bit engine run beside the headline")
+    ap.add_argument("--fast-steps", type=int, default=3)
+    ap.add_argument("--dist-timeout", type=float, default=900.0,
+                    help="seconds before a blocked collective (a dead rank) fails the job")
     ap.add_argument("--no-other-configs", action="store_true",
                     help="skip the one-GPU runs of BASELINE configs 3-5 and the reference width reported beside the headline")
     ap.add_argument("--master-port", type=int, default=29511)
     ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)  # CPU/gloo launcher test only
+    ap.add_argument("--stub-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)  # launcher fail-fast test
     return ap.parse_args()
 
 
 # ------------------------------------------------------------------------------ launcher
-def launch_ranks(args):
+def launch_ranks(args, poll_s=0.2):
     """Start args.gpus rank processes (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* in their environment) and
-    wait for all of them; the parent initialises no GPU state. Exit status: the worst child's."""
+    wait for them, polling: the first rank to exit non-zero gets its siblings terminated (they would
+    otherwise block in a collective until the timeout). The parent initialises no GPU state. Exit
+    status: the first failure's, else 0."""
     env0 = dict(os.environ)
     env0.setdefault("MASTER_ADDR", "127.0.0.1")
     env0.setdefault("MASTER_PORT", str(args.master_port))
@@ -85,9 +120,61 @@ def launch_ranks(args):
         env = dict(env0, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus), LOCAL_WORLD_SIZE=str(args.gpus))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
     rc = 0
-    for p in procs:
-        rc = max(rc, p.wait())
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                sys.stderr.write(f"bench.py: rank {procs.index(p)} exited with {code}; terminating the other ranks\n")
+                for q in live:
+                    q.terminate()
+                deadline = time.time() + 10
+                for q in live:
+                    try:
+                        q.wait(timeout=max(0.1, deadline - time.time()))
+                    except subprocess.TimeoutExpired:
+                        q.kill()
+                        q.wait()
+                live = []
+                break
+        if live:
+            time.sleep(poll_s)
     return rc
+
+
+def init_dist(backend, dev, timeout_s):
+    """init_process_group with a timeout (a dead rank fails the others instead of hanging them); the world
+    size torch.distributed reports must equal WORLD_SIZE."""
+    import torch.distributed as dist
+    kw = {"timeout": datetime.timedelta(seconds=timeout_s)}
+    if dev is not None:
+        kw["device_id"] = dev
+    dist.init_process_group(backend, **kw)
+    world = dist.get_world_size()
+    if world != int(os.environ["WORLD_SIZE"]):
+        raise RuntimeError(f"torch.distributed world size {world} != WORLD_SIZE {os.environ['WORLD_SIZE']}")
+    return world
+
+
+def rank_devices(dist, world, dev):
+    """Every rank's device as 'rank:pci_domain:bus:device name' (gathered), so the line records which
+    GPUs ran the job."""
+    import torch
+    if dev is None:
+        mine = f"{dist.get_rank() if world > 1 else 0}:cpu"
+    else:
+        pr = torch.cuda.get_device_properties(dev)
+        mine = (f"{dist.get_rank() if world > 1 else 0}:{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:"
+                f"{pr.pci_device_id:02x} {pr.name} {pr.gcnArchName}")
+    if world == 1:
+        return [mine]
+    out = [None] * world
+    dist.all_gather_object(out, mine)
+    return out
 
 
 # ------------------------------------------------------------------------------ workloads
@@ -112,7 +199,7 @@ def synthetic_y():
     return np.abs(np.random.default_rng(13).normal(0.3, 0.4, YDIM)).astype(np.float32)
 
 
-def pmc_traffic(kernel_match="em_sampler"):
+def pmc_traffic(kernel_match="x3_sampler"):
     """HBM bytes per launch of the sampler kernel from the committed rocprofv3 PMC summary
     (profiles/pmc_summary_latest.json, written by scripts/pmc_summary.py from separate --pmc
     passes on the same workload), or None."""
@@ -208,9 +295,7 @@ class Workload:
             self.model, self.weights = load_model(pkg, dev)
             self.flops_sample_step = flops_per_sample_step()
             self.peak = PEAK_F32_TFLOPS if args.precision == "fp32" else PEAK_BF16_TFLOPS
-            self.kernel = {"bf16": "em_sampler_kernel<0,256,3,3,0,8,4,false> (+a1_prep, inside the events)",
-                           "fp32x3": "x3_sampler_kernel<0,256,3,0,false> (+x3_bias_prep)",
-                           "fp32": "f32_sampler_kernel<0,256,3,0,false> (+l1_prep)"}[args.precision]
+            self.kernel = KERNELS[args.precision]
             self.workload = "scatterometry CDE posterior sampling (BASELINE configs[1])"
             self.kw = {"precision": args.precision}
         elif args.workload == "cdiffe-pc":
@@ -219,8 +304,9 @@ class Workload:
             self.model.sde.a.to(dev)
             self.kw = {"corrector_steps": 1, "snr": 0.16, "precision": args.precision}
             self.flops_sample_step = 2 * flops_per_sample_step(XDIM + YDIM + 1, WIDTH, NH, XDIM + YDIM)
-            self.peak = PEAK_BF16_TFLOPS if args.precision == "bf16" else PEAK_F32_TFLOPS
-            self.kernel = "em_sampler_kernel<2,256,3,3,23,8,4,false> (CDiffE + Langevin corrector)"
+            self.peak = PEAK_F32_TFLOPS if args.precision == "fp32" else PEAK_BF16_TFLOPS
+            self.kernel = {"fp32x3": "x3_sampler_kernel<2,256,3,23,false>", "bf16": "em_sampler_kernel<2,256,3,3,23,8,4,false>",
+                           "fp32": "f32_sampler_kernel<2,256,3,23,false>"}[args.precision] + " (CDiffE + Langevin corrector)"
             self.workload = "scatterometry CDiffE predictor-corrector (BASELINE configs[2])"
         else:  # dps
             fm, prm = pkg.load_forward_model(gold)
@@ -289,51 +375,58 @@ def other_configs(args, pkg, lib, dev):
     import torch
     out = {}
 
-    def sampler(name, workload, chains, reps, **kw):
+    fam = {"fp32x3": "x3_sampler_kernel", "bf16": "em_sampler_kernel", "fp32": "f32_sampler_kernel"}
+
+    def sampler(name, workload, chains, reps, precision, **kw):
         try:
             a = copy.copy(args)
-            a.workload, a.chains, a.chains_total = workload, chains, 0
+            a.workload, a.chains, a.chains_total, a.precision = workload, chains, 0, precision
             for k, v in kw.items():
                 setattr(a, k, v)
             wl = Workload(a, pkg, dev, 0, 1)
+            mode = {"cde": 0, "cdiffe-pc": 2}.get(workload)
             if workload == "cde" and kw.get("width"):
                 torch.manual_seed(0)
                 W = kw["width"]
                 if kw.get("posterior"):  # two networks: likelihood (x, y, t) + prior (x, t)
                     wl.model = pkg.PosteriorDiffusionEstimator(XDIM, YDIM, [W] * NH)
                     wl.flops_sample_step = flops_per_sample_step(w=W) + flops_per_sample_step(XDIM + 1, W, NH, XDIM)
-                    wl.kernel = f"em_sampler_kernel<1,{W},3,3,...> (output layers through the ring)"
-                    wl.workload = "PosteriorDiffusionEstimator at the reference width"
+                    wl.workload, mode = "PosteriorDiffusionEstimator at the reference width", 1
                 else:
                     wl.model = pkg.CDE(XDIM, YDIM, [W] * NH)
                     wl.flops_sample_step = flops_per_sample_step(w=W)
-                    wl.kernel, wl.workload = f"em_sampler_kernel<0,{W},3,3,...>", "CDE at the reference width"
+                    wl.workload = "CDE at the reference width"
                 wl.model.sde.a.to(dev)
                 wl.weights = "random-init"
+            W = kw.get("width", WIDTH)
             if workload == "cdiffe-pc" and kw.get("width"):
                 torch.manual_seed(0)
-                W = kw["width"]
                 wl.model = pkg.CDiffE(XDIM, YDIM, [W] * NH)
                 wl.model.sde.a.to(dev)
                 wl.flops_sample_step = 2 * flops_per_sample_step(XDIM + YDIM + 1, W, NH, XDIM + YDIM)
-                wl.kernel = f"em_sampler_kernel<2,{W},3,3,23,...> (layer 1 through the ring)"
                 wl.workload = "CDiffE predictor-corrector at the reference width"
+            if workload != "dps":
+                wl.kernel = f"{fam[precision]}<{mode},{W},...>"
+            wl.peak = PEAK_F32_TFLOPS if precision == "fp32" or workload == "dps" else PEAK_BF16_TFLOPS
             wl.step(3000)
             el, lm, x = timed(wl, reps, None, 1, dev, seed0=3100)
             lib.device_status(dev)
             ach = wl.flops_sample_step * a.num_steps * wl.n_local / (lm * 1e-3) / 1e12
             out[name] = {"workload": wl.workload, "chains": wl.n_local, "sde_steps": a.num_steps,
-                         "value": wl.n_local * reps / el, "unit": "samples/s", "launch_ms": lm,
+                         "precision": precision if workload != "dps" else "fp32", "value": wl.n_local * reps / el,
+                         "unit": "samples/s", "launch_ms": lm,
                          "roofline": {"achieved": ach, "peak": wl.peak, "unit": "TFLOP/s", "frac": ach / wl.peak},
                          "kernel": wl.kernel, "weights": wl.weights, "finite": bool(torch.isfinite(x).all())}
         except Exception as e:  # noqa: BLE001 -- reported in the line, never fatal to the headline
             out[name] = {"error": f"{type(e).__name__}: {e}"}
 
-    sampler("config3_cdiffe_pc_per_gpu", "cdiffe-pc", 125000, 2)
-    sampler("config4_dps", "dps", 262144, 1)
-    sampler("cde_reference_width_512", "cde", 100000, 2, width=512)
-    sampler("posterior_reference_width_512", "cde", 100000, 2, width=512, posterior=True)
-    sampler("cdiffe_pc_reference_width_512", "cdiffe-pc", 100000, 1, width=512)
+    sampler("config3_cdiffe_pc_per_gpu", "cdiffe-pc", 125000, 2, "fp32x3")
+    sampler("config3_cdiffe_pc_per_gpu_fast", "cdiffe-pc", 125000, 2, "bf16")
+    sampler("config4_dps", "dps", 262144, 1, "fp32")
+    sampler("cde_reference_width_512", "cde", 100000, 2, "fp32x3", width=512)
+    sampler("posterior_reference_width_512", "cde", 100000, 1, "fp32x3", width=512, posterior=True)
+    # CDiffE scatterometry at width 512 has no fp32x3 kernel (its 27-input layer 1 does not fit beside the ring)
+    sampler("cdiffe_pc_reference_width_512_fast", "cdiffe-pc", 100000, 1, "bf16", width=512)
     try:
         tr = importlib.import_module(PKG + ".training")
         torch.manual_seed(0)
@@ -369,6 +462,24 @@ def other_configs(args, pkg, lib, dev):
     return out
 
 
+def side_mode(wl, args, dist, world, dev, lib, metrics, precision, steps, S, flops_launch):
+    """The headline workload on another engine, timed beside the headline (not the headline)."""
+    wl.step(2000, precision=precision)
+    el, lm, x = timed(wl, steps, dist, world, dev, seed0=100, precision=precision)
+    lib.device_status(dev)
+    if dist is not None and world > 1 and dist.get_rank() != 0:
+        return None
+    peak = PEAK_F32_TFLOPS if precision == "fp32" else PEAK_BF16_TFLOPS
+    a = flops_launch / (lm * 1e-3) / 1e12
+    rep = parity_vs_reference(metrics, x.reshape(-1, XDIM).cpu().numpy(), S, wl.weights)
+    return {"precision": precision, "dtype": DTYPE[precision], "arith": ARITH[precision],
+            "value": wl.n_total * steps / el, "unit": "samples/s", "steps": steps,
+            "ms_per_step": el / steps * 1e3, "launch_ms": lm, "kernel": KERNELS[precision],
+            "roofline": {"bound": "mfma", "achieved": a, "peak": peak, "unit": "TFLOP/s", "frac": a / peak,
+                         "traffic": pmc_traffic(KERNEL_MATCH[precision])},
+            "ks_vs_ref": ks_field(rep), "w1_vs_ref": w1_field(rep), "parity": {"pass": rep["pass"]} if rep else None}
+
+
 def main_worker(args):
     import torch
     import torch.distributed as dist
@@ -381,7 +492,8 @@ def main_worker(args):
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        world = init_dist("nccl", dev, args.dist_timeout)
+    devices = rank_devices(dist, world, dev)
     pkg = importlib.import_module(PKG)
     lib = importlib.import_module(PKG + "._lib")
     metrics = importlib.import_module(PKG + ".metrics")
@@ -398,7 +510,16 @@ def main_worker(args):
     value = wl.n_total * args.steps / elapsed
     flops_launch = wl.flops_sample_step * S * wl.n_local
     achieved = flops_launch / (launch_ms * 1e-3) / 1e12
-    dtype = "fp16" if (args.workload != "dps" and args.precision == "bf16") else "f32"
+    prec = args.precision if args.workload != "dps" else "fp32"
+    dtype = DTYPE[prec]
+    roof = {"bound": "mfma", "achieved": achieved, "peak": wl.peak, "unit": "TFLOP/s", "frac": achieved / wl.peak,
+            "traffic": pmc_traffic(KERNEL_MATCH[prec]) if args.workload == "cde" else None,
+            "kernel": wl.kernel, "launch_ms": launch_ms, "flops_per_launch": flops_launch}
+    if args.workload == "cde" and prec == "fp32x3":
+        ex = executed_flops_per_sample_step("fp32x3") * S * wl.n_local / (launch_ms * 1e-3) / 1e12
+        roof.update({"pipe": "v_mfma_f32_16x16x32_f16 (2500 TFLOP/s dense); three products per fp32 product",
+                     "executed_tflops": ex, "executed_frac": ex / wl.peak,
+                     "vs_f32_mfma_peak": achieved / PEAK_F32_TFLOPS})
     line = {
         "metric": "posterior samples/sec (1000-step reverse SDE)",
         "value": value,
@@ -415,14 +536,10 @@ def main_worker(args):
         "config": {"workload": wl.workload, "xdim": XDIM, "ydim": YDIM, "hidden_layers": [WIDTH] * NH,
                    "sde_steps": S, "chains_per_gpu": wl.n_local, "chains_total": wl.n_total,
                    "parallelism": f"sample-parallel x{world}" + (" + RCCL all_gather" if world > 1 else ""),
-                   "arith": ("16-bit MFMA operands (layer 1: bf16 over split hi+lo inputs, ~fp32; hidden and output "
-                             "layers: fp16 weights and activations), fp32 accumulate; fp32 chain state / SDE update"
-                             if dtype == "fp16"
-                             else "exact f32 MFMA (v_mfma_f32_16x16x4_f32); fp32 chain state / SDE update")},
-        "roofline": {"bound": "mfma", "achieved": achieved, "peak": wl.peak, "unit": "TFLOP/s",
-                     "frac": achieved / wl.peak,
-                     "traffic": pmc_traffic() if (args.workload == "cde" and dtype == "fp16") else None,
-                     "kernel": wl.kernel, "launch_ms": launch_ms, "flops_per_launch": flops_launch},
+                   "precision": prec, "arith": ARITH[prec]},
+        "roofline": roof,
+        "dist": {"world_size_observed": world, "backend": "nccl (RCCL)" if world > 1 else None,
+                 "devices": devices},
     }
     rep = None
     if args.workload == "cde" and rank == 0:
@@ -430,21 +547,10 @@ def main_worker(args):
         line["ks_vs_ref"] = ks_field(rep)
         line["w1_vs_ref"] = w1_field(rep)
         line["parity"] = {"pass": rep["pass"]} if rep else None
-    if args.workload == "cde" and args.precision == "bf16" and not args.no_fp32:
-        # the exact-f32 parity mode on the same workload, timed beside the headline (not the headline)
-        wl.step(2000, precision="fp32")
-        el32, lm32, x32 = timed(wl, args.fp32_steps, dist, world, dev, seed0=100, precision="fp32")
-        lib.device_status(dev)
-        if rank == 0:
-            a32 = flops_launch / (lm32 * 1e-3) / 1e12
-            rep32 = parity_vs_reference(metrics, x32.reshape(-1, XDIM).cpu().numpy(), S, wl.weights)
-            line["fp32_mode"] = {
-                "value": wl.n_total * args.fp32_steps / el32, "unit": "samples/s", "steps": args.fp32_steps,
-                "ms_per_step": el32 / args.fp32_steps * 1e3, "launch_ms": lm32, "kernel": "f32_sampler_kernel",
-                "roofline": {"bound": "mfma", "achieved": a32, "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s",
-                             "frac": a32 / PEAK_F32_TFLOPS},
-                "ks_vs_ref": ks_field(rep32), "w1_vs_ref": w1_field(rep32),
-                "parity": {"pass": rep32["pass"]} if rep32 else None}
+    if args.workload == "cde" and prec != "bf16" and not args.no_fast:
+        line["fast_mode"] = side_mode(wl, args, dist, world, dev, lib, metrics, "bf16", args.fast_steps, S, flops_launch)
+    if args.workload == "cde" and prec != "fp32" and not args.no_fp32:
+        line["fp32_mode"] = side_mode(wl, args, dist, world, dev, lib, metrics, "fp32", args.fp32_steps, S, flops_launch)
     if rank == 0 and world == 1 and args.workload == "cde" and not args.no_other_configs:
         line["other_configs"] = other_configs(args, pkg, lib, dev)
     if rank == 0 and world == 1 and args.workload == "cde" and not args.no_cpu_baseline:
@@ -458,12 +564,17 @@ def main_worker(args):
 
 def stub_worker(args, rank, world):
     """CPU / gloo stand-in for the sampler (launcher test only): every rank contributes its chain
-    range [lo, hi) as x[c] = (c, c, c); rank 0 checks the gathered tensor and prints the line."""
+    range [lo, hi) as x[c] = (c, c, c); rank 0 checks the gathered tensor and prints the line.
+    --stub-fail-rank R: rank R exits 1 after init while the others block in the gather (fail-fast test)."""
     import torch
     import torch.distributed as dist
     par = importlib.import_module(PKG + ".parallel")
     if world > 1:
-        dist.init_process_group("gloo")
+        world = init_dist("gloo", None, args.dist_timeout)
+    devices = rank_devices(dist, world, None)
+    if rank == args.stub_fail_rank:
+        sys.stderr.write(f"stub rank {rank}: failing on purpose\n")
+        return 1
     n_total = args.chains_total if args.chains_total > 0 else args.chains * world
     lo, hi = par.shard_range(n_total, rank, world)
     local = torch.arange(lo, hi, dtype=torch.float32)[None, :, None].expand(1, hi - lo, XDIM).contiguous()
@@ -473,7 +584,8 @@ def stub_worker(args, rank, world):
         dist.barrier()
     if rank == 0:
         print(json.dumps({"metric": "stub", "n_gpus": world, "chains_total": n_total,
-                          "gathered_shape": list(x.shape), "gather_ok": ok}), flush=True)
+                          "gathered_shape": list(x.shape), "gather_ok": ok,
+                          "dist": {"world_size_observed": world, "devices": devices}}), flush=True)
     if world > 1:
         dist.destroy_process_group()
     return 0 if ok else 1

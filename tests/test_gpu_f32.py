@@ -253,25 +253,23 @@ def test_unfused_shape_loop_is_shard_invariant(dmip):
 
 # ---------------------------------------------- distributional parity vs the reference (§8c)
 @pytest.mark.parametrize("tag", ["lin", "scat"])
-def test_posterior_parity_both_precisions(dmip, golden, tag):
-    """100k samples per precision against the reference sampler's draws on the same weights and y."""
+def test_posterior_parity_all_precisions(dmip, golden, tag):
+    """100k samples per precision against the reference sampler's draws on the same weights and y. Every
+    precision -- exact f32, the default fp32x3 and the 16-bit engine -- is held to the fp32 gate: KS
+    against the 20k draws and the 100k-run quantiles, per-dimension and sliced W1 <= 3x the null level."""
     M = _metrics()
     smp = golden(f"samples_{tag}.npz")
     m = _cde(dmip, tag, golden(f"ckpt_{tag}.npz"))
     S = int(smp["num_steps"])
     y = torch.from_numpy(smp["y"]).to(DEV)
-    reps = {}
-    for prec in ("fp32", "bf16"):
+    for prec in ("fp32", "fp32x3", "bf16"):
         torch.manual_seed(0)
         x = m(y, num_samples=100000, num_steps=S, precision=prec)
         assert x.shape == (100000, smp["samples"].shape[1]) and np.all(np.isfinite(x))
-        reps[prec] = M.parity_report(x, smp["samples"], smp["quantiles"], int(smp["n_total"]))
-    r = reps["fp32"]
-    assert r["pass"], r
-    b = reps["bf16"]
-    assert max(b["ks_draws"]["stat"]) < b["ks_draws"]["crit"], b
-    assert all(s <= 5 * n for s, n in zip(b["w1_draws"]["stat"], b["w1_draws"]["null"])), b
-    assert b["sliced_w1_draws"]["stat"] <= 5 * b["sliced_w1_draws"]["null"], b
+        r = M.parity_report(x, smp["samples"], smp["quantiles"], int(smp["n_total"]))
+        print(f"\n[parity] {tag} {prec}: KS {r['ks_draws']['stat']} (crit {r['ks_draws']['crit']:.4f}), "
+              f"sliced W1 {r['sliced_w1_draws']['stat']:.4f} (null {r['sliced_w1_draws']['null']:.4f})")
+        assert r["pass"], (prec, r)
 
 
 @pytest.mark.parametrize("cls,W,n", [("CDE", 256, 70001), ("CDE", 512, 40001), ("PosteriorDiffusionEstimator", 256, 70001),

@@ -1,8 +1,11 @@
 """Parity of the HIP path (through libdmip's C-ABI) against the oracle and the reference's own
 outputs (golden fixtures). Every test here needs an MI355X: run with `pytest -m gpu`.
 
-Tolerances (stated per test): integer/index work bit-exact; the schedule bit-exact; the network
-in bf16-MFMA mode within bf16 error bounds; posteriors by two-sample KS at alpha = 0.01.
+This module exercises the 16-bit engine (precision "bf16": fp16 hidden / output layers, split-bf16
+layer 1): an autouse fixture sets $DMIP_PRECISION=bf16 for every model it builds. The package default
+("fp32x3") is held to the fp32 gates in test_gpu_x3.py. Tolerances (stated per test): integer/index
+work bit-exact; the schedule bit-exact; the 16-bit engine's samples within about twice the error it is
+measured to have (the measured value beside each bound); posteriors by two-sample KS at alpha = 0.01.
 """
 import ctypes
 
@@ -22,6 +25,16 @@ DEV = "cuda:0"
 def _need_gpu():
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
+
+
+@pytest.fixture(autouse=True)
+def _sixteen_bit(monkeypatch):
+    monkeypatch.setenv("DMIP_PRECISION", "bf16")
+
+
+def _report(tag, value):
+    print(f"\n[bf16] {tag}: {value:.3e}")
+    return value
 
 
 def _sync():
@@ -145,7 +158,8 @@ def test_em_trajectory_injected_noise(dmip, golden, tag):
     # kernel: bf16 network, fp32 state; errors stay at the bf16 level through the contracting flow
     err = np.abs(out - ref)
     assert np.all(np.isfinite(out))
-    assert err.max() < 0.05 * max(1.0, np.abs(ref).max()), err.max()
+    e = _report(f"G3 {tag} {S} steps, err / max|x|", err.max() / max(1.0, np.abs(ref).max()))
+    assert e < 0.05, e
 
 
 @pytest.mark.parametrize("tag", ["lin", "scat"])
@@ -157,7 +171,8 @@ def test_em_short_trajectory_injected_noise(dmip, golden, tag):
     n = tr["x0_short"].shape[0]
     out = m.sample_device(torch.from_numpy(tr["y"]).to(DEV), n, S, noise=torch.from_numpy(noise).to(DEV))
     ref = tr["x_final_short"]
-    assert np.abs(out[0].cpu().numpy() - ref).max() < 0.02 * max(1.0, np.abs(ref).max())
+    e = _report(f"G3 {tag} {S} steps, err / max|x|", np.abs(out[0].cpu().numpy() - ref).max() / max(1.0, np.abs(ref).max()))
+    assert e < 0.02, e
 
 
 # --------------------------------------------------------------- posterior distribution (A2)
@@ -278,7 +293,8 @@ def test_sampler_all_widths_vs_oracle_product_rng(dmip, W):
     ref = O.cde_sample(params, y, n, S, seed)
     err = np.abs(x - ref)
     assert np.all(np.isfinite(x))
-    assert err.max() < 0.02 * max(1.0, np.abs(ref).max()), err.max()
+    e = _report("product-RNG sampler vs oracle, err / max|x|", err.max() / max(1.0, np.abs(ref).max()))
+    assert e < 0.02, e
 
 
 # ------------------------------------------------ fused Posterior / CDiffE samplers vs the oracle
@@ -304,7 +320,8 @@ def test_posterior_sampler_vs_oracle_product_rng(dmip, W, NL, xd, yd):
     ref = O.posterior_sample(prior, lik, y, n, S, seed)
     err = np.abs(x - ref)
     assert np.all(np.isfinite(x))
-    assert err.max() < 0.02 * max(1.0, np.abs(ref).max()), err.max()
+    e = _report("product-RNG sampler vs oracle, err / max|x|", err.max() / max(1.0, np.abs(ref).max()))
+    assert e < 0.02, e
 
 
 @pytest.mark.parametrize("W,NL", [(64, 3), (128, 3), (256, 3), (256, 2), (512, 3), (512, 2)])
@@ -324,7 +341,8 @@ def test_cdiffe_sampler_vs_oracle_product_rng(dmip, W, NL, xd, yd):
     ref = O.cdiffe_sample(params, y, n, S, seed)
     err = np.abs(x - ref)
     assert np.all(np.isfinite(x))
-    assert err.max() < 0.02 * max(1.0, np.abs(ref).max()), err.max()
+    e = _report("product-RNG sampler vs oracle, err / max|x|", err.max() / max(1.0, np.abs(ref).max()))
+    assert e < 0.02, e
 
 
 @pytest.mark.parametrize("cls", ["PosteriorDiffusionEstimator", "CDiffE"])
@@ -434,6 +452,42 @@ def test_fused_loss_grad_vs_oracle_ragged(dmip, name, NL):
     assert max(errs) < 3e-2, errs
 
 
+def _config5_batch(n=65536, seed=2024):
+    g = np.random.default_rng(seed)
+    x = g.normal(size=(n, 2)).astype(np.float32)
+    y = (x @ np.array([[1, 0.5], [0, 1]], np.float32).T + np.array([0.3, 0.5], np.float32)
+         + 0.3 * g.normal(size=(n, 2))).astype(np.float32)
+    t = (1e-4 + g.uniform(size=(n, 1)) * (1 - 1e-4)).astype(np.float32)
+    eps = g.normal(size=(n, 2)).astype(np.float32)
+    return x, y, t, eps
+
+
+@pytest.mark.parametrize("weights", ["trained", "init"])
+def test_config5_loss_grad_at_batch_65536_vs_oracle(dmip, golden, weights):
+    """BASELINE config 5 at its own batch: the PINNLoss step bench.py times (linear CDE [64]*3, batch
+    65,536, lam 1e-3 / lam2 0.1, FPE, L1 PDE / L2 IC metric; losses.py:214-242) -- the bf16 kernel's loss,
+    its components and all 8 gradient tensors against oracle.loss_grad (float64 jets + backward) on the
+    same (x, y, t, eps). Bounds: about twice the measured error (printed)."""
+    m = dmip.CDE(2, 2, [64] * 3)
+    if weights == "trained":
+        m.sde.a.load_state_dict(state_from_npz(golden("ckpt_lin.npz")))
+    else:
+        torch.manual_seed(5)
+        m = dmip.CDE(2, 2, [64] * 3)
+    params = _linear_params(m.sde.a)
+    x, y, t, eps = _config5_batch()
+    loss, info, grads = _fused(dmip, m, _loss_obj(dmip, "pinn"), *[torch.from_numpy(a).to(DEV) for a in (x, y, t, eps)])
+    ref_loss, comps, ref = O.loss_grad(params, x, y, t, eps, **_LOSS_CFGS["pinn"], ic_A=[[1, 0.5], [0, 1]],
+                                       ic_b=[0.3, 0.5], ic_Sinv=np.eye(2) / 0.3)
+    errs = [_rel(gk, rk) for gk, rk in zip(grads, [a for wb in ref for a in wb])]
+    lrel = abs(loss - ref_loss) / abs(ref_loss)
+    _report(f"config5 B=65536 {weights}: loss rel", lrel)
+    _report(f"config5 B=65536 {weights}: max grad rel L2", max(errs))
+    print(f"[bf16] config5 {weights} per-tensor grad rel L2: {[f'{e:.2e}' for e in errs]}")
+    assert lrel < 1e-2, lrel
+    assert max(errs) < 3e-2, errs
+
+
 def test_fused_loss_grad_deterministic(dmip, golden):
     """Per-wave partials + a fixed-order reduction: identical gradients on every call."""
     z = golden("pinn_linear.npz")
@@ -498,7 +552,8 @@ def test_cdiffe_predictor_corrector_vs_oracle(dmip, W, xd, yd):
     ref = O.cdiffe_sample(params, y, n, S, seed, corrector_steps=2, snr=0.16)
     err = np.abs(x - ref)
     assert np.all(np.isfinite(x))
-    assert err.max() < 0.02 * max(1.0, np.abs(ref).max()), err.max()
+    e = _report("product-RNG sampler vs oracle, err / max|x|", err.max() / max(1.0, np.abs(ref).max()))
+    assert e < 0.02, e
     # the corrector changes the result (it is not silently skipped)
     plain = O.cdiffe_sample(params, y, n, S, seed)
     assert np.abs(plain - ref).max() > 10 * err.max()
