@@ -301,6 +301,12 @@ class Workload:
         elif args.workload == "cdiffe-pc":
             torch.manual_seed(0)
             self.model = pkg.CDiffE(XDIM, YDIM, [WIDTH] * NH)
+            ck = os.path.join(gold, "ckpt_cdiffe_scat.npz")
+            if os.path.exists(ck):  # trained by scripts/bench_posterior_e2e.py (joint DSM, fused), scored vs MCMC
+                z = np.load(ck)
+                self.model.sde.a.load_state_dict({k.replace("_", "."): torch.from_numpy(z[k]) for k in z.files
+                                                  if k.split("_")[0].isdigit()})
+                self.weights = "trained (tests/golden/ckpt_cdiffe_scat.npz: joint DSM on the device, profiles/r3_e2e_cdiffe_pc.json)"
             self.model.sde.a.to(dev)
             self.kw = {"corrector_steps": 1, "snr": 0.16, "precision": args.precision}
             self.flops_sample_step = 2 * flops_per_sample_step(XDIM + YDIM + 1, WIDTH, NH, XDIM + YDIM)
@@ -405,6 +411,7 @@ def other_configs(args, pkg, lib, dev):
                 wl.model.sde.a.to(dev)
                 wl.flops_sample_step = 2 * flops_per_sample_step(XDIM + YDIM + 1, W, NH, XDIM + YDIM)
                 wl.workload = "CDiffE predictor-corrector at the reference width"
+                wl.weights = "random-init"
             if workload != "dps":
                 wl.kernel = f"{fam[precision]}<{mode},{W},...>"
             wl.peak = PEAK_F32_TFLOPS if precision == "fp32" or workload == "dps" else PEAK_BF16_TFLOPS

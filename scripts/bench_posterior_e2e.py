@@ -7,6 +7,9 @@ main_diffusion_scatterometry.py train + evaluate, with generate_scatterometry_gr
     sampled with the fused two-network sampler -- BASELINE config 4's reference method;
   * CDE [W]^3 trained with the reference config's PINNLoss (lam 0.01, lam2 0.001, FPE/L1, IC L2 with the
     -energy_grad initial condition, main_diffusion_scatterometry.py:142-145) on the exact-f32 engine;
+  * CDiffE [W]^3 on the joint z = (x, y) trained with DSMLoss (the only loss the reference's joint
+    training accepts; the fused exact-f32 joint DSM), sampled predictor-only and with the Langevin
+    predictor-corrector (BASELINE config 3: 1 corrector step per step, snr 0.16);
   * for comparison: DPS guided by the same surrogate (fixture prior) and two independent MH runs (the
     KL2 noise floor at this sample size).
 Data: the reference's own generator (inverse-CDF prior samples pushed through the surrogate with its
@@ -38,6 +41,11 @@ def main():
     ap.add_argument("--steps", type=int, default=1000, help="SDE steps")
     ap.add_argument("--y-index", type=int, default=0)
     ap.add_argument("--no-cde", action="store_true")
+    ap.add_argument("--no-posterior", action="store_true")
+    ap.add_argument("--no-cdiffe", action="store_true")
+    ap.add_argument("--snr", type=float, default=0.16, help="corrector signal-to-noise ratio (config 3)")
+    ap.add_argument("--snr-sweep", default="", help="comma-separated corrector snr values to score as well")
+    ap.add_argument("--save-cdiffe", default="", help="write the trained CDiffE's state_dict here (.npz)")
     a = ap.parse_args()
     pkg = importlib.import_module("diffusion-modelling-for-inverse-problems_amd")
     ev = importlib.import_module("diffusion-modelling-for-inverse-problems_amd.evaluate")
@@ -82,15 +90,16 @@ def main():
            "y_index": a.y_index, "n": a.n, "sde_steps": a.steps,
            "mcmc_floor": {"KL2_mcmc_vs_mcmc": ev.hist_kl(h_gt, ev.histograms(gt2, 75, (-1.2, 1.2))[0])[0]}}
 
-    post = pkg.PosteriorDiffusionEstimator(3, 23, [a.width] * 3)
-    post.sde.a.to(dev)
-    plf = pkg.PosteriorLoss(fm, prm["a"], prm["b"], 0.01)  # config_scatterometry.yml lam
-    n0 = pkg._lib.calls.get("posterior_loss_grad", 0)
-    r = train(post, plf, "PosteriorDiffusionEstimator + PosteriorLoss")
-    r["fused_steps"] = pkg._lib.calls.get("posterior_loss_grad", 0) - n0
-    x = post.sample_device(y, a.n, a.steps, seed=7)
-    r["quality"] = score(x)
-    out["posterior"] = r
+    if not a.no_posterior:
+        post = pkg.PosteriorDiffusionEstimator(3, 23, [a.width] * 3)
+        post.sde.a.to(dev)
+        plf = pkg.PosteriorLoss(fm, prm["a"], prm["b"], 0.01)  # config_scatterometry.yml lam
+        n0 = pkg._lib.calls.get("posterior_loss_grad", 0)
+        r = train(post, plf, "PosteriorDiffusionEstimator + PosteriorLoss")
+        r["fused_steps"] = pkg._lib.calls.get("posterior_loss_grad", 0) - n0
+        x = post.sample_device(y, a.n, a.steps, seed=7)
+        r["quality"] = score(x)
+        out["posterior"] = r
 
     if not a.no_cde:
         cde = pkg.CDE(3, 23, [a.width] * 3)
@@ -104,6 +113,24 @@ def main():
         x = cde.sample_device(y, a.n, a.steps, seed=8)
         r["quality"] = score(x)
         out["cde_pinn"] = r
+
+    if not a.no_cdiffe:
+        cd = pkg.CDiffE(3, 23, [a.width] * 3)
+        cd.sde.a.to(dev)
+        n0 = pkg._lib.calls.get("loss_grad_f32", 0)
+        r = train(cd, pkg.DSMLoss(), "CDiffE + DSMLoss on the joint z = (x, y)")
+        r["fused_steps"] = pkg._lib.calls.get("loss_grad_f32", 0) - n0
+        r["quality_predictor_only"] = score(cd.sample_device(y, a.n, a.steps, seed=10))
+        r["quality_predictor_corrector"] = score(cd.sample_device(y, a.n, a.steps, seed=11, corrector_steps=1,
+                                                                  snr=a.snr))
+        r["corrector"] = {"steps_per_sde_step": 1, "snr": a.snr}
+        if a.snr_sweep:  # the corrector's step-size rule at other signal-to-noise ratios
+            r["snr_sweep"] = {v: score(cd.sample_device(y, a.n, a.steps, seed=12, corrector_steps=1, snr=float(v)))
+                              for v in a.snr_sweep.split(",")}
+        out["cdiffe"] = r
+        if a.save_cdiffe:
+            sd = {k.replace(".", "_"): v.detach().cpu().numpy() for k, v in cd.sde.a.state_dict().items()}
+            np.savez(a.save_cdiffe, **sd)
 
     dps = pkg.DPS(3, 23, [256] * 3, fm, prm)
     ck = os.path.join(gold, "ckpt_prior_scat.npz")

@@ -1,0 +1,13 @@
+#!/bin/bash
+# Observed errors of the 16-bit engine's and the f32 training engine's parity tests (their -s reports),
+# for setting each bound at ~2-3x the measured value.   usage: bash scripts/gpu_measure_errs.sh [tag]
+set -u
+TAG=${1:-errs}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_train_f32.py tests/test_gpu_posterior_loss.py \
+  tests/test_gpu_f32.py -m gpu -v -s --timeout 120 --timeout-method thread -p no:cacheprovider > "$OUT/pytest_s.log" 2>&1
+rc=$?; echo "pytest rc=$rc"
+grep -E "^\[|^$|PASSED|FAILED" "$OUT/pytest_s.log" | grep -E "\[" | head -150 > "$OUT/reports.txt"
+case $rc in 0|1) ;; *) exit $rc ;; esac

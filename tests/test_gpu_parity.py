@@ -159,7 +159,8 @@ def test_em_trajectory_injected_noise(dmip, golden, tag):
     err = np.abs(out - ref)
     assert np.all(np.isfinite(out))
     e = _report(f"G3 {tag} {S} steps, err / max|x|", err.max() / max(1.0, np.abs(ref).max()))
-    assert e < 0.05, e
+    # measured (round 3): lin 200 steps 1.21e-4, scat 1000 steps 3.87e-3
+    assert e < {"lin": 3e-4, "scat": 8e-3}[tag], e
 
 
 @pytest.mark.parametrize("tag", ["lin", "scat"])
@@ -172,7 +173,8 @@ def test_em_short_trajectory_injected_noise(dmip, golden, tag):
     out = m.sample_device(torch.from_numpy(tr["y"]).to(DEV), n, S, noise=torch.from_numpy(noise).to(DEV))
     ref = tr["x_final_short"]
     e = _report(f"G3 {tag} {S} steps, err / max|x|", np.abs(out[0].cpu().numpy() - ref).max() / max(1.0, np.abs(ref).max()))
-    assert e < 0.02, e
+    # measured (round 3): lin 2.37e-4, scat 2.18e-3 after 10 steps
+    assert e < {"lin": 5e-4, "scat": 5e-3}[tag], e
 
 
 # --------------------------------------------------------------- posterior distribution (A2)
@@ -294,7 +296,7 @@ def test_sampler_all_widths_vs_oracle_product_rng(dmip, W):
     err = np.abs(x - ref)
     assert np.all(np.isfinite(x))
     e = _report("product-RNG sampler vs oracle, err / max|x|", err.max() / max(1.0, np.abs(ref).max()))
-    assert e < 0.02, e
+    assert e < 1e-4, e  # CDE, widths 64-512: measured 3.2e-5 - 3.9e-5 (round 3)
 
 
 # ------------------------------------------------ fused Posterior / CDiffE samplers vs the oracle
@@ -321,7 +323,7 @@ def test_posterior_sampler_vs_oracle_product_rng(dmip, W, NL, xd, yd):
     err = np.abs(x - ref)
     assert np.all(np.isfinite(x))
     e = _report("product-RNG sampler vs oracle, err / max|x|", err.max() / max(1.0, np.abs(ref).max()))
-    assert e < 0.02, e
+    assert e < 7e-4, e  # Posterior (two networks): measured 2.2e-4 - 3.1e-4 (round 3)
 
 
 @pytest.mark.parametrize("W,NL", [(64, 3), (128, 3), (256, 3), (256, 2), (512, 3), (512, 2)])
@@ -342,7 +344,7 @@ def test_cdiffe_sampler_vs_oracle_product_rng(dmip, W, NL, xd, yd):
     err = np.abs(x - ref)
     assert np.all(np.isfinite(x))
     e = _report("product-RNG sampler vs oracle, err / max|x|", err.max() / max(1.0, np.abs(ref).max()))
-    assert e < 0.02, e
+    assert e < 1.2e-4, e  # CDiffE: measured 2.5e-5 - 5.2e-5 (round 3)
 
 
 @pytest.mark.parametrize("cls", ["PosteriorDiffusionEstimator", "CDiffE"])
@@ -422,6 +424,9 @@ def test_fused_loss_grad_vs_reference_fixture(dmip, golden, name):
     else:
         assert loss == pytest.approx(float(z["dsm_rows"].mean()), rel=1e-2)
     errs = [_rel(g, r) for g, r in zip(grads, ref_grads)]
+    _report(f"G5 {name}: loss rel", abs(loss - (float(z[f"{name}_loss"]) if name != "dsm" else float(z["dsm_rows"].mean())))
+            / abs(float(z[f"{name}_loss"]) if name != "dsm" else float(z["dsm_rows"].mean())))
+    _report(f"G5 {name}: max grad rel L2", max(errs))
     assert max(errs) < 3e-2, errs
 
 
@@ -449,6 +454,8 @@ def test_fused_loss_grad_vs_oracle_ragged(dmip, name, NL):
     assert loss == pytest.approx(ref_loss, rel=1e-2)
     flat_ref = [a for wb in ref for a in wb]
     errs = [_rel(gk, rk) for gk, rk in zip(grads, flat_ref)]
+    _report(f"ragged NL={NL} {name}: loss rel", abs(loss - ref_loss) / abs(ref_loss))
+    _report(f"ragged NL={NL} {name}: max grad rel L2", max(errs))
     assert max(errs) < 3e-2, errs
 
 
@@ -484,8 +491,9 @@ def test_config5_loss_grad_at_batch_65536_vs_oracle(dmip, golden, weights):
     _report(f"config5 B=65536 {weights}: loss rel", lrel)
     _report(f"config5 B=65536 {weights}: max grad rel L2", max(errs))
     print(f"[bf16] config5 {weights} per-tensor grad rel L2: {[f'{e:.2e}' for e in errs]}")
-    assert lrel < 1e-2, lrel
-    assert max(errs) < 3e-2, errs
+    # measured (round 3): loss 5.5e-6 (trained) / 9.7e-8 (init); gradients 1.2e-3 / 2.9e-3
+    assert lrel < 2e-5, lrel
+    assert max(errs) < 6e-3, errs
 
 
 def test_fused_loss_grad_deterministic(dmip, golden):
@@ -553,7 +561,7 @@ def test_cdiffe_predictor_corrector_vs_oracle(dmip, W, xd, yd):
     err = np.abs(x - ref)
     assert np.all(np.isfinite(x))
     e = _report("product-RNG sampler vs oracle, err / max|x|", err.max() / max(1.0, np.abs(ref).max()))
-    assert e < 0.02, e
+    assert e < 4e-5, e  # CDiffE predictor-corrector: measured 7.0e-6 - 1.5e-5 (round 3)
     # the corrector changes the result (it is not silently skipped)
     plain = O.cdiffe_sample(params, y, n, S, seed)
     assert np.abs(plain - ref).max() > 10 * err.max()

@@ -3,9 +3,10 @@ reference's values and gradients -- at the linear fixture's width 64 (G5) and at
 hidden_layers [512]*3 for both problems (G11) -- and against the oracle at other shapes.
 Needs an MI355X: `pytest -m gpu`.
 
-Tolerances (exact f32 arithmetic, summation order differing from torch-CPU's; the PINN residual
-is a difference of nearly equal terms): loss 1e-3 relative, every gradient tensor 1e-2 relative L2 at
-width 512 and 3e-3 at width 64 -- against 1 % / 3 % for the bf16 kernel (test_gpu_parity.py)."""
+Tolerances: exact f32 arithmetic whose summation order differs from torch-CPU's, so the errors are
+f32 rounding (measured, round 3: loss <= 7.5e-7 relative, every gradient tensor <= 9.2e-7 relative L2
+against the reference's own values, <= 3.3e-7 against the float64 oracle; the L1 PDE metric's sign
+flips did not show). Each bound is about 3-5x the measured value, stated beside it."""
 import importlib
 
 import numpy as np
@@ -63,12 +64,14 @@ def test_f32_loss_grad_vs_reference_width64(dmip, golden, name):
     keys = ("0_weight", "0_bias", "3_weight", "3_bias", "5_weight", "5_bias", "7_weight", "7_bias")
     ref_grads = [z[f"{name}_grad_{k}"] for k in keys]
     ref_loss = float(z["dsm_rows"].mean()) if name == "dsm" else float(z[f"{name}_loss"])
-    assert loss == pytest.approx(ref_loss, rel=1e-3)
     if name != "dsm":
-        assert info["PDE-Loss"] == pytest.approx(float(z[f"{name}_PDE_Loss"]), rel=1e-2, abs=1e-7)
+        pde_rel = abs(info["PDE-Loss"] - float(z[f"{name}_PDE_Loss"])) / abs(float(z[f"{name}_PDE_Loss"]))
+        print(f"\n[f32] G5 {name}: PDE component rel {pde_rel:.2e}")
+        assert info["PDE-Loss"] == pytest.approx(float(z[f"{name}_PDE_Loss"]), rel=1e-4, abs=1e-7)
     errs = [_rel(g, r) for g, r in zip(grads, ref_grads)]
     print(f"\n[f32] G5 {name}: loss rel {abs(loss - ref_loss) / abs(ref_loss):.2e}, grad rel L2 {[f'{e:.2e}' for e in errs]}")
-    assert max(errs) < 3e-3, errs
+    assert loss == pytest.approx(ref_loss, rel=3e-6)  # measured <= 7.5e-7 (round 3)
+    assert max(errs) < 3e-6, errs  # measured <= 9.2e-7 (round 3)
 
 
 @pytest.mark.parametrize("tag", ["lin", "scat"])
@@ -95,14 +98,14 @@ def test_f32_loss_grad_vs_reference_width512(dmip, golden, tag):
         lf = dmip.PINNLoss(sp, lam=0.01, lam2=0.001, pde_loss="FPE", ic_metric="L2", pde_metric="L1")
     args = [torch.from_numpy(z[f"{tag}_{k}"]).to(DEV) for k in ("x", "y", "t", "eps")]
     loss, info, grads = _step(dmip, m, lf, *args)
-    assert loss == pytest.approx(float(z[f"{tag}_loss"]), rel=1e-3)
-    assert info["Initial Condition"] == pytest.approx(float(z[f"{tag}_Initial_Condition"]), rel=1e-3)
-    assert info["DSM-Loss"] == pytest.approx(float(z[f"{tag}_DSM_Loss"]), rel=1e-4)
+    assert loss == pytest.approx(float(z[f"{tag}_loss"]), rel=2e-6)  # measured <= 3.5e-7 (round 3)
+    assert info["Initial Condition"] == pytest.approx(float(z[f"{tag}_Initial_Condition"]), rel=1e-4)
+    assert info["DSM-Loss"] == pytest.approx(float(z[f"{tag}_DSM_Loss"]), rel=1e-5)
     keys = ("0_weight", "0_bias", "3_weight", "3_bias", "5_weight", "5_bias", "7_weight", "7_bias")
     errs = [_rel(g, z[f"{tag}_grad_{k}"]) for g, k in zip(grads, keys)]
     print(f"\n[f32] G11 {tag}: loss rel {abs(loss - float(z[f'{tag}_loss'])) / abs(float(z[f'{tag}_loss'])):.2e}, "
           f"grad rel L2 {[f'{e:.2e}' for e in errs]}")
-    assert max(errs) < 1e-2, errs
+    assert max(errs) < 2e-6, errs  # measured <= 4.3e-7 (round 3)
 
 
 @pytest.mark.parametrize("W,NL,n", [(100, 2, 777), (256, 3, 5003), (512, 1, 300)])
@@ -125,11 +128,11 @@ def test_f32_loss_grad_vs_oracle(dmip, W, NL, n, name):
             "pinn_cfpe": dict(kind="pinn", pde="cFPE", pde_metric="L2", ic_metric="L2", lam=1e-3, lam2=0.1)}
     ref_loss, _, ref = O.loss_grad(params, x, y, t, eps, **cfgs[name], ic_A=[[1, 0.5], [0, 1]], ic_b=[0.3, 0.5],
                                    ic_Sinv=np.eye(2) / 0.3)
-    assert loss == pytest.approx(ref_loss, rel=1e-3)
     errs = [_rel(gk, rk) for gk, rk in zip(grads, [a for wb in ref for a in wb])]
     print(f"\n[f32] oracle W={W} L={NL} n={n} {name}: loss rel {abs(loss - ref_loss) / abs(ref_loss):.2e}, "
           f"grad rel L2 {[f'{e:.2e}' for e in errs]}")
-    assert max(errs) < 1e-2, errs
+    assert loss == pytest.approx(ref_loss, rel=3e-7)  # measured <= 4.3e-8 (round 3)
+    assert max(errs) < 1e-6, errs  # measured <= 3.3e-7 (round 3)
 
 
 @pytest.mark.parametrize("weights", ["trained", "init"])
@@ -157,8 +160,8 @@ def test_f32_config5_batch_65536_vs_oracle(dmip, golden, weights):
     errs = [_rel(gk, rk) for gk, rk in zip(grads, [a for wb in ref for a in wb])]
     lrel = abs(loss - ref_loss) / abs(ref_loss)
     print(f"\n[f32] config5 B=65536 {weights}: loss rel {lrel:.2e}, grad rel L2 {[f'{e:.2e}' for e in errs]}")
-    assert lrel < 1e-3, lrel
-    assert max(errs) < 1e-2, errs
+    assert lrel < 2e-7, lrel  # measured 3.2e-8 / 8.8e-10 (round 3)
+    assert max(errs) < 1e-6, errs  # measured <= 2.3e-7 (round 3)
 
 
 def test_f32_loss_grad_deterministic(dmip, golden):
