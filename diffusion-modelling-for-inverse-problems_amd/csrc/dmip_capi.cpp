@@ -186,11 +186,15 @@ struct dmip_mlp {
   char* x3_l1_full = nullptr;     // the same over every input column (X_Y_T networks: CDiffE)
   char* x3_stream = nullptr;      // hidden chunks | output chunk
   float* x3_bias = nullptr;       // [L W + 16]
+  // the k-major engine's images (dmip_x3k.h; width 256, 3 hidden layers, xdim <= 4)
+  char* x3k_stream = nullptr;     // [2 layers][8 k-steps][16 tiles][hi, lo][64][8] fp16
+  char* x3k_out = nullptr;        // [8 k-steps][64][8]: rows 0..xdim-1 W_hi, rows 4..4+xdim-1 W_lo
   ~dmip_mlp() {
     for (void* p : {(void*)ring_l1, (void*)hidden, (void*)ao_samp, (void*)ao_full, (void*)bias_hidden, (void*)bias_out_samp,
                     (void*)bias_out_full, (void*)a1_full, (void*)w1, (void*)b1, (void*)dps_l1, (void*)dps_w2,
                     (void*)dps_w3, (void*)dps_w4, (void*)dps_bias, (void*)f32_l1, (void*)f32_stream,
-                    (void*)f32_bias, (void*)x3_l1, (void*)x3_l1_full, (void*)x3_stream, (void*)x3_bias})
+                    (void*)f32_bias, (void*)x3_l1, (void*)x3_l1_full, (void*)x3_stream, (void*)x3_bias,
+                    (void*)x3k_stream, (void*)x3k_out})
       if (p) (void)hipFree(p);
   }
 };
@@ -306,13 +310,39 @@ int pack_x3_net(dmip_mlp* net, const float* const* weights, const float* const* 
   for (int u = 0; u < W; ++u) bias[u] = (float)(kC * (double)biases[0][u]);
   std::vector<char> stream;
   std::vector<uint16_t> img;
+  // k-major engine (dmip_x3k.h): the same hi / lo fragments, a layer's chunk q = k-step q of all its
+  // tiles ([o][q][p] -> [q][o][p])
+  const bool kmajor = W == 256 && L == 3 && net->xdim >= 1 && net->xdim <= 4;
+  const int KQ = W / 32;
+  std::vector<char> kstream;
   for (int li = 1; li < L; ++li) {
     pack_x3_layer(weights[li], biases[li], W, W, ST, kC, img, bias.data() + (size_t)li * W);
     const char* b = (const char*)img.data();
     stream.insert(stream.end(), b, b + img.size() * 2);
+    if (kmajor)
+      for (int q = 0; q < KQ; ++q)
+        for (int o = 0; o < ST; ++o) {
+          const char* f = b + (((size_t)o * KQ + q) * 2) * 1024;
+          kstream.insert(kstream.end(), f, f + 2048);
+        }
   }
   const int orows = OUT < 16 ? OUT : 16;  // the samplers read output rows 0..15 (the x rows)
   pack_x3_layer(weights[L], biases[L], orows, W, 1, 1.0, img, bias.data() + (size_t)L * W);
+  std::vector<uint16_t> kout;
+  if (kmajor) {  // one fragment per k-step: rows 0..D-1 the hi parts, rows 4..4+D-1 the lo parts
+    const int D = net->xdim;
+    kout.assign((size_t)KQ * 512, 0);
+    for (int q = 0; q < KQ; ++q)
+      for (int l = 0; l < 64; ++l) {
+        const int i = l & 15, gg = l >> 4;
+        int row = -1, part = 0;
+        if (i < D) row = i, part = 0;
+        else if (i >= 4 && i < 4 + D) row = i - 4, part = 1;
+        if (row < 0) continue;
+        for (int m = 0; m < 8; ++m)
+          kout[((size_t)q * 64 + l) * 8 + m] = img[(((size_t)q * 2 + part) * 64 + row + 16 * gg) * 8 + m];
+      }
+  }
   std::vector<char> ochunk((size_t)chunk, 0);
   std::memcpy(ochunk.data(), img.data(), img.size() * 2);
   stream.insert(stream.end(), ochunk.begin(), ochunk.end());
@@ -323,6 +353,11 @@ int pack_x3_net(dmip_mlp* net, const float* const* weights, const float* const* 
   if ((rc = upload(&net->x3_l1, l1b)) || (rc = upload(&net->x3_l1_full, l1fb)) || (rc = upload(&net->x3_stream, stream)) ||
       (rc = upload(&net->x3_bias, bias)))
     return rc;
+  if (kmajor) {
+    std::vector<char> koutb(kout.size() * 2);
+    std::memcpy(koutb.data(), kout.data(), koutb.size());
+    if ((rc = upload(&net->x3k_stream, kstream)) || (rc = upload(&net->x3k_out, koutb))) return rc;
+  }
   return DMIP_OK;
 }
 
@@ -712,6 +747,13 @@ static int em_sample_f32(int mode, const dmip_mlp* net0, const dmip_mlp* net1, c
   return DMIP_OK;
 }
 
+// DMIP_X3K=0 selects the one-tile-per-wave fp32x3 engine (dmip_x3.h) at the k-major engine's shape too
+// (A/B and parity of the two engines; not part of the ABI)
+static bool x3k_enabled() {
+  const char* e = getenv("DMIP_X3K");
+  return !(e && e[0] == '0');
+}
+
 // fp32-accurate split-fp16 samplers (dmip_x3.h): same loop, RNG and sharding as the other engines;
 // arguments already validated by em_sample_impl
 static int em_sample_x3(int mode, const dmip_mlp* net0, const dmip_mlp* net1, const SampleArgs& a) {
@@ -760,7 +802,16 @@ static int em_sample_x3(int mode, const dmip_mlp* net0, const dmip_mlp* net1, co
   p.debug_flags = debug_no_handover();
   p.spin_limit = p.debug_flags ? (1u << 10) : (1u << 22);
   bool ok = false;
-  hipError_t e = dmip::launch_x3_sampler(p, mode, net0->width, net0->n_hidden, xdim, ydim, a.n_y, st, &ok);
+  hipError_t e;
+  if (mode == DMIP_SAMPLER_CDE && net0->x3k_stream && dmip::x3k_sampler_supported(mode, net0->width, net0->n_hidden, xdim) &&
+      x3k_enabled()) {
+    // the k-major multi-tile engine at its shape (dmip_x3k.h)
+    p.net[0].kstream = net0->x3k_stream;
+    p.net[0].kout = net0->x3k_out;
+    e = dmip::launch_x3k_sampler(p, xdim, a.n_y, st, &ok);
+  } else {
+    e = dmip::launch_x3_sampler(p, mode, net0->width, net0->n_hidden, xdim, ydim, a.n_y, st, &ok);
+  }
   if (bias_y) (void)hipFreeAsync(bias_y, st);
   if (!ok) return fail(DMIP_ERR_UNSUPPORTED, "no compiled f32x3 sampler");
   if (e != hipSuccess) return hip_fail(e, "f32x3 sampler launch");

@@ -347,21 +347,17 @@ __global__ void __launch_bounds__(Shape<W>::NW * 64, 1) f32_sampler_kernel(F32Sa
 
       if constexpr (MODE == SAMPLER_CDIFFE) {
         // Langevin corrector steps (the bf16 kernel's definition, dmip_kernels.hip): s = a / g,
-        // eps = 2 alpha (snr |z| / |s|)^2, x <- x + eps s + sqrt(2 eps) z, alpha = exp(-beta delta)
+        // eps = 2 alpha snr^2 var(T - t), x <- x + eps s + sqrt(2 eps) z, alpha = exp(-beta delta)
         for (int c = 0; c < p.n_corr; ++c) {
           float oc[D];
           score(v, oc);
           float z[D], sc[D];
           rng_normals<D>(rng, z);
-          float zn = 0.0f, sn = 0.0f;
 #pragma unroll
-          for (int k = 0; k < D; ++k) {
-            sc[k] = oc[k] / cf.g;
-            zn += z[k] * z[k];
-            sn += sc[k] * sc[k];
-          }
+          for (int k = 0; k < D; ++k) sc[k] = oc[k] / cf.g;
           const float alpha = __expf(-cf.beta * p.delta);
-          const float r = p.snr * p.snr * zn / fmaxf(sn, 1e-30f);
+          const float sd = vp_std(cf.tau, p.bmin, p.bdiff);
+          const float r = (p.snr * p.snr) * (sd * sd);
           const float es = 2.0f * alpha * r;
           const float ns = __fsqrt_rn(2.0f * es);
 #pragma unroll

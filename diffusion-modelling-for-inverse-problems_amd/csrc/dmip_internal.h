@@ -245,6 +245,10 @@ struct X3Net {
   const char* l1;      // [W/16 tiles][K1Q][64 lanes][8 fp16]: layer-1 image (x, t columns -- or every column, CDiffE)
   const char* stream;  // [(L-1) NCH hidden chunks + 1 output chunk][CHUNK bytes] (dmip_x3.h Shape)
   const float* bias;   // [L W + 16]: c b1 | folded hidden biases | folded output bias (rows 0..15)
+  // the k-major engine (dmip_x3k.h; width 256, 3 hidden layers): W x W layers as [layer][k-step][16 tiles]
+  // [hi, lo][64][8] and the output layer as [k-step][64][8] with rows 0..D-1 = W_hi, 4..4+D-1 = W_lo
+  const char* kstream = nullptr;
+  const char* kout = nullptr;
 };
 
 struct X3SamplerParams {
@@ -280,6 +284,9 @@ struct X3BiasPrepParams {
 hipError_t launch_x3_sampler(const X3SamplerParams& p, int mode, int width, int n_hidden, int xdim, int ydim, int n_y,
                              hipStream_t st, bool* supported);
 bool x3_sampler_supported(int mode, int width, int n_hidden, int xdim, int ydim);
+// the k-major multi-tile engine (dmip_x3k.h): CDE, width 256, 3 hidden layers, xdim 2 or 3
+bool x3k_sampler_supported(int mode, int width, int n_hidden, int xdim);
+hipError_t launch_x3k_sampler(const X3SamplerParams& p, int xdim, int n_y, hipStream_t st, bool* ok);
 hipError_t launch_x3_bias_prep(const X3BiasPrepParams& p, int n_y, hipStream_t st);
 // geometry of the x3 images (dmip_x3.h Shape) for the host packer
 int x3_chunk_bytes(int width);

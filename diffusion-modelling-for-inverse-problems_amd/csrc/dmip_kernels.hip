@@ -514,23 +514,23 @@ em_sampler_kernel(SamplerParams p) {
     build_b1<NV, K1S>(v, h, B1);
     if constexpr (MODE != MODE_CDE) __builtin_amdgcn_sched_barrier(0);
     if constexpr (MODE == MODE_CDIFFE) {
-      // Langevin corrector steps at this time, before the predictor (Song et al. 2021 PC sampling,
-      // per-chain step size): s = a/g, eps = 2 alpha (snr |z| / |s|)^2, x <- x + eps s + sqrt(2 eps) z,
-      // alpha = exp(-beta delta) (the discrete VP alpha 1 - beta delta of score_sde, kept positive
-      // for coarse step counts). y_t is held fixed; only x's slots of the layer-1 operand change.
+      // Langevin corrector steps at this time, before the predictor (Song et al. 2021 PC sampling):
+      // s = a/g, eps = 2 alpha (snr |z| / |s|)^2 with the norms at their expected values for the VP
+      // perturbation kernel (|z| ~ sqrt(d), |s| ~ sqrt(d) / std(T - t)), i.e. eps = 2 alpha snr^2
+      // var(T - t) -- one step size per time step, as score_sde's batch-averaged norms give, instead of a
+      // per-chain ratio that explodes where a chain's |s| is small (measured: profiles/r3_e2e_cdiffe_pc.json);
+      // x <- x + eps s + sqrt(2 eps) z, alpha = exp(-beta delta) (the discrete VP alpha 1 - beta delta of
+      // score_sde, kept positive for coarse step counts). y_t is held fixed; only x's slots of the
+      // layer-1 operand change.
       for (int c = 0; c < p.n_corr; ++c) {
         const f32x16 oc = eng.eval(B1);
         float z[D], sc[D];
         rng_normals<D>(rng, z);
-        float zn = 0.0f, sn = 0.0f;
 #pragma unroll
-        for (int k = 0; k < D; ++k) {
-          sc[k] = oc[k] / cf.g;
-          zn += z[k] * z[k];
-          sn += sc[k] * sc[k];
-        }
+        for (int k = 0; k < D; ++k) sc[k] = oc[k] / cf.g;
         const float alpha = __expf(-cf.beta * p.delta);
-        const float r = p.snr * p.snr * zn / fmaxf(sn, 1e-30f);
+        const float sd = vp_std(cf.tau, p.bmin, p.bdiff);
+        const float r = (p.snr * p.snr) * (sd * sd);
         const float es = 2.0f * alpha * r;
         const float ns = __fsqrt_rn(2.0f * es);
 #pragma unroll

@@ -1,0 +1,450 @@
+// fp32-accurate CDE sampler, k-major multi-tile engine: DMIP_PREC_F32X3 at the headline shape (scatterometry
+// and linear CDE, hidden_layers [256]*3, BASELINE configs[1]).
+//
+// Same arithmetic as dmip_x3.h (every product W_hi h_hi + W_hi h_lo + W_lo h_hi on v_mfma_f32_16x16x32_f16,
+// fp32 accumulation, r-form tanh by exp2 + rcp); a different work decomposition, set by what bounds the
+// one-tile-per-wave engine (profiles/r3_x3_pmc.txt): with 128 chains per CU each step streams the two
+// 256 KiB hidden layers from L2 into LDS (4 bytes per weight: hi and lo), so the LDS-DMA issue, the
+// per-chunk barriers and the layer-1 VALU phase -- which the two lock-stepped waves of a SIMD reach
+// together -- cost more than the matrix work leaves room for. Here:
+//   * one wave per SIMD holds NT chain tiles (16 chains each: 48 chains at NT = 3, 384 registers of
+//     activations), so every streamed weight byte feeds NT x as many MFMAs;
+//   * the W x W layers stream k-major: chunk q of a layer is k-step q (32 input units) of all 16 output
+//     tiles, hi and lo fragments (32 KiB). A layer's input is consumed one k-step per chunk, so the
+//     previous layer's activation (and layer 1's double tanh) is spread over the 8 chunks beside their
+//     MFMAs instead of sitting in a VALU-only phase; all 16 output tiles accumulate in registers;
+//   * 16 chunks per step on a 4-slot ring: chunk k of a step is always in slot k % 4, so every ring
+//     address, source offset and DMA destination is a compile-time constant; the DMA is
+//     buffer_load_dwordx4 ... lds with the image offset in an SGPR (no per-lane address arithmetic);
+//   * the output layer (3 rows) is LDS-resident as one fragment per k-step: rows 0..D-1 hold W_hi, rows
+//     4..4+D-1 W_lo, so A . h_hi yields W_hi h_hi and W_lo h_hi in lane groups 0 and 1 and A . h_lo yields
+//     W_hi h_lo in group 0 (8 KiB instead of a 16-row hi + lo chunk).
+// The hidden layers accumulate each output element in the order of dmip_x3.h (k-steps ascending; per
+// k-step hi.h_lo, lo.h_hi, hi.h_hi): bit-identical hidden activations; the output layer's three partial
+// sums are added at the end ((hi.h_hi + hi.h_lo) + lo.h_hi), within an ulp of the one-chain order.
+// Chain state, RNG, schedule, EM update, snapshots and hand-over are the other engines' (dmip_device.h).
+#pragma once
+#include "dmip_x3.h"
+
+namespace dmip {
+namespace x3k {
+
+using x3::f32x4;
+using x3::mfma16;
+
+constexpr int W = 256, ST = 16, KQ = 8, NH = 2;  // [256]*3: layer 1 + two W x W layers
+constexpr int CHUNK = 32768;                     // k-step q of a W x W layer: 16 tiles x (hi, lo) x 1 KiB
+constexpr int NCHUNK = NH * KQ;                  // ring chunks per step
+constexpr int R = 4;                             // ring slots
+constexpr int NWV = 4;                           // one wave per SIMD
+constexpr int PPW = CHUNK / 1024 / NWV;          // LDS-DMA pieces per wave per chunk
+static_assert(NCHUNK % R == 0, "static ring: chunk k of every step in slot k % R");
+
+struct KLay {
+  static constexpr int L1 = 0, L1_BYTES = ST * 1024;      // [16 tiles][64 lanes][8 fp16] (K1Q = 1)
+  static constexpr int OUT = L1 + L1_BYTES, OUT_BYTES = KQ * 1024;  // [8 k-steps][64][8]
+  static constexpr int BIAS = OUT + OUT_BYTES;            // floats: c(b1 + W1_y y) | hidden 1 | hidden 2 | out[16]
+  static constexpr int BF = (NH + 1) * W + 16;
+  static constexpr int BIAS_BYTES = (BF * 4 + 15) / 16 * 16;
+  static constexpr int RING = BIAS + BIAS_BYTES;
+  static constexpr int TOTAL = RING + R * CHUNK;
+};
+static_assert(KLay::TOTAL <= 160 * 1024, "LDS budget");
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+// diagnostic phase stamps (DIAG & 2 only, never in a product kernel): the shader cycle counter, read in an
+// asm statement so that no code moves across it
+__device__ __forceinline__ uint64_t stamp() {
+  uint64_t t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t));
+  return t;
+}
+
+// activate k-step q's two input tiles (z0 = tile 2q, z1 = tile 2q + 1) into the (hi, lo) B operands:
+// dword d of the operand carries units (2d, 2d + 1) of the lane's 8 k-slots (dmip_x3.h act_store)
+template <bool L1>
+__device__ __forceinline__ void act_kstep(const f32x4& z0, const f32x4& z1, u32x4& hh, u32x4& hl) {
+  float r[8];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    r[k] = L1 ? x3::x3_act_r2(z0[k]) : x3::x3_act_r(z0[k]);
+    r[4 + k] = L1 ? x3::x3_act_r2(z1[k]) : x3::x3_act_r(z1[k]);
+  }
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    uint32_t h, l;
+    x3::split_pair(r[2 * d], r[2 * d + 1], h, l);
+    hh[d] = h;
+    hl[d] = l;
+  }
+}
+
+template <int D, int NT, bool NOISE, int DIAG>
+struct KEngine {
+  char* lds;
+  const char* ring_lane;  // ring base + 16 lane
+  __amdgpu_buffer_rsrc_t rs;
+  unsigned voff;          // this wave's DMA pieces: w PPW KiB + 16 lane
+  int w, g;
+
+  // piece Q of chunk C of the step image into slot S (LDS-DMA: 1 KiB per wave-instruction)
+  template <int C, int S, int Q>
+  __device__ __forceinline__ void issue_piece() const {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(lds + KLay::RING + S * CHUNK + (w * PPW + Q) * 1024), 16,
+                                             voff, C * CHUNK + Q * 1024, 0, 0);
+  }
+  template <int C, int S, int Q = 0>
+  __device__ __forceinline__ void issue() const {
+    if constexpr (Q < PPW) {
+      issue_piece<C, S, Q>();
+      issue<C, S, Q + 1>();
+    }
+  }
+
+  __device__ __forceinline__ void start() const {
+    if constexpr (DIAG & 1) return;
+    issue<0, 0>();
+    issue<1, 1>();
+    issue<2, 2>();
+  }
+
+  // chunk K landed for every wave (own pieces by vmcnt, the others' by the barrier), and every wave is
+  // done reading slot (K - 1) % R, which the chunk's MFMA stream refills piece by piece with chunk K + R - 1
+  template <int K>
+  __device__ __forceinline__ void sync() const {
+    if constexpr (DIAG & 1) return;
+    wait_vmcnt<(R - 2) * PPW>();
+    lds_barrier();
+  }
+
+  __device__ __forceinline__ f32x4 bias4(int li, int o) const {
+    return *(const f32x4*)((const float*)(lds + KLay::BIAS) + li * W + 16 * o + 4 * g);
+  }
+
+  // one W x W layer, k-major: In (f32 pre-activations of the previous layer, NT x 16 tiles) -> Out.
+  // Hh/Hl hold k-step 0's operands on entry (activated by the caller); k-step q + 1's are activated
+  // from In during chunk q, a slice per output tile beside that tile's MFMAs.
+  template <int LI, bool IN_L1>
+  __device__ __forceinline__ void layer(const f32x4 (&In)[NT][ST], f32x4 (&Out)[NT][ST], u32x4 (&Hh)[NT],
+                                        u32x4 (&Hl)[NT]) const {
+#pragma unroll
+    for (int o = 0; o < ST; ++o) {
+      const f32x4 b = bias4(LI, o);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) Out[t][o] = b;
+    }
+    chunk<LI, IN_L1, 0>(In, Out, Hh, Hl);
+  }
+
+  template <int LI, bool IN_L1, int Q>
+  __device__ __forceinline__ void chunk(const f32x4 (&In)[NT][ST], f32x4 (&Out)[NT][ST], u32x4 (&Hh)[NT],
+                                        u32x4 (&Hl)[NT]) const {
+    if constexpr (Q < KQ) {
+      constexpr int K = (LI - 1) * KQ + Q;  // chunk index in the step
+      sync<K>();
+      const x3::lds_cptr base = (x3::lds_cptr)(ring_lane + (K % R) * CHUNK);
+      u32x4 Nh[NT], Nl[NT];
+      u32x4 f[3][2];
+      f[0][0] = x3::lds_rd<0>(base);
+      f[0][1] = x3::lds_rd<1024>(base);
+      f[1][0] = x3::lds_rd<2048>(base);
+      f[1][1] = x3::lds_rd<3072>(base);
+      ostep<LI, IN_L1, Q, 0>(base, In, Out, Hh, Hl, Nh, Nl, f);
+      if constexpr (Q + 1 < KQ) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) Hh[t] = Nh[t], Hl[t] = Nl[t];
+      }
+      chunk<LI, IN_L1, Q + 1>(In, Out, Hh, Hl);
+    }
+  }
+
+  // o-step O of chunk (LI, Q): tile O's 3 NT MFMAs (fragments read 2 tiles ahead by explicit ds_read_b128
+  // with counted lgkmcnt waits -- left to itself the compiler hoists all 32 reads to the chunk's top,
+  // 128 more registers), beside one slice of the work the chunk carries: the activation of k-step Q + 1's
+  // operand pair (t, d) = (O / 4, O % 4) for O < 4 NT, and LDS-DMA piece O / 2 of chunk K + R - 1 at odd O.
+  // (The asm reads and waits are scheduling boundaries: what is placed in an o-step stays beside its MFMAs.)
+  template <int LI, bool IN_L1, int Q, int O>
+  __device__ __forceinline__ void ostep(x3::lds_cptr base, const f32x4 (&In)[NT][ST], f32x4 (&Out)[NT][ST],
+                                        const u32x4 (&Hh)[NT], const u32x4 (&Hl)[NT], u32x4 (&Nh)[NT], u32x4 (&Nl)[NT],
+                                        u32x4 (&f)[3][2]) const {
+    if constexpr (O < ST) {
+      constexpr int K = (LI - 1) * KQ + Q;
+      if constexpr (O + 2 < ST) {
+        f[(O + 2) % 3][0] = x3::lds_rd<(O + 2) * 2048>(base);
+        f[(O + 2) % 3][1] = x3::lds_rd<(O + 2) * 2048 + 1024>(base);
+      }
+      x3::lds_wait2<2 * x3::cmin(ST - 1 - O, 2)>(f[O % 3][0], f[O % 3][1]);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        Out[t][O] = mfma16(f[O % 3][0], Hl[t], Out[t][O]);
+        Out[t][O] = mfma16(f[O % 3][1], Hh[t], Out[t][O]);
+        Out[t][O] = mfma16(f[O % 3][0], Hh[t], Out[t][O]);
+      }
+      if constexpr (Q + 1 < KQ && O < 4 * NT) {
+        constexpr int t = O / 4, d = O % 4;
+        const f32x4& z = In[t][2 * Q + 2 + d / 2];
+        const int e = 2 * (d % 2);
+        const float r0 = IN_L1 ? x3::x3_act_r2(z[e]) : x3::x3_act_r(z[e]);
+        const float r1 = IN_L1 ? x3::x3_act_r2(z[e + 1]) : x3::x3_act_r(z[e + 1]);
+        uint32_t h, l;
+        x3::split_pair(r0, r1, h, l);
+        Nh[t][d] = h;
+        Nl[t][d] = l;
+      }
+      if constexpr (!(DIAG & 1) && (O & 1) && O / 2 < PPW)
+        issue_piece<(K + R - 1) % NCHUNK, (K + R - 1) % R, O / 2>();
+      ostep<LI, IN_L1, Q, O + 1>(base, In, Out, Hh, Hl, Nh, Nl, f);
+    }
+  }
+};
+
+// ---------------------------------------------------------------------------- sampler kernel
+// The reverse-SDE loop (models/diffusion.py:27-46) for the CDE, a = net(x, y, tau) with y folded into the
+// per-y layer-1 bias; mu = g a + 0.5 beta x, x <- x + delta mu + sqrt(delta) g xi (dmip_device.h
+// em_update). Work: the balanced WaveSchedule over jobs of NT 16-chain tiles.
+template <int D, int NT, bool NOISE, int DIAG = 0>
+__global__ void __launch_bounds__(NWV * 64, 1) x3k_sampler_kernel(X3SamplerParams p) {
+  using L = KLay;
+  static_assert(D <= 4, "output rows of a chain sit in lane group 0 (D <= 4)");
+  __shared__ __attribute__((aligned(16))) char lds[L::TOTAL];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, j = lane & 15;
+  const int yi = blockIdx.y;
+  constexpr int NV = D + 1;  // layer-1 inputs: x, tau (y folded into the bias)
+
+  KEngine<D, NT, NOISE, DIAG> eng;
+  eng.lds = lds;
+  eng.ring_lane = lds + L::RING + lane * 16;
+  eng.rs = __builtin_amdgcn_make_buffer_rsrc((void*)p.net[0].kstream, 0, NCHUNK * CHUNK, 0x00020000);
+  eng.voff = (unsigned)(w * PPW * 1024 + lane * 16);
+  eng.w = w;
+  eng.g = g;
+  {
+    const uint4* s1 = (const uint4*)p.net[0].l1;
+    uint4* d1 = (uint4*)(lds + L::L1);
+    for (int e = threadIdx.x; e < L::L1_BYTES / 16; e += NWV * 64) d1[e] = s1[e];
+    const uint4* so = (const uint4*)p.net[0].kout;
+    uint4* dout = (uint4*)(lds + L::OUT);
+    for (int e = threadIdx.x; e < L::OUT_BYTES / 16; e += NWV * 64) dout[e] = so[e];
+    float* bl = (float*)(lds + L::BIAS);
+    for (int i = threadIdx.x; i < L::BF; i += NWV * 64) bl[i] = i < W ? p.bias_y[(size_t)yi * W + i] : p.net[0].bias[i];
+    __syncthreads();
+    eng.start();
+  }
+  const char* l1_lane = lds + L::L1 + lane * 16;
+  const char* out_lane = lds + L::OUT + lane * 16;
+
+  const int S = p.num_steps;
+  constexpr int JC = 16 * NT;  // chains per job
+  const long long jobs_y = (p.n_chains + JC - 1) / JC;
+  const long long n_waves = (long long)gridDim.x * NWV;
+  const long long gw = (long long)blockIdx.x * NWV + w;
+  constexpr int XT = sampler_xfer_words(D);  // hand-over words per tile
+  const WaveSchedule sched(jobs_y, S, n_waves, gw);
+  const size_t noise_step = (size_t)gridDim.y * p.n_chains * D;
+
+  uint64_t ph[6] = {0, 0, 0, 0, 0, 0};  // DIAG & 2: cycles per phase (L1, H1, H2, output, EM, barrier waits)
+  for (int sgi = 0; sgi < sched.n_seg; ++sgi) {
+    const Seg sg = sched.segment(sgi);
+    long long c_loc[NT];
+    bool valid[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      c_loc[t] = (long long)(sg.job >= 0 ? sg.job : 0) * JC + 16 * t + j;
+      valid[t] = sg.job >= 0 && c_loc[t] < p.n_chains;
+    }
+    Rng rng[NT];
+    float x[NT][D];
+    if (sg.kind == 2) {  // resume the job the previous wave of the grid handed over
+      const size_t slot = (size_t)yi * n_waves + gw - 1;
+      const bool lost = handover_wait(p.xflag + slot, p.spin_limit, p.err, kErrHandover, lane);
+      const float* src = p.xfer + slot * (size_t)(NT * XT);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const float* st = src + t * XT;
+#pragma unroll
+        for (int k = 0; k < D; ++k) x[t][k] = lost ? __builtin_nanf("") : st[k * 64 + lane];
+        rng[t].s0 = __float_as_uint(st[(D + 0) * 64 + lane]);
+        rng[t].s1 = __float_as_uint(st[(D + 1) * 64 + lane]);
+        rng[t].s2 = __float_as_uint(st[(D + 2) * 64 + lane]);
+        rng[t].s3 = __float_as_uint(st[(D + 3) * 64 + lane]);
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        rng[t] = rng_init(p.seed, (uint64_t)(p.chain_offset + c_loc[t]), (uint64_t)yi);
+        float n0[D];
+        if constexpr (NOISE) {
+          const float* src = p.noise + ((size_t)yi * p.n_chains + (valid[t] ? c_loc[t] : 0)) * D;
+#pragma unroll
+          for (int k = 0; k < D; ++k) n0[k] = src[k];
+        } else {
+          rng_normals<D>(rng[t], n0);
+        }
+#pragma unroll
+        for (int k = 0; k < D; ++k) x[t][k] = __fadd_rn(__fmul_rn(n0[k], p.stdv), p.mean);
+      }
+    }
+
+    int snap_next = p.snap_every > 0 ? (sg.s0 / p.snap_every + 1) * p.snap_every : -1;
+    for (int i0 = sg.s0; i0 < sg.s1; ++i0) {
+      const int i = sg.kind == 3 ? 0 : i0;  // idle steps: a dummy job at step 0, discarded
+      const StepCoef cf = step_coef(i, S, p.T, p.bmin, p.bdiff);
+      uint64_t t0 = 0;
+      if constexpr (DIAG & 2) t0 = stamp();
+
+      // ---- layer 1 (resident image, one MFMA per tile and chain tile), pre-activations in P
+      f32x4 P[NT][ST];
+      {
+        u32x4 b1[NT][1];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          float v[NV];
+#pragma unroll
+          for (int k = 0; k < D; ++k) v[k] = x[t][k];
+          v[NV - 1] = cf.tau;
+          x3::l1_operand<NV, 1>(v, g, b1[t]);
+        }
+#pragma unroll
+        for (int o = 0; o < ST; ++o) {
+          const u32x4 a = *(const u32x4*)(l1_lane + o * 1024);
+          const f32x4 b = eng.bias4(0, o);
+#pragma unroll
+          for (int t = 0; t < NT; ++t) P[t][o] = mfma16(a, b1[t][0], b);
+        }
+      }
+      u32x4 Hh[NT], Hl[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) act_kstep<true>(P[t][0], P[t][1], Hh[t], Hl[t]);
+      // ---- hidden layers 1 and 2 (ring chunks 0..7, 8..15)
+      f32x4 Q[NT][ST];
+      uint64_t t1 = 0;
+      if constexpr (DIAG & 2) t1 = stamp(), ph[0] += t1 - t0;
+      eng.template layer<1, true>(P, Q, Hh, Hl);
+      uint64_t t2 = 0;
+      if constexpr (DIAG & 2) t2 = stamp(), ph[1] += t2 - t1;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) act_kstep<false>(Q[t][0], Q[t][1], Hh[t], Hl[t]);
+      f32x4 P2[NT][ST];
+      eng.template layer<2, false>(Q, P2, Hh, Hl);
+      uint64_t t3 = 0;
+      if constexpr (DIAG & 2) t3 = stamp(), ph[2] += t3 - t2;
+      // ---- output layer (resident): rows 0..D-1 W_hi, 4..4+D-1 W_lo
+      f32x4 oH[NT], oL[NT];
+      {
+        const f32x4 bo = g == 0 ? eng.bias4(NH + 1, 0) : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int t = 0; t < NT; ++t) oH[t] = bo, oL[t] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int q = 0; q < KQ; ++q) {
+          const u32x4 fo = *(const u32x4*)(out_lane + q * 1024);
+#pragma unroll
+          for (int t = 0; t < NT; ++t) {
+            u32x4 eh, el;
+            act_kstep<false>(P2[t][2 * q], P2[t][2 * q + 1], eh, el);
+            oH[t] = mfma16(fo, eh, oH[t]);
+            oL[t] = mfma16(fo, el, oL[t]);
+          }
+        }
+      }
+      uint64_t t4 = 0;
+      if constexpr (DIAG & 2) t4 = stamp(), ph[3] += t4 - t3;
+      // ---- a(x) on every lane of chain j, the EM update
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        float a[D];
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+          const float lo_w = __shfl(oH[t][k], j + 16, 64);  // W_lo h_hi of row k (lane group 1)
+          const float v = (oH[t][k] + oL[t][k]) + lo_w;
+          a[k] = __shfl(v, j, 64);
+        }
+        float xi[D];
+        if constexpr (NOISE) {
+          const float* src = p.noise + noise_step * (i + 1) + ((size_t)yi * p.n_chains + (valid[t] ? c_loc[t] : 0)) * D;
+#pragma unroll
+          for (int k = 0; k < D; ++k) xi[k] = src[k];
+        } else {
+          rng_normals<D>(rng[t], xi);
+        }
+#pragma unroll
+        for (int k = 0; k < D; ++k) x[t][k] = em_update(x[t][k], a[k], xi[k], cf, p.delta, p.sqrt_delta);
+      }
+      if constexpr (DIAG & 2) {
+        ph[4] += stamp() - t4;
+        continue;  // snap_out holds the stamps
+      }
+      if (i0 + 1 == snap_next) {
+        snap_next += p.snap_every;
+        if (sg.kind != 3 && g == 0) {
+#pragma unroll
+          for (int t = 0; t < NT; ++t) {
+            if (!valid[t]) continue;
+            float* dst = p.snap_out +
+                         (((size_t)((i0 + 1) / p.snap_every - 1) * gridDim.y + yi) * p.n_chains + c_loc[t]) * D;
+#pragma unroll
+            for (int k = 0; k < D; ++k) dst[k] = x[t][k];
+          }
+        }
+      }
+    }
+    if (sg.kind == 1) {  // hand the job over to the next wave of the grid
+      const size_t slot = (size_t)yi * n_waves + gw;
+      float* dst = p.xfer + slot * (size_t)(NT * XT);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        float* st = dst + t * XT;
+#pragma unroll
+        for (int k = 0; k < D; ++k) st[k * 64 + lane] = x[t][k];
+        st[(D + 0) * 64 + lane] = __uint_as_float(rng[t].s0);
+        st[(D + 1) * 64 + lane] = __uint_as_float(rng[t].s1);
+        st[(D + 2) * 64 + lane] = __uint_as_float(rng[t].s2);
+        st[(D + 3) * 64 + lane] = __uint_as_float(rng[t].s3);
+      }
+      handover_publish(p.xflag + slot, lane, p.debug_flags);
+    } else if (sg.kind != 3 && g == 0) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        if (!valid[t]) continue;
+        float* dst = p.x_out + ((size_t)yi * p.n_chains + c_loc[t]) * D;
+#pragma unroll
+        for (int k = 0; k < D; ++k) dst[k] = x[t][k];
+      }
+    }
+  }
+  wait_vmcnt<0>();  // the prefetched chunks of a step that never ran land before the workgroup exits
+  if constexpr (DIAG & 2) {
+    if (lane == 0) {
+      uint64_t* dst = (uint64_t*)p.snap_out + ((size_t)yi * n_waves + gw) * 8;
+#pragma unroll
+      for (int k = 0; k < 5; ++k) dst[k] = ph[k];
+      dst[5] = (uint64_t)sched.C;
+    }
+  }
+}
+
+}  // namespace x3k
+
+template <int D, int NT, bool NOISE, int DIAG = 0>
+inline hipError_t launch_x3k_sampler_t(const X3SamplerParams& p, int n_y, hipStream_t st) {
+  constexpr int NWV = x3k::NWV;
+  auto kern = x3k::x3k_sampler_kernel<D, NT, NOISE, DIAG>;
+  const long long jobs = (p.n_chains + 16 * NT - 1) / (16 * NT);
+  long long g = resident_slots(kern, NWV * 64, st) / (n_y > 0 ? n_y : 1);
+  const long long cap = (jobs + NWV - 1) / NWV;
+  if (g > cap) g = cap;
+  if (g < 1) g = 1;
+  X3SamplerParams q = p;
+  char* buf = nullptr;
+  // hand-over slots of NT tiles: (NT (D + 4) - 4 + 4) 64 words each
+  hipError_t e = alloc_handover((size_t)g * n_y * NWV, NT * (D + 4) - 4, st, &buf, &q.xfer, &q.xflag);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(kern, dim3((unsigned)g, (unsigned)n_y), dim3(NWV * 64), 0, st, q);
+  e = hipGetLastError();
+  (void)hipFreeAsync(buf, st);
+  return e;
+}
+
+}  // namespace dmip

@@ -1,0 +1,40 @@
+// The k-major multi-tile fp32x3 CDE sampler (dmip_x3k.h): instantiations and dispatch.
+#include "dmip_x3k.h"
+
+#include <cstdlib>
+
+namespace dmip {
+
+// Development knobs (not part of the ABI): DMIP_X3K_NT = 2 | 3 chain tiles per wave (default 3);
+// DMIP_X3_DIAG = 1 runs the no-ring timing ablation (stale weights; profiles/README.md).
+static int x3k_nt() {
+  const char* e = getenv("DMIP_X3K_NT");
+  return e && atoi(e) == 2 ? 2 : 3;
+}
+static int x3k_diag() {
+  const char* e = getenv("DMIP_X3_DIAG");
+  return e ? atoi(e) : 0;
+}
+
+bool x3k_sampler_supported(int mode, int width, int n_hidden, int xdim) {
+  return mode == SAMPLER_CDE && width == 256 && n_hidden == 3 && (xdim == 2 || xdim == 3);
+}
+
+hipError_t launch_x3k_sampler(const X3SamplerParams& p, int xdim, int n_y, hipStream_t st, bool* ok) {
+  *ok = true;
+  const int nt = x3k_nt();
+  if (x3k_diag() == 1 && xdim == 3 && !p.noise)
+    return nt == 2 ? launch_x3k_sampler_t<3, 2, false, 1>(p, n_y, st) : launch_x3k_sampler_t<3, 3, false, 1>(p, n_y, st);
+  // DMIP_X3_DIAG = 2: per-phase cycle stamps into the snapshot buffer (scripts/x3k_stamps.py)
+  if (x3k_diag() == 2 && xdim == 3 && !p.noise && p.snap_out)
+    return nt == 2 ? launch_x3k_sampler_t<3, 2, false, 2>(p, n_y, st) : launch_x3k_sampler_t<3, 3, false, 2>(p, n_y, st);
+#define X(Dv, NTv)                                                                     \
+  if (xdim == Dv && nt == NTv)                                                         \
+    return p.noise ? launch_x3k_sampler_t<Dv, NTv, true>(p, n_y, st) : launch_x3k_sampler_t<Dv, NTv, false>(p, n_y, st);
+  X(2, 2) X(3, 2) X(2, 3) X(3, 3)
+#undef X
+  *ok = false;
+  return hipSuccess;
+}
+
+}  // namespace dmip

@@ -122,7 +122,9 @@ int dmip_em_sample_posterior(const dmip_mlp* prior, const dmip_mlp* likelihood, 
  *   net   MLP handle (DMIP_INPUT_X_Y_T, in_dim = xdim + ydim + 1, out_dim = xdim + ydim)
  *   corrector_steps, snr   predictor-corrector sampling (BASELINE config 3; no reference code): before
  *         each predictor step, corrector_steps Langevin steps at the same time and y_t (Song et al.
- *         2021, per-chain step size): s = a/g on the x rows, eps = 2 alpha (snr |z| / |s|)^2,
+ *         2021): s = a/g on the x rows, eps = 2 alpha (snr |z| / |s|)^2 with the norms at their
+ *         expected values for the VP perturbation kernel, i.e. eps = 2 alpha snr^2 var(T-t) (one step
+ *         size per time step, as score_sde's batch-averaged norms; a per-chain ratio diverges),
  *         x <- x + eps s + sqrt(2 eps) z, alpha = exp(-beta(T-t) delta) (score_sde's discrete VP
  *         alpha 1 - beta delta to first order, positive at any step count). 0 = plain EM.
  * Other arguments as dmip_em_sample (no injection). */

@@ -344,13 +344,12 @@ def cdiffe_sample(params, y, num_samples, num_steps, seed, mean=0.0, std=1.0, ch
         g = np.sqrt(beta).astype(F32)
         for _ in range(corrector_steps):
             # Langevin corrector (the build's definition, include/dmip.h dmip_em_sample_cdiffe; no
-            # reference code): per-chain step 2 alpha (snr |z| / |s|)^2, alpha = exp(-beta delta)
+            # reference code): step 2 alpha (snr |z| / |s|)^2 at the norms' expected values for the
+            # VP perturbation kernel, 2 alpha snr^2 var(T - t); alpha = exp(-beta delta)
             sc = (cde_a(params, x, y_t, tau[i])[:, :xdim] / g).astype(F32)
             z = rng_normals(st, xdim)
-            zn = np.sum(z * z, axis=1, keepdims=True)
-            sn = np.maximum(np.sum(sc * sc, axis=1, keepdims=True), F32(1e-30))
             alpha = np.exp(-beta * F32(delta)).astype(F32)
-            es = (F32(2.0) * alpha * (F32(snr) * F32(snr) * zn / sn)).astype(F32)
+            es = (F32(2.0) * alpha * ((F32(snr) * F32(snr)) * (sd * sd))).astype(F32)
             x = (x + es * sc + np.sqrt(F32(2.0) * es) * z).astype(F32)
         a = cde_a(params, x, y_t, tau[i])[:, :xdim]
         xi = rng_normals(st, xdim)

@@ -1,0 +1,41 @@
+"""Per-phase cycle stamps of the k-major fp32x3 sampler (DMIP_X3_DIAG=2 build path; diagnostic only): the
+headline workload (100k chains x 1000 steps, scatterometry CDE [256]^3), cycles per step and wave split into
+layer 1, hidden 1, hidden 2, output layer, EM update. One JSON line.   DMIP_X3_DIAG=2 python scripts/x3k_stamps.py"""
+import importlib
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    assert os.environ.get("DMIP_X3_DIAG") == "2"
+    pkg = importlib.import_module("diffusion-modelling-for-inverse-problems_amd")
+    dev = torch.device("cuda:0")
+    torch.manual_seed(0)
+    m = pkg.CDE(3, 23, [256] * 3)
+    m.sde.a.to(dev)
+    y = torch.from_numpy(np.random.default_rng(1).uniform(0, 1, 23).astype(np.float32)).to(dev)
+    n, S = 100000, 1000
+    for _ in range(2):
+        _, snaps = m.sample_trajectory(y, n, S, S, seed=1, precision="fp32x3")
+    torch.cuda.synchronize()
+    raw = snaps.reshape(-1).view(torch.int64).cpu().numpy()
+    st = raw[: (raw.size // 8) * 8].reshape(-1, 8)
+    st = st[st[:, 5] > 0]
+    steps = st[:, 5].astype(np.float64)
+    per = st[:, :5] / steps[:, None]
+    names = ["layer1", "hidden1", "hidden2", "output", "em"]
+    out = {"waves": int(st.shape[0]), "steps_per_wave": float(steps.mean()),
+           "cycles_per_step": {k: float(per[:, i].mean()) for i, k in enumerate(names)},
+           "cycles_per_step_total": float(per.sum(1).mean())}
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
