@@ -55,10 +55,10 @@ def flops_per_sample_step(in_dim=XDIM + YDIM + 1, w=WIDTH, nh=NH, out=XDIM):
 F_PRIOR = flops_per_sample_step(XDIM + 1, WIDTH, NH, XDIM)
 
 # the headline workload's sampler kernel per precision (+ its per-y prep kernel, inside the HIP events)
-KERNELS = {"fp32x3": "x3_sampler_kernel<0,256,3,0,false> (+x3_bias_prep)",
+KERNELS = {"fp32x3": "x3k_sampler_kernel<3,3,false> (+x3_bias_prep)",
            "bf16": "em_sampler_kernel<0,256,3,3,0,8,4,false> (+a1_prep)",
            "fp32": "f32_sampler_kernel<0,256,3,0,false> (+f32_l1_prep)"}
-KERNEL_MATCH = {"fp32x3": "x3_sampler", "bf16": "em_sampler", "fp32": "f32_sampler"}
+KERNEL_MATCH = {"fp32x3": "x3k_sampler_kernel", "bf16": "em_sampler_kernel", "fp32": "f32_sampler_kernel"}
 ARITH = {
     "fp32x3": "fp32-accurate: every product as three fp16 MFMAs W_hi h_hi + W_hi h_lo + W_lo h_hi "
               "(v_mfma_f32_16x16x32_f16, fp32 accumulation; 2^-23.2 of sum|w h| per product vs 2^-23.0 for an fp32 "
@@ -199,17 +199,15 @@ def synthetic_y():
     return np.abs(np.random.default_rng(13).normal(0.3, 0.4, YDIM)).astype(np.float32)
 
 
-def pmc_traffic(kernel_match="x3_sampler"):
-    """HBM bytes per launch of the sampler kernel from the committed rocprofv3 PMC summary
-    (profiles/pmc_summary_latest.json, written by scripts/pmc_summary.py from separate --pmc
-    passes on the same workload), or None."""
-    p = os.path.join(ROOT, "profiles", "pmc_summary_latest.json")
+def pmc_traffic(kernel_family="x3k_sampler_kernel"):
+    """HBM bytes per launch of a sampler kernel family on this workload from the committed rocprofv3 PMC
+    passes (profiles/pmc_traffic.json, written by scripts/pmc_traffic.py from separate FETCH_SIZE and
+    WRITE_SIZE passes over this bench line, corrected per MI355X_MICROARCH.md §HBM), or None."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(p):
         return None
-    z = json.load(open(p))
-    if kernel_match not in z.get("kernel_match", "") or "hbm_bytes_per_launch" not in z:
-        return None
-    return z["hbm_bytes_per_launch"]
+    z = json.load(open(p)).get(kernel_family)
+    return z["hbm_bytes_per_launch"] if z else None
 
 
 def parity_vs_reference(metrics, x, num_steps, weights):

@@ -36,8 +36,13 @@ constexpr int W = 256, ST = 16, KQ = 8, NH = 2;  // [256]*3: layer 1 + two W x W
 constexpr int CHUNK = 32768;                     // k-step q of a W x W layer: 16 tiles x (hi, lo) x 1 KiB
 constexpr int NCHUNK = NH * KQ;                  // ring chunks per step
 constexpr int R = 4;                             // ring slots
-constexpr int NWV = 4;                           // one wave per SIMD
-constexpr int PPW = CHUNK / 1024 / NWV;          // LDS-DMA pieces per wave per chunk
+// waves per workgroup: one per SIMD for 2-3 chain tiles per wave (up to 512 registers), two per SIMD for
+// one tile per wave (<= 256 registers: each wave's VALU chains issue between the other's MFMAs)
+template <int NT>
+struct KWaves {
+  static constexpr int NWV = NT == 1 ? 8 : 4;
+  static constexpr int PPW = CHUNK / 1024 / NWV;  // LDS-DMA pieces per wave per chunk
+};
 static_assert(NCHUNK % R == 0, "static ring: chunk k of every step in slot k % R");
 
 struct KLay {
@@ -82,11 +87,13 @@ __device__ __forceinline__ void act_kstep(const f32x4& z0, const f32x4& z1, u32x
 
 template <int D, int NT, bool NOISE, int DIAG>
 struct KEngine {
+  static constexpr int NWV = KWaves<NT>::NWV, PPW = KWaves<NT>::PPW;
   char* lds;
   const char* ring_lane;  // ring base + 16 lane
   __amdgpu_buffer_rsrc_t rs;
   unsigned voff;          // this wave's DMA pieces: w PPW KiB + 16 lane
   int w, g;
+  mutable uint64_t ph_vm = 0, ph_bar = 0;  // DIAG & 2: cycles in the ring's vmcnt waits and barriers
 
   // piece Q of chunk C of the step image into slot S (LDS-DMA: 1 KiB per wave-instruction)
   template <int C, int S, int Q>
@@ -102,20 +109,49 @@ struct KEngine {
     }
   }
 
-  __device__ __forceinline__ void start() const {
-    if constexpr (DIAG & 1) return;
-    issue<0, 0>();
-    issue<1, 1>();
-    issue<2, 2>();
+  // Ring protocol. Chunk K's barrier B(K) sits in the MIDDLE of chunk K - 1 (o-step 8), not at a chunk
+  // boundary: before it each wave waits for its own pieces of chunk K (vmcnt), after it every wave's
+  // pieces have landed and every wave has finished chunk K - 2, whose slot ((K + 2) % R) the rest of
+  // chunk K - 1 refills with chunk K + 2, piece by piece beside its MFMAs. So the first fragments of
+  // chunk K are read ahead at the end of chunk K - 1 (no LDS latency bubble at a chunk start), and the
+  // barrier waits on nothing but the other waves (no lgkmcnt(0): every read of a refilled slot was consumed
+  // by an MFMA whose operand wait has retired it).
+  __device__ __forceinline__ void start(u32x4 (&fpre)[2][2]) const {
+    if constexpr (!(DIAG & 1)) {
+      issue<0, 0>();
+      issue<1, 1>();
+      issue<2, 2>();
+      wait_vmcnt<2 * PPW>();  // chunk 0 landed (this wave's pieces)
+    }
+    barrier();
+    const x3::lds_cptr b0 = (x3::lds_cptr)ring_lane;
+    fpre[0][0] = x3::lds_rd<0>(b0);
+    fpre[0][1] = x3::lds_rd<1024>(b0);
+    fpre[1][0] = x3::lds_rd<2048>(b0);
+    fpre[1][1] = x3::lds_rd<3072>(b0);
+    x3::lds_wait2<0>(fpre[1][0], fpre[1][1]);
+    x3::lds_wait2<0>(fpre[0][0], fpre[0][1]);
   }
 
-  // chunk K landed for every wave (own pieces by vmcnt, the others' by the barrier), and every wave is
-  // done reading slot (K - 1) % R, which the chunk's MFMA stream refills piece by piece with chunk K + R - 1
-  template <int K>
-  __device__ __forceinline__ void sync() const {
+  __device__ __forceinline__ void barrier() const {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  }
+
+  // B(KN), in the middle of chunk KN - 1: this wave's pieces of chunk KN have landed (chunk KN + 1's, issued
+  // in chunk KN - 2, may still be in flight), then the workgroup barrier
+  template <int KN>
+  __device__ __forceinline__ void sync_mid() const {
     if constexpr (DIAG & 1) return;
-    wait_vmcnt<(R - 2) * PPW>();
-    lds_barrier();
+    uint64_t s0 = 0, s1 = 0;
+    if constexpr (DIAG & 2) s0 = stamp();
+    wait_vmcnt<PPW>();
+    if constexpr (DIAG & 2) s1 = stamp(), ph_vm += s1 - s0;
+    barrier();
+    if constexpr (DIAG & 2) ph_bar += stamp() - s1;
   }
 
   __device__ __forceinline__ f32x4 bias4(int li, int o) const {
@@ -124,57 +160,65 @@ struct KEngine {
 
   // one W x W layer, k-major: In (f32 pre-activations of the previous layer, NT x 16 tiles) -> Out.
   // Hh/Hl hold k-step 0's operands on entry (activated by the caller); k-step q + 1's are activated
-  // from In during chunk q, a slice per output tile beside that tile's MFMAs.
+  // from In during chunk q, a slice per output tile beside that tile's MFMAs. fpre: the first two
+  // fragment pairs of the layer's first chunk on entry, of the next chunk on exit.
   template <int LI, bool IN_L1>
   __device__ __forceinline__ void layer(const f32x4 (&In)[NT][ST], f32x4 (&Out)[NT][ST], u32x4 (&Hh)[NT],
-                                        u32x4 (&Hl)[NT]) const {
+                                        u32x4 (&Hl)[NT], u32x4 (&fpre)[2][2]) const {
 #pragma unroll
     for (int o = 0; o < ST; ++o) {
       const f32x4 b = bias4(LI, o);
 #pragma unroll
       for (int t = 0; t < NT; ++t) Out[t][o] = b;
     }
-    chunk<LI, IN_L1, 0>(In, Out, Hh, Hl);
+    chunk<LI, IN_L1, 0>(In, Out, Hh, Hl, fpre);
   }
 
   template <int LI, bool IN_L1, int Q>
   __device__ __forceinline__ void chunk(const f32x4 (&In)[NT][ST], f32x4 (&Out)[NT][ST], u32x4 (&Hh)[NT],
-                                        u32x4 (&Hl)[NT]) const {
+                                        u32x4 (&Hl)[NT], u32x4 (&fpre)[2][2]) const {
     if constexpr (Q < KQ) {
       constexpr int K = (LI - 1) * KQ + Q;  // chunk index in the step
-      sync<K>();
       const x3::lds_cptr base = (x3::lds_cptr)(ring_lane + (K % R) * CHUNK);
+      const x3::lds_cptr nbase = (x3::lds_cptr)(ring_lane + ((K + 1) % R) * CHUNK);
       u32x4 Nh[NT], Nl[NT];
       u32x4 f[3][2];
-      f[0][0] = x3::lds_rd<0>(base);
-      f[0][1] = x3::lds_rd<1024>(base);
-      f[1][0] = x3::lds_rd<2048>(base);
-      f[1][1] = x3::lds_rd<3072>(base);
-      ostep<LI, IN_L1, Q, 0>(base, In, Out, Hh, Hl, Nh, Nl, f);
+      f[0][0] = fpre[0][0], f[0][1] = fpre[0][1];
+      f[1][0] = fpre[1][0], f[1][1] = fpre[1][1];
+      ostep<LI, IN_L1, Q, 0>(base, nbase, In, Out, Hh, Hl, Nh, Nl, f, fpre);
+      // the next chunk's first fragments (read at o-steps 14 and 15) are complete before they leave the
+      // chunk: an asm load's registers must not be copied before its data lands
+      x3::lds_wait2<0>(fpre[0][0], fpre[0][1]);
+      x3::lds_wait2<0>(fpre[1][0], fpre[1][1]);
       if constexpr (Q + 1 < KQ) {
 #pragma unroll
         for (int t = 0; t < NT; ++t) Hh[t] = Nh[t], Hl[t] = Nl[t];
       }
-      chunk<LI, IN_L1, Q + 1>(In, Out, Hh, Hl);
+      chunk<LI, IN_L1, Q + 1>(In, Out, Hh, Hl, fpre);
     }
   }
 
-  // o-step O of chunk (LI, Q): tile O's 3 NT MFMAs (fragments read 2 tiles ahead by explicit ds_read_b128
-  // with counted lgkmcnt waits -- left to itself the compiler hoists all 32 reads to the chunk's top,
-  // 128 more registers), beside one slice of the work the chunk carries: the activation of k-step Q + 1's
-  // operand pair (t, d) = (O / 4, O % 4) for O < 4 NT, and LDS-DMA piece O / 2 of chunk K + R - 1 at odd O.
-  // (The asm reads and waits are scheduling boundaries: what is placed in an o-step stays beside its MFMAs.)
+  // o-step O of chunk K = (LI, Q): tile O's 3 NT MFMAs (fragments read 2 tiles ahead -- across the chunk
+  // boundary at O = 14, 15 -- by explicit ds_read_b128 with counted lgkmcnt waits; left to itself the
+  // compiler hoists all 32 reads to the chunk's top, 128 more registers), beside one slice of the work the
+  // chunk carries: the activation of k-step Q + 1's operand pair (t, d) = (O / 4, O % 4) for O < 4 NT;
+  // B(K + 1) at O = 8; LDS-DMA pieces of chunk K + 3 at O = 9..15. (The asm reads and waits are scheduling
+  // boundaries: what is placed in an o-step stays beside its MFMAs.)
   template <int LI, bool IN_L1, int Q, int O>
-  __device__ __forceinline__ void ostep(x3::lds_cptr base, const f32x4 (&In)[NT][ST], f32x4 (&Out)[NT][ST],
-                                        const u32x4 (&Hh)[NT], const u32x4 (&Hl)[NT], u32x4 (&Nh)[NT], u32x4 (&Nl)[NT],
-                                        u32x4 (&f)[3][2]) const {
+  __device__ __forceinline__ void ostep(x3::lds_cptr base, x3::lds_cptr nbase, const f32x4 (&In)[NT][ST],
+                                        f32x4 (&Out)[NT][ST], const u32x4 (&Hh)[NT], const u32x4 (&Hl)[NT],
+                                        u32x4 (&Nh)[NT], u32x4 (&Nl)[NT], u32x4 (&f)[3][2],
+                                        u32x4 (&fpre)[2][2]) const {
     if constexpr (O < ST) {
       constexpr int K = (LI - 1) * KQ + Q;
       if constexpr (O + 2 < ST) {
         f[(O + 2) % 3][0] = x3::lds_rd<(O + 2) * 2048>(base);
         f[(O + 2) % 3][1] = x3::lds_rd<(O + 2) * 2048 + 1024>(base);
+      } else {  // the next chunk's fragment O + 2 - 16 (its barrier has passed at O = 8)
+        fpre[O + 2 - ST][0] = x3::lds_rd<(O + 2 - ST) * 2048>(nbase);
+        fpre[O + 2 - ST][1] = x3::lds_rd<(O + 2 - ST) * 2048 + 1024>(nbase);
       }
-      x3::lds_wait2<2 * x3::cmin(ST - 1 - O, 2)>(f[O % 3][0], f[O % 3][1]);
+      x3::lds_wait2<4>(f[O % 3][0], f[O % 3][1]);  // two younger fragment pairs are always in flight
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         Out[t][O] = mfma16(f[O % 3][0], Hl[t], Out[t][O]);
@@ -192,9 +236,16 @@ struct KEngine {
         Nh[t][d] = h;
         Nl[t][d] = l;
       }
-      if constexpr (!(DIAG & 1) && (O & 1) && O / 2 < PPW)
-        issue_piece<(K + R - 1) % NCHUNK, (K + R - 1) % R, O / 2>();
-      ostep<LI, IN_L1, Q, O + 1>(base, In, Out, Hh, Hl, Nh, Nl, f);
+      if constexpr (O == 8) sync_mid<(K + 1) % NCHUNK>();
+      if constexpr (!(DIAG & 1) && PPW == 8 && O == 9) {
+        issue_piece<(K + R - 1) % NCHUNK, (K + R - 1) % R, 0>();
+        issue_piece<(K + R - 1) % NCHUNK, (K + R - 1) % R, 1>();
+      }
+      if constexpr (!(DIAG & 1) && PPW == 8 && O >= 10)
+        issue_piece<(K + R - 1) % NCHUNK, (K + R - 1) % R, O - 8>();
+      if constexpr (!(DIAG & 1) && PPW == 4 && O >= 9 && O < 13)
+        issue_piece<(K + R - 1) % NCHUNK, (K + R - 1) % R, O - 9>();
+      ostep<LI, IN_L1, Q, O + 1>(base, nbase, In, Out, Hh, Hl, Nh, Nl, f, fpre);
     }
   }
 };
@@ -204,7 +255,8 @@ struct KEngine {
 // per-y layer-1 bias; mu = g a + 0.5 beta x, x <- x + delta mu + sqrt(delta) g xi (dmip_device.h
 // em_update). Work: the balanced WaveSchedule over jobs of NT 16-chain tiles.
 template <int D, int NT, bool NOISE, int DIAG = 0>
-__global__ void __launch_bounds__(NWV * 64, 1) x3k_sampler_kernel(X3SamplerParams p) {
+__global__ void __launch_bounds__(KWaves<NT>::NWV * 64, KWaves<NT>::NWV / 4) x3k_sampler_kernel(X3SamplerParams p) {
+  constexpr int NWV = KWaves<NT>::NWV, PPW = KWaves<NT>::PPW;
   using L = KLay;
   static_assert(D <= 4, "output rows of a chain sit in lane group 0 (D <= 4)");
   __shared__ __attribute__((aligned(16))) char lds[L::TOTAL];
@@ -231,8 +283,9 @@ __global__ void __launch_bounds__(NWV * 64, 1) x3k_sampler_kernel(X3SamplerParam
     float* bl = (float*)(lds + L::BIAS);
     for (int i = threadIdx.x; i < L::BF; i += NWV * 64) bl[i] = i < W ? p.bias_y[(size_t)yi * W + i] : p.net[0].bias[i];
     __syncthreads();
-    eng.start();
   }
+  u32x4 fpre[2][2];  // the first fragment pairs of the next ring chunk (read ahead across phases)
+  eng.start(fpre);
   const char* l1_lane = lds + L::L1 + lane * 16;
   const char* out_lane = lds + L::OUT + lane * 16;
 
@@ -322,13 +375,13 @@ __global__ void __launch_bounds__(NWV * 64, 1) x3k_sampler_kernel(X3SamplerParam
       f32x4 Q[NT][ST];
       uint64_t t1 = 0;
       if constexpr (DIAG & 2) t1 = stamp(), ph[0] += t1 - t0;
-      eng.template layer<1, true>(P, Q, Hh, Hl);
+      eng.template layer<1, true>(P, Q, Hh, Hl, fpre);
       uint64_t t2 = 0;
       if constexpr (DIAG & 2) t2 = stamp(), ph[1] += t2 - t1;
 #pragma unroll
       for (int t = 0; t < NT; ++t) act_kstep<false>(Q[t][0], Q[t][1], Hh[t], Hl[t]);
       f32x4 P2[NT][ST];
-      eng.template layer<2, false>(Q, P2, Hh, Hl);
+      eng.template layer<2, false>(Q, P2, Hh, Hl, fpre);
       uint64_t t3 = 0;
       if constexpr (DIAG & 2) t3 = stamp(), ph[2] += t3 - t2;
       // ---- output layer (resident): rows 0..D-1 W_hi, 4..4+D-1 W_lo
@@ -421,6 +474,8 @@ __global__ void __launch_bounds__(NWV * 64, 1) x3k_sampler_kernel(X3SamplerParam
 #pragma unroll
       for (int k = 0; k < 5; ++k) dst[k] = ph[k];
       dst[5] = (uint64_t)sched.C;
+      dst[6] = eng.ph_vm;
+      dst[7] = eng.ph_bar;
     }
   }
 }
@@ -429,7 +484,7 @@ __global__ void __launch_bounds__(NWV * 64, 1) x3k_sampler_kernel(X3SamplerParam
 
 template <int D, int NT, bool NOISE, int DIAG = 0>
 inline hipError_t launch_x3k_sampler_t(const X3SamplerParams& p, int n_y, hipStream_t st) {
-  constexpr int NWV = x3k::NWV;
+  constexpr int NWV = x3k::KWaves<NT>::NWV;
   auto kern = x3k::x3k_sampler_kernel<D, NT, NOISE, DIAG>;
   const long long jobs = (p.n_chains + 16 * NT - 1) / (16 * NT);
   long long g = resident_slots(kern, NWV * 64, st) / (n_y > 0 ? n_y : 1);

@@ -9,7 +9,8 @@ namespace dmip {
 // DMIP_X3_DIAG = 1 runs the no-ring timing ablation (stale weights; profiles/README.md).
 static int x3k_nt() {
   const char* e = getenv("DMIP_X3K_NT");
-  return e && atoi(e) == 2 ? 2 : 3;
+  const int v = e ? atoi(e) : 3;
+  return v == 1 || v == 2 ? v : 3;
 }
 static int x3k_diag() {
   const char* e = getenv("DMIP_X3_DIAG");
@@ -27,11 +28,13 @@ hipError_t launch_x3k_sampler(const X3SamplerParams& p, int xdim, int n_y, hipSt
     return nt == 2 ? launch_x3k_sampler_t<3, 2, false, 1>(p, n_y, st) : launch_x3k_sampler_t<3, 3, false, 1>(p, n_y, st);
   // DMIP_X3_DIAG = 2: per-phase cycle stamps into the snapshot buffer (scripts/x3k_stamps.py)
   if (x3k_diag() == 2 && xdim == 3 && !p.noise && p.snap_out)
-    return nt == 2 ? launch_x3k_sampler_t<3, 2, false, 2>(p, n_y, st) : launch_x3k_sampler_t<3, 3, false, 2>(p, n_y, st);
+    return nt == 1   ? launch_x3k_sampler_t<3, 1, false, 2>(p, n_y, st)
+           : nt == 2 ? launch_x3k_sampler_t<3, 2, false, 2>(p, n_y, st)
+                     : launch_x3k_sampler_t<3, 3, false, 2>(p, n_y, st);
 #define X(Dv, NTv)                                                                     \
   if (xdim == Dv && nt == NTv)                                                         \
     return p.noise ? launch_x3k_sampler_t<Dv, NTv, true>(p, n_y, st) : launch_x3k_sampler_t<Dv, NTv, false>(p, n_y, st);
-  X(2, 2) X(3, 2) X(2, 3) X(3, 3)
+  X(2, 1) X(3, 1) X(2, 2) X(3, 2) X(2, 3) X(3, 3)
 #undef X
   *ok = false;
   return hipSuccess;

@@ -15,7 +15,8 @@ from collections import defaultdict
 def summarise(tag, match="em_sampler"):
     vals = defaultdict(list)
     durs = []
-    for f in sorted(glob.glob(f"gpurun_out/{tag}/pmc_*/pmc_counter_collection.csv")):
+    for f in sorted(glob.glob(f"gpurun_out/{tag}/pmc_*/pmc_counter_collection.csv") +
+                    glob.glob(f"gpurun_out/{tag}/pmc_counter_collection.csv")):
         seen = {}
         for row in csv.DictReader(open(f)):
             if match not in row["Kernel_Name"]:

@@ -33,7 +33,9 @@ def main():
     names = ["layer1", "hidden1", "hidden2", "output", "em"]
     out = {"waves": int(st.shape[0]), "steps_per_wave": float(steps.mean()),
            "cycles_per_step": {k: float(per[:, i].mean()) for i, k in enumerate(names)},
-           "cycles_per_step_total": float(per.sum(1).mean())}
+           "cycles_per_step_total": float(per.sum(1).mean()),
+           "ring_vmcnt_wait_per_step": float((st[:, 6] / steps).mean()),
+           "ring_barrier_per_step": float((st[:, 7] / steps).mean())}
     print(json.dumps(out), flush=True)
 
 
