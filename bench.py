@@ -462,9 +462,39 @@ def other_configs(args, pkg, lib, dev):
             "value": B / (ms * 1e-3), "unit": "samples/s", "ms_per_step": ms,
             "roofline": {"achieved": ach, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": ach / PEAK_BF16_TFLOPS},
             "loss_finite": bool(torch.isfinite(out_loss).all())}
+        try:
+            out["config5_pinn_train_step"]["loss_vs_ref"] = config5_loss_check(tr, m, lf, prob, B, dev)
+        except Exception as e:  # noqa: BLE001
+            out["config5_pinn_train_step"]["loss_vs_ref"] = {"error": f"{type(e).__name__}: {e}"}
     except Exception as e:  # noqa: BLE001
         out["config5_pinn_train_step"] = {"error": f"{type(e).__name__}: {e}"}
     return out
+
+
+def config5_loss_check(tr, m, lf, prob, B, dev):
+    """BASELINE configs[4]'s loss-vs-ref tolerance check at its own batch: on one seeded batch (x, y, t,
+    eps of the timed shape) the timed bf16 kernel's PINNLoss value and all 8 gradient tensors against the
+    exact-f32 engine (dmip_loss_grad_f32), which reproduces the reference's own loss and gradients
+    (losses.py:214-242) to <= 3e-6 (tests/test_gpu_train_f32.py, fixtures G5/G11). Bounds: those of
+    tests/test_gpu_parity.py::test_config5_loss_grad_at_batch_65536_vs_oracle (loss 2e-5, gradients 6e-3)."""
+    import torch
+    g = torch.Generator().manual_seed(2024)
+    x = torch.randn(B, 2, generator=g)
+    y = x @ prob.A.T + prob.b + 0.3 * torch.randn(B, 2, generator=g)
+    t = 1e-4 + torch.rand(B, 1, generator=g) * (1 - 1e-4)
+    eps = torch.randn(B, 2, generator=g)
+    args = [a.to(dev) for a in (x, y, t, eps)]
+    cfg = tr.fused_config(m, lf)
+    res = {}
+    for prec in ("bf16", "fp32"):
+        loss, _ = tr.fused_loss_grad(m, lf, cfg, *args, precision=prec)
+        res[prec] = (float(loss), [p.grad.detach().double().clone() for p in m.sde.a.parameters()])
+    (lb, gb), (lr, gr) = res["bf16"], res["fp32"]
+    lrel = abs(lb - lr) / max(abs(lr), 1e-30)
+    grel = max(float((a - b).norm() / max(float(b.norm()), 1e-30)) for a, b in zip(gb, gr))
+    return {"loss": lb, "loss_ref": lr, "loss_rel": lrel, "max_grad_rel_l2": grel,
+            "bound": {"loss_rel": 2e-5, "grad_rel_l2": 6e-3}, "pass": lrel < 2e-5 and grel < 6e-3,
+            "ref": "exact-f32 engine on the same batch (pinned to the reference's loss/gradients, G5/G11, <= 3e-6)"}
 
 
 def side_mode(wl, args, dist, world, dev, lib, metrics, precision, steps, S, flops_launch):
