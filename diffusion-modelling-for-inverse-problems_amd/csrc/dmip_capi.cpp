@@ -1071,7 +1071,8 @@ static int loss_grad_bf16_impl(int in_dim, int out_dim, int n_hidden, const int*
       (size_t)n_wg * dmip::train_partials_per_wg() * dmip::train_partial_stride(n_hidden) * sizeof(float);
   // one scratch allocation: the partial rows, then the packed LDS image of the weights
   const size_t part_pad = (part_bytes + 255) / 256 * 256;
-  const size_t need = part_pad + (size_t)dmip::train_packed_bytes(n_hidden);
+  const size_t packed_pad = ((size_t)dmip::train_packed_bytes(n_hidden) + 255) / 256 * 256;
+  const size_t need = part_pad + packed_pad + dmip::train_adj_bytes(batch);
   if (ws && ws->query) {
     ws->bytes = need;
     return DMIP_OK;
@@ -1085,6 +1086,7 @@ static int loss_grad_bf16_impl(int in_dim, int out_dim, int n_hidden, const int*
     return fail(DMIP_ERR_ALLOC, std::string("hipMallocAsync: ") + hipGetErrorString(e));
   }
   p.packed = (char*)partials + part_pad;
+  p.adj = dmip::train_adj_bytes(batch) ? (float*)((char*)partials + part_pad + packed_pad) : nullptr;
   e = dmip::launch_loss_grad(p, n_hidden, grad_out_dev, loss_out_dev, partials, n_wg, st);
   if (!ws) (void)hipFreeAsync(partials, st);
   if (e != hipSuccess) return hip_fail(e, "loss_grad launch");

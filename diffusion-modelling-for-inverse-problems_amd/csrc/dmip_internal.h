@@ -118,13 +118,17 @@ struct TrainParams {
   float icA[4], icb[2], icS[4];  // linear-problem IC target: -x + ((y - (A x + b)) S^T) A
   float* partials;            // [n_waves][partial stride]
   char* packed;               // the shared LDS image of the weight fragments (written by the pack kernel)
+  float* adj;                 // split build: [n][kTrainAdj] per-sample loss adjoints + loss terms (forward -> reverse)
 };
+constexpr int kTrainAdj = 12;  // abP[2] abV[2] abC[2] dsm ic pde, padded to 48 bytes
 
+bool train_split();
 int train_nparam(int n_hidden);
 int train_partial_stride(int n_hidden);
 int train_waves_per_wg();
 int train_partials_per_wg();
 int train_packed_bytes(int n_hidden);
+size_t train_adj_bytes(long long batch);  // 0 unless the forward / reverse split kernels run
 hipError_t launch_loss_grad(const TrainParams& p, int n_hidden, float* grads, float* loss_out, float* partials,
                             int n_wg, hipStream_t st);
 

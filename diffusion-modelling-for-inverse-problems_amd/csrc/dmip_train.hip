@@ -25,6 +25,9 @@
 // v_mfma_f32_32x32x16_bf16 (K = the tile's 16 samples). Each wave accumulates its gradient partial
 // in its own row of `partials` (global, 4-wave build) or LDS region (2-wave build, summed in wave
 // order per workgroup); loss_grad_reduce_kernel sums the rows in a fixed order (deterministic).
+#include <algorithm>
+#include <cstdlib>
+
 #include "dmip_device.h"
 #include "dmip_internal.h"
 
@@ -60,8 +63,20 @@ constexpr int NSTREAM = 8;      // P, V, C, E0, E1, E00, E01, E11
 static_assert(W == 64 && D == 2, "compiled for the linear problem's width-64 CDE");
 static_assert(3 * IN + 2 <= 32, "layer-1 split operand fits one k-step");
 
-template <int NL>
+// PH: 0 = the fused kernel (forward jets, loss terms and reverse pass in one wave, one wave per SIMD);
+// 1 = the forward half (jets + per-sample loss terms and adjoints into p.adj; two waves per SIMD);
+// 2 = the reverse half (adjoints from p.adj, recompute + weight gradients; ~450 registers, one wave per SIMD:
+// at two waves per SIMD it spills ~220 registers). The reverse half accumulates the workgroup's gradient in
+// ONE LDS partial, its waves taking turns: at turn k wave w adds sub-block (w + k) % 4 of a layer's
+// gradient, a workgroup barrier between turns, so every address is summed in a fixed wave order
+// (deterministic) with no global atomics (~160 per tile in the fused kernel: its L2 atomic rate alone,
+// ~50 ns per 256-byte wave-instruction per CU, was ~130 us of the 0.3 ms)
+template <int NL, int PH = 0>
 struct TL {
+  static constexpr int NW = PH == 0 ? NWV : 4;               // waves per workgroup
+  static constexpr bool TURN = PH == 2;                      // one LDS partial per workgroup, waves take turns
+  static constexpr bool GG = PH == 0 ? GACC_GLOBAL : false;  // gradient partial rows in global memory
+  static constexpr int RSV = PH == 2 ? 16 : RS;              // scratch row stride (reverse half: unpadded, to fit)
   static constexpr int p_w(int l) { return l == 0 ? 0 : W * IN + W + (l - 1) * (W * W + W); }
   static constexpr int p_b(int l) { return l == NL ? p_w(NL) + OUT * W : p_w(l) + (l == 0 ? W * IN : W * W); }
   static constexpr int NPARAM = p_w(NL) + OUT * W + OUT;
@@ -71,16 +86,18 @@ struct TL {
   static constexpr int WFL = WF + (NL - 1) * 8192;       // their bf16 residuals (lo), for the split products
   static constexpr int WT = WFL + (NL - 1) * 8192;       // transposed fragments (reverse pass)
   static constexpr int A1 = WT + (NL - 1) * 8192;        // layer-1 split fragments
-  static constexpr int AO = A1 + 4096;                   // output layer, rows duplicated per lane group
-  static constexpr int AOL = AO + 2048;                  // its lo residuals
-  static constexpr int AOT = AOL + 2048;                 // output layer transposed
+  static constexpr int AOT = A1 + 4096;                  // output layer transposed
   static constexpr int BIAS = AOT + 4096;                // fp32 [NL + 1][64]: b_l of hidden l, b_out at NL
-  static constexpr int COL = BIAS + (NL + 1) * W * 4;    // fp32 [D][64]: layer-1 weight columns of x
+  static constexpr int AO = BIAS + (NL + 1) * W * 4;     // output layer, rows duplicated per lane group (forward)
+  static constexpr int AOL = AO + 2048;                  // its lo residuals (forward)
+  static constexpr int COL = AOL + 2048;                 // fp32 [D][64]: layer-1 weight columns of x (forward)
   static constexpr int WAVE = COL + D * W * 4;
+  static constexpr int IMG = PH == 2 ? AO : WAVE;        // image bytes this kernel copies (reverse: no forward-only parts)
+  static constexpr int GP_BYTES = TURN ? ((PART * 4 + 15) / 16) * 16 : 0;  // the workgroup's LDS partial (TURN)
   static constexpr int GACC = 0;                         // per wave: fp32 gradient partial (param order, LDS mode)
-  static constexpr int SCR = GACC_GLOBAL ? 0 : ((PART * 4 + 15) / 16) * 16;  // per wave: 6 transposed [64][16] bf16
-  static constexpr int WAVE_BYTES = SCR + 6 * W * RS * 2;
-  static constexpr int TOTAL = WAVE + NWV * WAVE_BYTES;
+  static constexpr int SCR = (GG || TURN) ? 0 : ((PART * 4 + 15) / 16) * 16;  // per wave: 6 transposed [64][16] bf16
+  static constexpr int WAVE_BYTES = PH == 1 ? 0 : SCR + 6 * W * RSV * 2;
+  static constexpr int TOTAL = IMG + GP_BYTES + NW * WAVE_BYTES;
   static_assert(TOTAL <= 160 * 1024, "LDS budget");
 };
 
@@ -123,11 +140,12 @@ __device__ __forceinline__ const bf16x8& frag(const char* base, int idx, int lan
 }
 
 // write one acc-form stream (64 units x 16 samples) transposed: scr[unit][sample] bf16
+template <int RSV>
 __device__ __forceinline__ void put_t(__bf16* scr, const f32x4 (&z)[4], int g, int c16) {
 #pragma unroll
   for (int R = 0; R < 4; ++R)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) scr[(16 * R + 4 * g + r) * RS + c16] = (__bf16)z[R][r];
+    for (int r = 0; r < 4; ++r) scr[(16 * R + 4 * g + r) * RSV + c16] = (__bf16)z[R][r];
 }
 
 __device__ __forceinline__ void pack_b(const f32x4 (&z)[4], bf16x8 (&b)[2]) {
@@ -164,9 +182,10 @@ __device__ __forceinline__ f32x4 mm3(const bf16x8& a0, const bf16x8& a1, const b
 }
 
 // the 32x32x16 operand of a sample-contracted product: lane (i, hh) reads row (row0 + i), samples 8hh..8hh+7
+template <int RSV>
 __device__ __forceinline__ bf16x8 tread(const __bf16* scr, int row, bool ok, int hh) {
   if (!ok) return bf16x8{};
-  return *(const bf16x8*)(scr + row * RS + 8 * hh);
+  return *(const bf16x8*)(scr + row * RSV + 8 * hh);
 }
 
 // The shared part of the LDS image (weight fragments, biases, layer-1 columns), packed ONCE per
@@ -238,14 +257,24 @@ __global__ void __launch_bounds__(256) train_pack_kernel(TrainParams p) {
 // wait for a load of its own row before every update: those read-modify-write round trips sat on the
 // tile's dependency chain); the row is the wave's own, and its updates to one address are issued in
 // program order, so the sums keep a fixed order. In LDS a plain add.
+// TURN: a workgroup barrier after this wave's LDS adds have completed (the next turn's adds may touch them)
+__device__ __forceinline__ void turn_barrier() {
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+  __builtin_amdgcn_s_barrier();
+}
+
+template <bool GG>
 __device__ __forceinline__ void gadd(float* a, float v) {
-  if constexpr (GACC_GLOBAL) (void)__hip_atomic_fetch_add(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if constexpr (GG) (void)__hip_atomic_fetch_add(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   else *a += v;
 }
 
-template <int NL>
-__global__ void __launch_bounds__(NWV * 64, 1) loss_grad_kernel(TrainParams p) {
-  using L = TL<NL>;
+template <int NL, int PH = 0>
+__global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss_grad_kernel(TrainParams p) {
+  using L = TL<NL, PH>;
+  constexpr int NWV = L::NW;
+  constexpr bool GACC_GLOBAL = L::GG;
+  constexpr int RS = L::RSV;
   __shared__ __attribute__((aligned(16))) char lds[L::TOTAL];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -255,12 +284,16 @@ __global__ void __launch_bounds__(NWV * 64, 1) loss_grad_kernel(TrainParams p) {
 
   // ---- the shared LDS image (packed once per launch by train_pack_kernel): 16-byte copies
   {
-    static_assert(L::WAVE % 16 == 0, "LDS image is a whole number of 16-byte pieces");
+    static_assert(L::IMG % 16 == 0, "LDS image is a whole number of 16-byte pieces");
     const uint4* src = (const uint4*)p.packed;
     uint4* dst = (uint4*)lds;
 #pragma unroll 4
-    for (int e = tid; e < L::WAVE / 16; e += NWV * 64) dst[e] = src[e];
-    if constexpr (!GACC_GLOBAL) {
+    for (int e = tid; e < L::IMG / 16; e += NWV * 64) dst[e] = src[e];
+    if constexpr (PH == 1) {
+    } else if constexpr (L::TURN) {
+      float* gp = (float*)(lds + L::IMG);
+      for (int e = tid; e < L::PART; e += NWV * 64) gp[e] = 0.0f;
+    } else if constexpr (!GACC_GLOBAL) {
       float* gacc = (float*)(lds + L::WAVE + w * L::WAVE_BYTES + L::GACC);
       for (int e = lane; e < L::PART; e += 64) gacc[e] = 0.0f;
     } else {
@@ -278,8 +311,9 @@ __global__ void __launch_bounds__(NWV * 64, 1) loss_grad_kernel(TrainParams p) {
   const char* aotr = lds + L::AOT;
   const float* bias = (const float*)(lds + L::BIAS);
   const float* col = (const float*)(lds + L::COL);
-  char* wave_base = lds + L::WAVE + w * L::WAVE_BYTES;
-  float* gacc = GACC_GLOBAL ? p.partials + ((size_t)blockIdx.x * NWV + w) * L::PART : (float*)(wave_base + L::GACC);
+  char* wave_base = lds + L::IMG + L::GP_BYTES + w * L::WAVE_BYTES;
+  float* gacc = L::TURN ? (float*)(lds + L::IMG)
+                        : (GACC_GLOBAL ? p.partials + ((size_t)blockIdx.x * NWV + w) * L::PART : (float*)(wave_base + L::GACC));
   __bf16* scr = (__bf16*)(wave_base + L::SCR);
   auto S_ = [&](int k) { return scr + k * W * RS; };
 
@@ -292,7 +326,11 @@ __global__ void __launch_bounds__(NWV * 64, 1) loss_grad_kernel(TrainParams p) {
   float lsum[3] = {0.0f, 0.0f, 0.0f};  // DSM, IC, PDE row sums (lane group 0 only)
 
   const long long n_tiles = (p.n + NS - 1) / NS;
-  for (long long tile = (long long)blockIdx.x * NWV + w; tile < n_tiles; tile += (long long)gridDim.x * NWV) {
+  // TURN: every wave of the workgroup runs the same rounds (a wave past the end runs an all-invalid tile),
+  // so the turn barriers match
+  for (long long tile0 = (long long)blockIdx.x * NWV + (L::TURN ? 0 : w); tile0 < n_tiles;
+       tile0 += (long long)gridDim.x * NWV) {
+    const long long tile = tile0 + (L::TURN ? w : 0);
     const long long si = tile * NS + c16;
     const bool valid = si < p.n;
     // ---------------------------------------------------------------- per-sample inputs
@@ -333,6 +371,19 @@ __global__ void __launch_bounds__(NWV * 64, 1) loss_grad_kernel(TrainParams p) {
     uP[IN - 1] = t, uV[IN - 1] = 1.0f, uC[IN - 1] = 0.0f;
     const bf16x8 BP = b1_operand(uP, 1.0f, g), BV = b1_operand(uV, 0.0f, g), BC = b1_operand(uC, 1.0f, g);
 
+    float abP[OUT], abV[OUT], abC[OUT];
+    if constexpr (PH == 2) {  // the forward half's adjoints and loss terms of this sample
+      const float4* rec = (const float4*)(p.adj + (valid ? si : 0) * kTrainAdj);
+      const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2];
+      const bool ok = valid;
+      abP[0] = ok ? r0.x : 0.0f, abP[1] = ok ? r0.y : 0.0f, abV[0] = ok ? r0.z : 0.0f, abV[1] = ok ? r0.w : 0.0f;
+      abC[0] = ok ? r1.x : 0.0f, abC[1] = ok ? r1.y : 0.0f;
+      if (valid && g == 0) {
+        lsum[0] += r1.z;
+        lsum[1] += r1.w;
+        lsum[2] += r2.x;
+      }
+    } else {
     // ======================================================== pass F: forward with jets
     float aS[NSTREAM][OUT];
     {
@@ -413,7 +464,6 @@ __global__ void __launch_bounds__(NWV * 64, 1) loss_grad_kernel(TrainParams p) {
     }
 
     // ======================================================== per-sample loss terms and adjoints
-    float abP[OUT], abV[OUT], abC[OUT];
     {
       float s[OUT], dLds[OUT];
 #pragma unroll
@@ -502,8 +552,16 @@ __global__ void __launch_bounds__(NWV * 64, 1) loss_grad_kernel(TrainParams p) {
         lsum[0] += dsm;
         lsum[1] += ic;
         lsum[2] += pde;
+        if constexpr (PH == 1) {
+          float4* rec = (float4*)(p.adj + si * kTrainAdj);
+          rec[0] = make_float4(abP[0], abP[1], abV[0], abV[1]);
+          rec[1] = make_float4(abC[0], abC[1], dsm, ic);
+          rec[2] = make_float4(pde, 0.0f, 0.0f, 0.0f);
+        }
       }
     }
+    }  // PH != 2
+    if constexpr (PH == 1) continue;
 
     // ======================================================== pass B: reverse with recomputation
     f32x4 hbar[3][4];  // adjoint of the current layer's output, streams P, V, C (acc form)
@@ -545,7 +603,7 @@ __global__ void __launch_bounds__(NWV * 64, 1) loss_grad_kernel(TrainParams p) {
           for (int S = 0; S < 3; ++S) pack_b2(Hf[S], H[S], HL[S]);
           if (l == li) {
 #pragma unroll
-            for (int S = 0; S < 3; ++S) put_t(S_(3 + S), Hf[S], g, c16);
+            for (int S = 0; S < 3; ++S) put_t<RS>(S_(3 + S), Hf[S], g, c16);
           }
           if (l == NL) break;  // li == NL: the output layer's pre-activation is not needed
           const char* wl = wfr + (l - 1) * 8192;
@@ -576,18 +634,35 @@ __global__ void __launch_bounds__(NWV * 64, 1) loss_grad_kernel(TrainParams p) {
         }
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's scratch writes landed
         __builtin_amdgcn_wave_barrier();
+        float go[2][OUT];  // TURN: this tile's output-layer gradient, added in turns
 #pragma unroll
         for (int U = 0; U < 2; ++U) {
           f32x16 acc{};
 #pragma unroll
           for (int S = 0; S < 3; ++S) {
-            const bf16x8 A = tread(S_(S), i32, i32 < OUT, hh);
-            const bf16x8 Bm = tread(S_(3 + S), 32 * U + i32, true, hh);
+            const bf16x8 A = tread<RS>(S_(S), i32, i32 < OUT, hh);
+            const bf16x8 Bm = tread<RS>(S_(3 + S), 32 * U + i32, true, hh);
             acc = mfma32(A, Bm, acc);
           }
-          if (hh == 0) {
+          if constexpr (L::TURN) {
 #pragma unroll
-            for (int o = 0; o < OUT; ++o) gadd(&gacc[L::p_w(NL) + o * W + 32 * U + i32], acc[o]);
+            for (int o = 0; o < OUT; ++o) go[U][o] = acc[o];
+          } else if (hh == 0) {
+#pragma unroll
+            for (int o = 0; o < OUT; ++o) gadd<GACC_GLOBAL>(&gacc[L::p_w(NL) + o * W + 32 * U + i32], acc[o]);
+          }
+        }
+        if constexpr (L::TURN) {  // sub-block (U, o) = ((w + k) % 4) / 2, ((w + k) % 4) % 2 at turn k
+          static_assert(OUT == 2, "four (U, o) sub-blocks, one per wave and turn");
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int sb = (w + k) & 3;
+            turn_barrier();
+            if (hh == 0) {
+#pragma unroll
+              for (int q = 0; q < 4; ++q)
+                if (sb == q) gacc[L::p_w(NL) + (q & 1) * W + 32 * (q >> 1) + i32] += go[q >> 1][q & 1];
+            }
           }
         }
 #pragma unroll
@@ -628,7 +703,7 @@ __global__ void __launch_bounds__(NWV * 64, 1) loss_grad_kernel(TrainParams p) {
           zb[2][R][r] = d1c * hbar[2][R][r];
         }
 #pragma unroll
-      for (int S = 0; S < 3; ++S) put_t(S_(S), zb[S], g, c16);
+      for (int S = 0; S < 3; ++S) put_t<RS>(S_(S), zb[S], g, c16);
       if (li == 0) {
         // layer-1 inputs transposed: rows 0..IN-1 = u, row IN = the bias column (1 for P and C)
         if (g == 0) {
@@ -647,39 +722,77 @@ __global__ void __launch_bounds__(NWV * 64, 1) loss_grad_kernel(TrainParams p) {
       __builtin_amdgcn_s_waitcnt(0xc07f);
       __builtin_amdgcn_wave_barrier();
       if (li == 0) {
+        f32x16 a0[2];
 #pragma unroll
         for (int T = 0; T < 2; ++T) {
           f32x16 acc{};
 #pragma unroll
           for (int S = 0; S < 3; ++S) {
-            const bf16x8 A = tread(S_(S), 32 * T + i32, true, hh);
-            const bf16x8 Bm = tread(S_(3 + S), i32, i32 <= IN, hh);
+            const bf16x8 A = tread<RS>(S_(S), 32 * T + i32, true, hh);
+            const bf16x8 Bm = tread<RS>(S_(3 + S), i32, i32 <= IN, hh);
             acc = mfma32(A, Bm, acc);
           }
+          if constexpr (L::TURN) {
+            a0[T] = acc;
+          } else {
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int row = 32 * T + (r & 3) + 8 * (r >> 2) + 4 * hh;
-            if (i32 < IN) gadd(&gacc[L::p_w(0) + row * IN + i32], acc[r]);
-            else if (i32 == IN) gadd(&gacc[L::p_b(0) + row], acc[r]);
+            for (int r = 0; r < 16; ++r) {
+              const int row = 32 * T + (r & 3) + 8 * (r >> 2) + 4 * hh;
+              if (i32 < IN) gadd<GACC_GLOBAL>(&gacc[L::p_w(0) + row * IN + i32], acc[r]);
+              else if (i32 == IN) gadd<GACC_GLOBAL>(&gacc[L::p_b(0) + row], acc[r]);
+            }
+          }
+        }
+        if constexpr (L::TURN) {  // sub-block (T, half) = ((w + k) % 4) / 2, % 2: accumulator registers 8 half .. + 7
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int sb = (w + k) & 3;
+            turn_barrier();
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              if (sb != q) continue;
+#pragma unroll
+              for (int r = 8 * (q & 1); r < 8 * (q & 1) + 8; ++r) {
+                const int row = 32 * (q >> 1) + (r & 3) + 8 * (r >> 2) + 4 * hh;
+                if (i32 < IN) gacc[L::p_w(0) + row * IN + i32] += a0[q >> 1][r];
+                else if (i32 == IN) gacc[L::p_b(0) + row] += a0[q >> 1][r];
+              }
+            }
           }
         }
       } else {
         const int pw = L::p_w(li);
+        if constexpr (L::TURN) {  // block (T, U) = ((w + k) % 4) / 2, % 2 at turn k: its MFMAs, then its adds
 #pragma unroll
-        for (int T = 0; T < 2; ++T)
+          for (int k = 0; k < 4; ++k) {
+            const int sb = (w + k) & 3, T = sb >> 1, U = sb & 1;
+            f32x16 acc{};
+#pragma unroll
+            for (int S = 0; S < 3; ++S) {
+              const bf16x8 A = tread<RS>(S_(S), 32 * T + i32, true, hh);
+              const bf16x8 Bm = tread<RS>(S_(3 + S), 32 * U + i32, true, hh);
+              acc = mfma32(A, Bm, acc);
+            }
+            turn_barrier();
+#pragma unroll
+            for (int r = 0; r < 16; ++r) gacc[pw + (32 * T + (r & 3) + 8 * (r >> 2) + 4 * hh) * W + 32 * U + i32] += acc[r];
+          }
+        }
+#pragma unroll
+        for (int T = 0; T < 2 && !L::TURN; ++T)
 #pragma unroll
           for (int U = 0; U < 2; ++U) {
             f32x16 acc{};
 #pragma unroll
             for (int S = 0; S < 3; ++S) {
-              const bf16x8 A = tread(S_(S), 32 * T + i32, true, hh);
-              const bf16x8 Bm = tread(S_(3 + S), 32 * U + i32, true, hh);
+              const bf16x8 A = tread<RS>(S_(S), 32 * T + i32, true, hh);
+              const bf16x8 Bm = tread<RS>(S_(3 + S), 32 * U + i32, true, hh);
               acc = mfma32(A, Bm, acc);
             }
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
               const int row = 32 * T + (r & 3) + 8 * (r >> 2) + 4 * hh;
-              gadd(&gacc[pw + row * W + 32 * U + i32], acc[r]);
+              gadd<GACC_GLOBAL>(&gacc[pw + row * W + 32 * U + i32], acc[r]);
             }
           }
         // h-bar of layer li-1 = W_li^T zbar
@@ -700,7 +813,14 @@ __global__ void __launch_bounds__(NWV * 64, 1) loss_grad_kernel(TrainParams p) {
     }
   }
 
-  // ---- flush: bias partials (reduce the 16 sample lanes of each lane group) and loss sums
+  if constexpr (PH == 1) return;  // the forward half: its adjoints and loss terms are in p.adj
+  // ---- flush: bias partials (reduce the 16 sample lanes of each lane group) and loss sums; TURN: one wave
+  // at a time into the workgroup's LDS partial (wave order), then the partial to its row in global memory
+  for (int turn = 0; turn < (L::TURN ? NWV : 1); ++turn) {
+    if constexpr (L::TURN) {
+      turn_barrier();
+      if (w != turn) continue;
+    }
 #pragma unroll
   for (int l = 0; l < NL - 1; ++l)
 #pragma unroll
@@ -710,21 +830,31 @@ __global__ void __launch_bounds__(NWV * 64, 1) loss_grad_kernel(TrainParams p) {
         float v = bbar[l][R][r];
 #pragma unroll
         for (int m = 1; m < 16; m <<= 1) v += __shfl_xor(v, m, 64);
-        if (c16 == 0) gadd(&gacc[L::p_b(l + 1) + 16 * R + 4 * g + r], v);
+        if (c16 == 0) gadd<GACC_GLOBAL>(&gacc[L::p_b(l + 1) + 16 * R + 4 * g + r], v);
       }
 #pragma unroll
   for (int o = 0; o < OUT; ++o) {
     float v = g == 0 ? bobar[o] : 0.0f;
 #pragma unroll
     for (int m = 1; m < 64; m <<= 1) v += __shfl_xor(v, m, 64);
-    if (lane == 0) gadd(&gacc[L::p_b(NL) + o], v);
+    if (lane == 0) gadd<GACC_GLOBAL>(&gacc[L::p_b(NL) + o], v);
   }
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     float v = lsum[k];
 #pragma unroll
     for (int m = 1; m < 64; m <<= 1) v += __shfl_xor(v, m, 64);
-    if (lane == 0) gacc[L::NPARAM + k] = v;
+    if (lane == 0) {
+      if constexpr (L::TURN) gacc[L::NPARAM + k] += v;
+      else gacc[L::NPARAM + k] = v;
+    }
+  }
+  }  // turns
+  if constexpr (L::TURN) {
+    turn_barrier();
+    float* row = p.partials + (size_t)blockIdx.x * L::PART;
+    for (int e = tid; e < L::PART; e += NWV * 64) row[e] = gacc[e];
+    return;
   }
   if constexpr (GACC_GLOBAL) {
     // fold the workgroup's NWV rows into its first row, in wave order (deterministic), so the
@@ -745,11 +875,11 @@ __global__ void __launch_bounds__(NWV * 64, 1) loss_grad_kernel(TrainParams p) {
   // one partial per workgroup: wave 0's region + wave 1's region, in that order (deterministic)
   __syncthreads();
   float* part = p.partials + (size_t)blockIdx.x * L::PART;
-  const float* g0 = (const float*)(lds + L::WAVE + L::GACC);
+  const float* g0 = (const float*)(lds + L::IMG + L::GACC);
   for (int e = tid; e < L::PART; e += NWV * 64) {
     float v = g0[e];
 #pragma unroll
-    for (int ww = 1; ww < NWV; ++ww) v += ((const float*)(lds + L::WAVE + ww * L::WAVE_BYTES + L::GACC))[e];
+    for (int ww = 1; ww < NWV; ++ww) v += ((const float*)(lds + L::IMG + ww * L::WAVE_BYTES + L::GACC))[e];
     part[e] = v;
   }
 }
@@ -786,6 +916,16 @@ __global__ void loss_total_kernel(float* loss_out, int has_dsm, int has_ic, int 
 
 }  // namespace train
 
+// the forward / reverse split (two kernels at two waves per SIMD) or the fused one-wave-per-SIMD kernel;
+// DMIP_TRAIN_SPLIT=0 selects the fused kernel (A/B knob, read once per process)
+bool train_split() {
+  static const bool v = [] {
+    const char* e = getenv("DMIP_TRAIN_SPLIT");
+    return e ? atoi(e) != 0 : true;
+  }();
+  return v;
+}
+
 int train_nparam(int n_hidden) {
   return n_hidden == 3 ? train::TL<3>::NPARAM : (n_hidden == 2 ? train::TL<2>::NPARAM : -1);
 }
@@ -803,10 +943,23 @@ hipError_t launch_loss_grad(const TrainParams& p, int n_hidden, float* grads, fl
     hipLaunchKernelGGL(train_pack_kernel<2>, dim3(32), dim3(256), 0, st, q);
   hipError_t e0 = hipGetLastError();
   if (e0 != hipSuccess) return e0;
-  if (n_hidden == 3)
+  if (train_split()) {
+    // forward half: 4-wave workgroups, two per CU (two waves per SIMD); reverse half: the caller's n_wg
+    if (!q.adj) return hipErrorInvalidValue;
+    const long long tiles = (p.n + NS - 1) / NS;
+    const long long g1 = std::min<long long>(2LL * n_wg, (tiles + 3) / 4);
+    if (n_hidden == 3) {
+      hipLaunchKernelGGL((loss_grad_kernel<3, 1>), dim3((unsigned)g1), dim3(TL<3, 1>::NW * 64), 0, st, q);
+      hipLaunchKernelGGL((loss_grad_kernel<3, 2>), dim3(n_wg), dim3(TL<3, 2>::NW * 64), 0, st, q);
+    } else {
+      hipLaunchKernelGGL((loss_grad_kernel<2, 1>), dim3((unsigned)g1), dim3(TL<2, 1>::NW * 64), 0, st, q);
+      hipLaunchKernelGGL((loss_grad_kernel<2, 2>), dim3(n_wg), dim3(TL<2, 2>::NW * 64), 0, st, q);
+    }
+  } else if (n_hidden == 3) {
     hipLaunchKernelGGL(loss_grad_kernel<3>, dim3(n_wg), dim3(NWV * 64), 0, st, q);
-  else
+  } else {
     hipLaunchKernelGGL(loss_grad_kernel<2>, dim3(n_wg), dim3(NWV * 64), 0, st, q);
+  }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(loss_grad_reduce_kernel, dim3((nparam + 3 + 63) / 64), dim3(256), 0, st, partials, n_wg,
@@ -820,7 +973,8 @@ hipError_t launch_loss_grad(const TrainParams& p, int n_hidden, float* grads, fl
 
 int train_partial_stride(int n_hidden) { return n_hidden == 3 ? train::TL<3>::PART : train::TL<2>::PART; }
 int train_packed_bytes(int n_hidden) { return n_hidden == 3 ? train::TL<3>::WAVE : train::TL<2>::WAVE; }
-int train_partials_per_wg() { return train::GACC_GLOBAL ? train::NWV : 1; }
-int train_waves_per_wg() { return train::NWV; }
+int train_partials_per_wg() { return train_split() ? 1 : (train::GACC_GLOBAL ? train::NWV : 1); }
+int train_waves_per_wg() { return train_split() ? train::TL<3, 2>::NW : train::NWV; }
+size_t train_adj_bytes(long long batch) { return train_split() ? (size_t)batch * kTrainAdj * sizeof(float) : 0; }
 
 }  // namespace dmip
