@@ -407,9 +407,9 @@ def _rel(a, b):
 @pytest.mark.parametrize("name", list(_LOSS_CFGS))
 def test_fused_loss_grad_vs_reference_fixture(dmip, golden, name):
     """dmip_loss_grad on the reference's G5 batch (trained linear CDE, 256 samples) against the
-    reference autograd values and gradients. Tolerance: bf16 MFMA operands with fp32 accumulation
-    through 4 layers and second-order jets -> loss within 1 %, each gradient tensor within 3 %
-    relative L2 error."""
+    reference autograd values and gradients. bf16 MFMA operands (split-bf16 primal streams) with fp32
+    accumulation through 4 layers and second-order jets. Bounds about 2-3x the measured error (round 3:
+    loss <= 3.0e-5 relative, every gradient tensor <= 4.5e-3 relative L2)."""
     z = golden("pinn_linear.npz")
     m = dmip.CDE(2, 2, [64] * 3)
     m.sde.a.load_state_dict(state_from_npz(golden("ckpt_lin.npz")))
@@ -419,22 +419,25 @@ def test_fused_loss_grad_vs_reference_fixture(dmip, golden, name):
     ref_grads = [z[f"{name}_grad_{k}"] for k in ("0_weight", "0_bias", "3_weight", "3_bias", "5_weight", "5_bias",
                                                  "7_weight", "7_bias")]
     if name != "dsm":
-        assert loss == pytest.approx(float(z[f"{name}_loss"]), rel=1e-2)
-        assert info["PDE-Loss"] == pytest.approx(float(z[f"{name}_PDE_Loss"]), rel=2e-2)
+        assert loss == pytest.approx(float(z[f"{name}_loss"]), rel=1e-4)
+        pde_ref = float(z[f"{name}_PDE_Loss"])
+        _report(f"G5 {name}: PDE-Loss rel", abs(info["PDE-Loss"] - pde_ref) / abs(pde_ref))
+        assert info["PDE-Loss"] == pytest.approx(pde_ref, rel=2e-2)
     else:
-        assert loss == pytest.approx(float(z["dsm_rows"].mean()), rel=1e-2)
+        assert loss == pytest.approx(float(z["dsm_rows"].mean()), rel=1e-4)
     errs = [_rel(g, r) for g, r in zip(grads, ref_grads)]
     _report(f"G5 {name}: loss rel", abs(loss - (float(z[f"{name}_loss"]) if name != "dsm" else float(z["dsm_rows"].mean())))
             / abs(float(z[f"{name}_loss"]) if name != "dsm" else float(z["dsm_rows"].mean())))
     _report(f"G5 {name}: max grad rel L2", max(errs))
-    assert max(errs) < 3e-2, errs
+    assert max(errs) < 1e-2, errs
 
 
 @pytest.mark.parametrize("name", ["pinn", "pinn_l1l2", "dsm", "pinn_cfpe"])
 @pytest.mark.parametrize("NL", [2, 3])
 def test_fused_loss_grad_vs_oracle_ragged(dmip, name, NL):
     """A ragged batch (5003 samples: not a multiple of the 16-sample tile nor of the waves) of a
-    seeded untrained net against oracle.loss_grad (float64), same tolerance as above."""
+    seeded untrained net against oracle.loss_grad (float64). Bounds about 3x the measured error (round 3:
+    loss <= 6.7e-6 relative, gradients <= 3.4e-3 relative L2)."""
     torch.manual_seed(NL)
     m = dmip.CDE(2, 2, [64] * NL)
     params = [(l.weight.detach().cpu().numpy(), l.bias.detach().cpu().numpy())
@@ -451,12 +454,12 @@ def test_fused_loss_grad_vs_oracle_ragged(dmip, name, NL):
                                *[torch.from_numpy(a).to(dev) for a in (x, y, t, eps)])
     ref_loss, comps, ref = O.loss_grad(params, x, y, t, eps, **_LOSS_CFGS[name], ic_A=[[1, 0.5], [0, 1]],
                                        ic_b=[0.3, 0.5], ic_Sinv=np.eye(2) / 0.3)
-    assert loss == pytest.approx(ref_loss, rel=1e-2)
+    assert loss == pytest.approx(ref_loss, rel=3e-5)
     flat_ref = [a for wb in ref for a in wb]
     errs = [_rel(gk, rk) for gk, rk in zip(grads, flat_ref)]
     _report(f"ragged NL={NL} {name}: loss rel", abs(loss - ref_loss) / abs(ref_loss))
     _report(f"ragged NL={NL} {name}: max grad rel L2", max(errs))
-    assert max(errs) < 3e-2, errs
+    assert max(errs) < 8e-3, errs
 
 
 def _config5_batch(n=65536, seed=2024):
