@@ -1,12 +1,12 @@
-"""The k-major multi-tile fp32x3 CDE engine (csrc/dmip_x3k.h: one wave per SIMD with 2 or 3 chain tiles,
-static weight ring, resident merged output layer) -- the default path of `CDE.sample_device` at the
-headline shape (hidden_layers [256]*3). Needs an MI355X: `pytest -m gpu`.
+"""The 32x32-tile k-major fp32x3 CDE engine (csrc/dmip_x3w.h: one wave per SIMD with one 32-chain tile,
+v_mfma_f32_32x32x16_f16, static weight ring, resident layer 1 and merged output layer) -- the default
+path of `CDE.sample_device` at the headline shape (hidden_layers [256]*3). Needs an MI355X: `pytest -m gpu`.
 
 Gates (the fp32 engines' own, test_gpu_x3.py): the float32 oracle on the same chains within 1e-4 of
-max(1, |x|); the one-tile fp32x3 engine (DMIP_X3K=0; identical hidden-layer arithmetic, the output
-layer's three partial sums added in another order) within 1e-5 after 1000 steps; chain results
-independent of the tiles per wave (bit-identical), of sharding and of the balanced schedule's
-hand-overs; the reference's draws through test_gpu_x3.py's parity gate (same entry point).
+max(1, |x|); the 16x16 k-major engine (DMIP_X3W=0: the same three-product arithmetic, its MFMAs summing
+in another order) within 3e-5 after 1000 steps; chain results independent of sharding and of the
+balanced schedule's hand-overs (bit-identical); snapshots; the reference's injected-noise trajectories
+and draws through test_gpu_x3.py's gates (same entry point).
 """
 import numpy as np
 import pytest
@@ -27,12 +27,6 @@ def _need_gpu():
         pytest.skip("no HIP device")
 
 
-@pytest.fixture(autouse=True)
-def _x3k_engine(monkeypatch):
-    """At its shape the 32x32-tile engine (dmip_x3w.h) is the default; these tests pin the 16x16 one."""
-    monkeypatch.setenv("DMIP_X3W", "0")
-
-
 def _params(net):
     return [(l.weight.detach().cpu().numpy(), l.bias.detach().cpu().numpy())
             for l in net if isinstance(l, torch.nn.Linear)]
@@ -47,60 +41,74 @@ def _seeded(dmip, xd, yd, seed):
     return dmip.CDE(xd, yd, [256] * 3)
 
 
+def test_x3w_is_the_default_at_its_shape(dmip):
+    """The headline shape runs the 32x32 engine (its launch counter), with no fallback."""
+    m = _seeded(dmip, 3, 23, 1)
+    y = torch.rand(23, device=DEV)
+    before = dmip._lib.calls.get("em_sample", 0)
+    x = m.sample_device(y, 100, 3, seed=1, precision=PREC)
+    assert dmip._lib.calls.get("em_sample", 0) == before + 1
+    assert torch.isfinite(x).all()
+
+
 @pytest.mark.parametrize("xd,yd", [(2, 2), (3, 23)])
-@pytest.mark.parametrize("n", [1, 15, 47, 49, 97, 1000])
-def test_x3k_vs_oracle_ragged(dmip, xd, yd, n):
-    """Chain counts that leave the last job (3 x 16 chains) partial or a tile partly empty."""
-    m = _seeded(dmip, xd, yd, 3 + n)
+@pytest.mark.parametrize("n", [1, 31, 33, 63, 65, 1000])
+def test_x3w_vs_oracle_ragged(dmip, xd, yd, n):
+    """Chain counts that leave the last 32-chain job partial."""
+    m = _seeded(dmip, xd, yd, 5 + n)
     y = np.random.default_rng(n).uniform(0, 1, yd).astype(np.float32)
-    S, seed = 6, 41
+    S, seed = 6, 43
     x = m.sample_device(torch.from_numpy(y).to(DEV), n, S, seed=seed, precision=PREC)[0].cpu().numpy()
     ref = O.cde_sample(_params(m.sde.a), y, n, S, seed)
     assert np.all(np.isfinite(x))
     e = _rel(x, ref)
-    print(f"\n[x3k] oracle xd={xd} n={n}: {e:.3e}")
+    print(f"\n[x3w] oracle xd={xd} n={n}: {e:.3e}")
     assert e < 1e-4, e
 
 
 @pytest.mark.parametrize("tag", ["scat", "lin256"])
-def test_x3k_matches_one_tile_engine_over_1000_steps(dmip, golden, tag, monkeypatch):
-    """Same chains through both fp32x3 engines: the hidden layers are bit-identical, the output layer's
-    partial sums are added in another order (~1 ulp per step), over 1000 contracting steps."""
+def test_x3w_matches_x3k_over_1000_steps(dmip, golden, tag, monkeypatch):
+    """Same chains through the 32x32 and the 16x16 k-major engines (same products, MFMA sums in another
+    order), over 1000 contracting steps."""
     if tag == "scat":
         m = dmip.CDE(3, 23, [256] * 3)
         m.sde.a.load_state_dict(state_from_npz(golden("ckpt_scat.npz")))
         y = torch.from_numpy(golden("samples_scat.npz")["y"]).to(DEV)
     else:
-        m = _seeded(dmip, 2, 2, 77)
+        m = _seeded(dmip, 2, 2, 79)
         y = torch.tensor([0.5, 1.0], device=DEV)
     a = m.sample_device(y, 20000, 1000, seed=321, precision=PREC)[0].cpu().numpy()
-    monkeypatch.setenv("DMIP_X3K", "0")
+    monkeypatch.setenv("DMIP_X3W", "0")
     b = m.sample_device(y, 20000, 1000, seed=321, precision=PREC)[0].cpu().numpy()
-    monkeypatch.delenv("DMIP_X3K")
+    monkeypatch.delenv("DMIP_X3W")
     assert np.all(np.isfinite(a))
     e = _rel(a, b)
-    print(f"\n[x3k] vs one-tile engine, {tag}, 1000 steps: {e:.3e}")
-    assert e < 1e-5, e
-    assert not np.array_equal(a, b)  # two engines ran (the output layer's summation order differs)
+    print(f"\n[x3w] vs x3k, {tag}, 1000 steps: {e:.3e}")
+    assert e < 3e-5, e
+    assert not np.array_equal(a, b)  # two engines ran
 
 
-def test_x3k_tiles_per_wave_bit_identical(dmip, monkeypatch):
-    """2 or 3 chain tiles per wave: a chain's arithmetic does not depend on its neighbours."""
-    m = _seeded(dmip, 3, 23, 5)
-    ys = torch.from_numpy(np.random.default_rng(3).uniform(0, 1, (2, 23)).astype(np.float32)).to(DEV)
-    monkeypatch.setenv("DMIP_X3K_NT", "2")
-    a = m.sample_device(ys, 70001, 8, seed=9, precision=PREC)
-    monkeypatch.setenv("DMIP_X3K_NT", "3")
-    b = m.sample_device(ys, 70001, 8, seed=9, precision=PREC)
-    assert torch.isfinite(a).all()
-    assert torch.equal(a, b)
+def test_x3w_injected_noise_matches_reference(dmip, golden):
+    """The reference's own x0 and per-step noise (G3, scatterometry, 1000 steps) through the 32x32
+    engine: within the fp32 gate 1e-3 max|x|."""
+    tr = golden("traj_scat.npz")
+    m = dmip.CDE(3, 23, [256] * 3)
+    m.sde.a.load_state_dict(state_from_npz(golden("ckpt_scat.npz")))
+    S = int(tr["num_steps"])
+    noise = np.concatenate([tr["x0"][None], tr["xi"]], 0)[:, None]
+    n = tr["x0"].shape[0]
+    out = m.sample_device(torch.from_numpy(tr["y"]).to(DEV), n, S, noise=torch.from_numpy(noise).to(DEV),
+                          precision=PREC)[0].cpu().numpy()
+    ref = tr["x_final"]
+    assert np.all(np.isfinite(out))
+    e = _rel(out, ref)
+    print(f"\n[x3w] G3 scat: {S} steps, max err / max|x| = {e:.3e}")
+    assert e < 1e-3, e
 
 
-@pytest.mark.parametrize("nt", ["2", "3"])
-def test_x3k_balanced_schedule_and_shards(dmip, monkeypatch, nt):
-    """More jobs than waves (hand-overs of 2-3 tiles of state) and two ys: every chain equals a launch
-    small enough to run whole, and a chain_offset shard is a slice of the whole run."""
-    monkeypatch.setenv("DMIP_X3K_NT", nt)
+def test_x3w_balanced_schedule_and_shards(dmip):
+    """More jobs than waves (hand-overs) and two ys: every chain equals a launch small enough to run
+    whole, and a chain_offset shard is a slice of the whole run."""
     m = _seeded(dmip, 3, 23, 6)
     ys = torch.from_numpy(np.random.default_rng(4).uniform(0, 1, (2, 23)).astype(np.float32)).to(DEV)
     n, S = 150001, 5
@@ -111,9 +119,8 @@ def test_x3k_balanced_schedule_and_shards(dmip, monkeypatch, nt):
     assert torch.isfinite(full).all()
 
 
-def test_x3k_snapshots(dmip):
-    """Trajectory snapshots through the multi-tile engine: last = output, shard slices, the oracle's
-    loop states."""
+def test_x3w_snapshots(dmip):
+    """Trajectory snapshots: last = output, shard slices, the oracle's loop states."""
     m = _seeded(dmip, 3, 23, 8)
     y = torch.from_numpy(np.random.default_rng(6).uniform(0, 1, (2, 23)).astype(np.float32)).to(DEV)
     n, S, every, seed = 90000, 24, 6, 7
