@@ -189,16 +189,12 @@ struct dmip_mlp {
   // the k-major engine's images (dmip_x3k.h; width 256, 3 hidden layers, xdim <= 4)
   char* x3k_stream = nullptr;     // [2 layers][8 k-steps][16 tiles][hi, lo][64][8] fp16
   char* x3k_out = nullptr;        // [8 k-steps][64][8]: rows 0..xdim-1 W_hi, rows 4..4+xdim-1 W_lo
-  // the 32x32-tile engine's images (dmip_x3w.h; same shapes)
-  char* x3w_stream = nullptr;     // [2 layers][8 input tiles][8 output tiles][2 halves][hi, lo][64][8] fp16
-  char* x3w_l1 = nullptr;         // [8 tiles][64][8]
-  char* x3w_out = nullptr;        // [16 k-steps][64][8]
   ~dmip_mlp() {
     for (void* p : {(void*)ring_l1, (void*)hidden, (void*)ao_samp, (void*)ao_full, (void*)bias_hidden, (void*)bias_out_samp,
                     (void*)bias_out_full, (void*)a1_full, (void*)w1, (void*)b1, (void*)dps_l1, (void*)dps_w2,
                     (void*)dps_w3, (void*)dps_w4, (void*)dps_bias, (void*)f32_l1, (void*)f32_stream,
                     (void*)f32_bias, (void*)x3_l1, (void*)x3_l1_full, (void*)x3_stream, (void*)x3_bias,
-                    (void*)x3k_stream, (void*)x3k_out, (void*)x3w_stream, (void*)x3w_l1, (void*)x3w_out})
+                    (void*)x3k_stream, (void*)x3k_out})
       if (p) (void)hipFree(p);
   }
 };
@@ -245,9 +241,6 @@ dmip::F32Net f32_net(const dmip_mlp* n) { return dmip::F32Net{n->f32_l1, n->f32_
 // lane l = i + 16 g holds A[row i][k-slot 8 g + m], m = 0..7. Hidden-layer k-slots follow the previous
 // layer's accumulator tiles: slot (q, g, m) is unit kperm16(q, g, m).
 inline int kperm16(int q, int g, int m) { return 32 * q + 16 * (m >> 2) + 4 * g + (m & 3); }
-// 32x32x16 fragments (dmip_x3w.h): lane l = i + 32 h holds A[row i][k-slot 8 h + j]; k-step s of a hidden
-// layer covers the previous layer's accumulator registers 8 (s & 1) .. + 7 of its output tile s >> 1
-inline int kperm32(int s, int h, int j) { return 32 * (s >> 1) + 16 * (s & 1) + 8 * (j >> 2) + 4 * h + (j & 3); }
 inline int x3_k1q(int nv) { return (3 * nv + 31) / 32; }
 
 // v = hi + lo in fp16 (hi = fp16(v), lo = fp16(v - hi))
@@ -299,69 +292,6 @@ void pack_x3_layer(const float* Wl, const float* bl, int n_rows, int W, int n_ti
             const size_t src = (size_t)row * W + kperm16(q, l >> 4, m);
             img[((((size_t)o * KQ + q) * 2 + p) * 64 + l) * 8 + m] = p == 0 ? hi[src] : lo[src];
           }
-}
-
-// the 32x32-tile engine's images (dmip_x3w.h) of the [256]*3 CDE: the same hi / lo split and folded
-// scales as pack_x3_layer / pack_x3_l1, in the 32x32x16 fragment layout
-int pack_x3w(dmip_mlp* net, const float* const* weights, const float* const* biases) {
-  const int W = net->width, L = net->n_hidden, IN = net->in_dim, D = net->xdim;
-  const int OT = W / 32, KS = W / 16;
-  std::vector<uint16_t> l1((size_t)OT * 512, 0);
-  std::vector<int> cols;
-  for (int k = 0; k < D; ++k) cols.push_back(k);
-  cols.push_back(IN - 1);
-  const int NV = (int)cols.size();
-  for (int o = 0; o < OT; ++o)
-    for (int l = 0; l < 64; ++l)
-      for (int j = 0; j < 8; ++j) {
-        const int i = l & 31, h = l >> 5, sl = 8 * h + j, n = sl / 3, pt = sl % 3;
-        if (n >= NV) continue;
-        uint16_t hi, lo;
-        split_h(kC * (double)weights[0][(size_t)(32 * o + i) * IN + cols[n]], hi, lo);
-        l1[((size_t)o * 64 + l) * 8 + j] = pt < 2 ? hi : lo;
-      }
-  std::vector<char> stream;
-  std::vector<uint16_t> hi((size_t)W * W), lo((size_t)W * W);
-  for (int li = 1; li < L; ++li) {
-    for (int r = 0; r < W; ++r)
-      for (int k = 0; k < W; ++k)
-        split_h(-2.0 * kC * (double)weights[li][(size_t)r * W + k], hi[(size_t)r * W + k], lo[(size_t)r * W + k]);
-    std::vector<uint16_t> img((size_t)OT * KS * 2 * 512);
-    size_t at = 0;
-    for (int q = 0; q < OT; ++q)           // input tile (chunk)
-      for (int o = 0; o < OT; ++o)         // output tile
-        for (int e = 0; e < 2; ++e)        // k-step half: s = 2 q + e
-          for (int pt = 0; pt < 2; ++pt)   // hi, lo
-            for (int l = 0; l < 64; ++l)
-              for (int j = 0; j < 8; ++j) {
-                const size_t src = (size_t)(32 * o + (l & 31)) * W + kperm32(2 * q + e, l >> 5, j);
-                img[at++] = pt == 0 ? hi[src] : lo[src];
-              }
-    const char* b = (const char*)img.data();
-    stream.insert(stream.end(), b, b + img.size() * 2);
-  }
-  // output layer: scale 1 (its input is r-form: A = -2 W, the init folded by pack_x3_layer)
-  std::vector<uint16_t> out((size_t)KS * 512, 0);
-  for (int s = 0; s < KS; ++s)
-    for (int l = 0; l < 64; ++l) {
-      const int i = l & 31, h = l >> 5;
-      int row = -1, pt = 0;
-      if (i < D) row = i, pt = 0;
-      else if (i >= 4 && i < 4 + D) row = i - 4, pt = 1;
-      if (row < 0) continue;
-      for (int j = 0; j < 8; ++j) {
-        uint16_t vh, vl;
-        split_h(-2.0 * (double)weights[L][(size_t)row * W + kperm32(s, h, j)], vh, vl);
-        out[((size_t)s * 64 + l) * 8 + j] = pt == 0 ? vh : vl;
-      }
-    }
-  std::vector<char> l1b(l1.size() * 2), outb(out.size() * 2);
-  std::memcpy(l1b.data(), l1.data(), l1b.size());
-  std::memcpy(outb.data(), out.data(), outb.size());
-  int rc = DMIP_OK;
-  if ((rc = upload(&net->x3w_stream, stream)) || (rc = upload(&net->x3w_l1, l1b)) || (rc = upload(&net->x3w_out, outb)))
-    return rc;
-  return DMIP_OK;
 }
 
 int pack_x3_net(dmip_mlp* net, const float* const* weights, const float* const* biases) {
@@ -427,7 +357,6 @@ int pack_x3_net(dmip_mlp* net, const float* const* weights, const float* const* 
     std::vector<char> koutb(kout.size() * 2);
     std::memcpy(koutb.data(), kout.data(), koutb.size());
     if ((rc = upload(&net->x3k_stream, kstream)) || (rc = upload(&net->x3k_out, koutb))) return rc;
-    if ((rc = pack_x3w(net, weights, biases))) return rc;
   }
   return DMIP_OK;
 }
@@ -824,11 +753,6 @@ static bool x3k_enabled() {
   const char* e = getenv("DMIP_X3K");
   return !(e && e[0] == '0');
 }
-// DMIP_X3W=0 selects the 16x16 k-major engine (dmip_x3k.h) instead of the 32x32 one (dmip_x3w.h)
-static bool x3w_enabled() {
-  const char* e = getenv("DMIP_X3W");
-  return !(e && e[0] == '0');
-}
 
 // fp32-accurate split-fp16 samplers (dmip_x3.h): same loop, RNG and sharding as the other engines;
 // arguments already validated by em_sample_impl
@@ -879,15 +803,8 @@ static int em_sample_x3(int mode, const dmip_mlp* net0, const dmip_mlp* net1, co
   p.spin_limit = p.debug_flags ? (1u << 10) : (1u << 22);
   bool ok = false;
   hipError_t e;
-  if (mode == DMIP_SAMPLER_CDE && net0->x3w_stream && dmip::x3w_sampler_supported(mode, net0->width, net0->n_hidden, xdim) &&
-      x3k_enabled() && x3w_enabled()) {
-    // the 32x32-tile k-major engine at its shape (dmip_x3w.h)
-    p.net[0].wstream = net0->x3w_stream;
-    p.net[0].wl1 = net0->x3w_l1;
-    p.net[0].wout = net0->x3w_out;
-    e = dmip::launch_x3w_sampler(p, xdim, a.n_y, st, &ok);
-  } else if (mode == DMIP_SAMPLER_CDE && net0->x3k_stream &&
-             dmip::x3k_sampler_supported(mode, net0->width, net0->n_hidden, xdim) && x3k_enabled()) {
+  if (mode == DMIP_SAMPLER_CDE && net0->x3k_stream && dmip::x3k_sampler_supported(mode, net0->width, net0->n_hidden, xdim) &&
+      x3k_enabled()) {
     // the k-major multi-tile engine at its shape (dmip_x3k.h)
     p.net[0].kstream = net0->x3k_stream;
     p.net[0].kout = net0->x3k_out;

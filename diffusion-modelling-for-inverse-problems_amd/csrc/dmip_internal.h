@@ -253,12 +253,6 @@ struct X3Net {
   // [hi, lo][64][8] and the output layer as [k-step][64][8] with rows 0..D-1 = W_hi, 4..4+D-1 = W_lo
   const char* kstream = nullptr;
   const char* kout = nullptr;
-  // the 32x32-tile engine (dmip_x3w.h; width 256, 3 hidden layers): W x W layers as [layer][input tile q]
-  // [output tile o][k-step half e][hi, lo][64][8], layer 1 as [8 tiles][64][8], the output layer as
-  // [16 k-steps][64][8] with rows 0..D-1 = W_hi, 4..4+D-1 = W_lo
-  const char* wstream = nullptr;
-  const char* wl1 = nullptr;
-  const char* wout = nullptr;
 };
 
 struct X3SamplerParams {
@@ -297,8 +291,6 @@ bool x3_sampler_supported(int mode, int width, int n_hidden, int xdim, int ydim)
 // the k-major multi-tile engine (dmip_x3k.h): CDE, width 256, 3 hidden layers, xdim 2 or 3
 bool x3k_sampler_supported(int mode, int width, int n_hidden, int xdim);
 hipError_t launch_x3k_sampler(const X3SamplerParams& p, int xdim, int n_y, hipStream_t st, bool* ok);
-bool x3w_sampler_supported(int mode, int width, int n_hidden, int xdim);
-hipError_t launch_x3w_sampler(const X3SamplerParams& p, int xdim, int n_y, hipStream_t st, bool* ok);
 hipError_t launch_x3_bias_prep(const X3BiasPrepParams& p, int n_y, hipStream_t st);
 // geometry of the x3 images (dmip_x3.h Shape) for the host packer
 int x3_chunk_bytes(int width);

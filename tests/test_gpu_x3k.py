@@ -27,12 +27,6 @@ def _need_gpu():
         pytest.skip("no HIP device")
 
 
-@pytest.fixture(autouse=True)
-def _x3k_engine(monkeypatch):
-    """At its shape the 32x32-tile engine (dmip_x3w.h) is the default; these tests pin the 16x16 one."""
-    monkeypatch.setenv("DMIP_X3W", "0")
-
-
 def _params(net):
     return [(l.weight.detach().cpu().numpy(), l.bias.detach().cpu().numpy())
             for l in net if isinstance(l, torch.nn.Linear)]
