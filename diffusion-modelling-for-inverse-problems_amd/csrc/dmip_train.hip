@@ -571,6 +571,10 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
 
     // ======================================================== pass B: reverse with recomputation
     f32x4 hbar[3][4];  // adjoint of the current layer's output, streams P, V, C (acc form)
+    // the reverse half is specialised per layer (every branch on li and the bias-partial index constant);
+    // the fused kernel keeps the loop (its code size)
+    constexpr int kLiUnroll = PH == 2 ? NL + 1 : 1;
+#pragma unroll kLiUnroll
     for (int li = NL; li >= 0; --li) {
       // ---- recompute P, V, C forward: h_{li-1} (B form + transposed into scratch 3..5) and z_li
       bf16x8 H[3][2], HL[3][2];
