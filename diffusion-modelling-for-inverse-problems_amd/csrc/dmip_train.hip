@@ -139,13 +139,22 @@ __device__ __forceinline__ const bf16x8& frag(const char* base, int idx, int lan
   return *(const bf16x8*)(base + (idx * 64 + lane) * 16);
 }
 
+// element (unit row, sample col) of a transposed scratch block: row stride RSV; the unpadded layout
+// (RSV = 16, 32-byte rows) swaps the two 16-byte halves of rows 8..15 mod 16, so that the rows 8 apart a
+// ds_read_b128 lane group or a put_t row group touches fall in different banks
+template <int RSV>
+__device__ __forceinline__ int sidx(int row, int col) {
+  if constexpr (RSV == 16) return row * 16 + (((col >> 3) ^ ((row >> 3) & 1)) << 3) + (col & 7);
+  return row * RSV + col;
+}
+
 // write one acc-form stream (64 units x 16 samples) transposed: scr[unit][sample] bf16
 template <int RSV>
 __device__ __forceinline__ void put_t(__bf16* scr, const f32x4 (&z)[4], int g, int c16) {
 #pragma unroll
   for (int R = 0; R < 4; ++R)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) scr[(16 * R + 4 * g + r) * RSV + c16] = (__bf16)z[R][r];
+    for (int r = 0; r < 4; ++r) scr[sidx<RSV>(16 * R + 4 * g + r, c16)] = (__bf16)z[R][r];
 }
 
 __device__ __forceinline__ void pack_b(const f32x4 (&z)[4], bf16x8 (&b)[2]) {
@@ -185,7 +194,7 @@ __device__ __forceinline__ f32x4 mm3(const bf16x8& a0, const bf16x8& a1, const b
 template <int RSV>
 __device__ __forceinline__ bf16x8 tread(const __bf16* scr, int row, bool ok, int hh) {
   // branch-free: every row < 64 is inside the scratch block; rows that are not operands read as zero
-  const u32x4 v = *(const u32x4*)(scr + row * RSV + 8 * hh);
+  const u32x4 v = *(const u32x4*)(scr + sidx<RSV>(row, 8 * hh));
   const u32x4 z = {0u, 0u, 0u, 0u};
   return __builtin_bit_cast(bf16x8, ok ? v : z);
 }
@@ -413,6 +422,7 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
           for (int S = 0; S < 3; ++S) HL[S][R >> 1][4 * (R & 1) + r] = bf_lo(v[S]);
         }
       }
+#pragma unroll
       for (int l = 1; l < NL; ++l) {
         bf16x8 Hn[NSTREAM][2], HLn[3][2];
         const char* wl = wfr + (l - 1) * 8192;
@@ -587,7 +597,9 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
           Z[1][R] = mfma16(a, BV, f32x4{});
           Z[2][R] = mfma16(a, BC, f32x4{});
         }
-        for (int l = 1; l <= li && l <= NL; ++l) {
+#pragma unroll
+        for (int l = 1; l <= NL; ++l) {
+          if (l > li) break;
           // activation of layer l-1 -> H
           f32x4 Hf[3][4];
 #pragma unroll
@@ -638,7 +650,7 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
 #pragma unroll
           for (int S = 0; S < 3; ++S)
 #pragma unroll
-            for (int o = 0; o < OUT; ++o) S_(S)[o * RS + c16] = (__bf16)ab[S][o];
+            for (int o = 0; o < OUT; ++o) S_(S)[sidx<RS>(o, c16)] = (__bf16)ab[S][o];
 #pragma unroll
           for (int o = 0; o < OUT; ++o) bobar[o] += abP[o] + abC[o];
         }
@@ -721,8 +733,8 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
 #pragma unroll
           for (int S = 0; S < 3; ++S) {
 #pragma unroll
-            for (int k = 0; k < IN; ++k) S_(3 + S)[k * RS + c16] = (__bf16)us[S][k];
-            S_(3 + S)[IN * RS + c16] = (__bf16)(S == 1 ? 0.0f : 1.0f);
+            for (int k = 0; k < IN; ++k) S_(3 + S)[sidx<RS>(k, c16)] = (__bf16)us[S][k];
+            S_(3 + S)[sidx<RS>(IN, c16)] = (__bf16)(S == 1 ? 0.0f : 1.0f);
           }
         }
       } else if (li >= 1) {
@@ -898,9 +910,13 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
 // grads[k] = sum over the per-workgroup partials in a fixed order (deterministic); slots nparam..+2
 // are the DSM / IC / PDE row sums -> loss_out = {loss, PDE, IC, DSM} means. 64 slots per block, the
 // partials split over 4 thread groups, combined in LDS in group order.
+// total_flags (bit 0 DSM, 1 IC, 2 PDE, bit 3 = set): the block holding the three loss slots also writes
+// loss_out[0] (their sum, as loss_total_kernel), saving that launch
 __global__ void __launch_bounds__(256) loss_grad_reduce_kernel(const float* partials, int n_parts, int stride,
-                                                               int nparam, float* grads, float* loss_out, float inv_n) {
+                                                               int nparam, float* grads, float* loss_out, float inv_n,
+                                                               int total_flags) {
   __shared__ double red[4][64];
+  __shared__ float lm[3];
   const int pi = threadIdx.x & 63, pg = threadIdx.x >> 6;
   const int k = blockIdx.x * 64 + pi;
   double s = 0.0;
@@ -910,15 +926,21 @@ __global__ void __launch_bounds__(256) loss_grad_reduce_kernel(const float* part
   }
   red[pg][pi] = s;
   __syncthreads();
-  if (pg != 0 || k >= nparam + 3) return;
-  s = red[0][pi] + red[1][pi] + red[2][pi] + red[3][pi];
-  if (k < nparam) {
-    grads[k] = (float)s;
-    return;
+  if (pg == 0 && k < nparam + 3) {
+    s = red[0][pi] + red[1][pi] + red[2][pi] + red[3][pi];
+    if (k < nparam) {
+      grads[k] = (float)s;
+    } else {
+      const float mean = (float)(s * inv_n);
+      const int c = k - nparam;  // 0 DSM, 1 IC, 2 PDE
+      loss_out[3 - c] = mean;
+      lm[c] = mean;
+    }
   }
-  const float mean = (float)(s * inv_n);
-  const int c = k - nparam;  // 0 DSM, 1 IC, 2 PDE
-  loss_out[3 - c] = mean;
+  if (!(total_flags & 8) || blockIdx.x != (unsigned)(nparam / 64)) return;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    loss_out[0] = ((total_flags & 1) ? lm[0] : 0.0f) + ((total_flags & 2) ? lm[1] : 0.0f) + ((total_flags & 4) ? lm[2] : 0.0f);
 }
 
 __global__ void loss_total_kernel(float* loss_out, int has_dsm, int has_ic, int has_pde) {
@@ -973,11 +995,14 @@ hipError_t launch_loss_grad(const TrainParams& p, int n_hidden, float* grads, fl
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
+  // the loss total rides on the reduction when the three loss slots share one 64-slot block
+  const bool fused_total = nparam / 64 == (nparam + 2) / 64;
+  const int flags = fused_total ? 8 | (p.has_dsm ? 1 : 0) | (p.has_ic ? 2 : 0) | (p.pde != 0 ? 4 : 0) : 0;
   hipLaunchKernelGGL(loss_grad_reduce_kernel, dim3((nparam + 3 + 63) / 64), dim3(256), 0, st, partials, n_wg,
                      part * train_partials_per_wg(),
-                     nparam, grads, loss_out, p.inv_n);
+                     nparam, grads, loss_out, p.inv_n, flags);
   e = hipGetLastError();
-  if (e != hipSuccess) return e;
+  if (e != hipSuccess || fused_total) return e;
   hipLaunchKernelGGL(loss_total_kernel, dim3(1), dim3(1), 0, st, loss_out, p.has_dsm, p.has_ic, p.pde != 0);
   return hipGetLastError();
 }
