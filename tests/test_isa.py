@@ -1,7 +1,8 @@
 """Static checks of the built gfx950 code objects (scripts/check_isa.py; CPU only): no kernel calls an
 outlined device function or needs a dynamic stack (an outlined score evaluation once put the f32
-sampler's activation arrays on an undersized scratch stack and faulted on the GPU), and the bf16
-product samplers run without any scratch."""
+sampler's activation arrays on an undersized scratch stack and faulted on the GPU), and the product
+samplers (16-bit, fp32x3 one-tile) and the config-5 training kernels run without any scratch (a
+register spill in them would be a silent slowdown); the k-major fp32x3 kernels within a small cap."""
 import importlib
 import os
 
@@ -23,7 +24,7 @@ def isa(dmip):
 def test_every_kernel_found(isa):
     names = " ".join(isa)
     for k in ("em_sampler_kernel", "f32_sampler_kernel", "f32_forward_kernel", "mlp_forward_kernel",
-              "loss_grad_kernel", "mh_kernel", "dps_kernel"):
+              "loss_grad_kernel", "mh_kernel", "dps_kernel", "x3_sampler_kernel", "x3k_sampler_kernel"):
         assert k in names, k
 
 
@@ -37,3 +38,19 @@ def test_bf16_samplers_have_no_scratch(isa):
     assert samplers
     spill = {k: v["private_segment_fixed_size"] for k, v in samplers.items() if v.get("private_segment_fixed_size")}
     assert not spill, spill
+
+
+# the k-major kernels hold ~460 registers; at NT = 3 the compiler parks ~20 dwords of per-segment state
+# (chain indices, output pointers) in scratch. Their loads and stores sit in the segment setup, the
+# hand-over epilogue and the snapshot branch, none in the step loop's hot path (checked in the ISA,
+# round 3); the cap keeps that from growing unnoticed.
+_SCRATCH_CAP = {"x3_sampler_kernel": 0, "x3k_sampler_kernel": 128, "loss_grad_kernel": 0}
+
+
+@pytest.mark.parametrize("family", list(_SCRATCH_CAP))
+def test_fp32x3_samplers_and_training_kernels_scratch(isa, family):
+    kernels = {k: v for k, v in isa.items() if family in k}
+    assert kernels, family
+    over = {k: v["private_segment_fixed_size"] for k, v in kernels.items()
+            if v.get("private_segment_fixed_size", 0) > _SCRATCH_CAP[family]}
+    assert not over, over
