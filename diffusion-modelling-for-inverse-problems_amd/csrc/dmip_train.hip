@@ -1,6 +1,7 @@
 // Fused score-matching training step: loss value and parameter gradients of the CDE training losses
-// (losses.py:42-242 as called by CDE.train_epoch, models/diffusion.py:74-89) for one batch, in one
-// persistent kernel plus a deterministic reduction.
+// (losses.py:42-242 as called by CDE.train_epoch, models/diffusion.py:74-89) for one batch: by default
+// a forward half and a reverse half (two kernels, see PH below), or the one-kernel build
+// (DMIP_TRAIN_SPLIT=0), plus a deterministic reduction.
 //
 // Formulation (restated and pinned in oracle/dmip_oracle.py:loss_grad):
 //  * forward pass with forward-mode jets through the MLP (nets.py:17-35, double tanh on layer 1):
@@ -22,9 +23,10 @@
 // four 16x16 accumulator tiles (v_mfma_f32_16x16x32_bf16: unit = 16R + 4(lane>>4) + reg, sample =
 // lane & 15), which repack into the next layer's B operand with no lane movement (k-permuted weight
 // fragments, as in the sampler). Weight-gradient products contract over samples and use
-// v_mfma_f32_32x32x16_bf16 (K = the tile's 16 samples). Each wave accumulates its gradient partial
-// in its own row of `partials` (global, 4-wave build) or LDS region (2-wave build, summed in wave
-// order per workgroup); loss_grad_reduce_kernel sums the rows in a fixed order (deterministic).
+// v_mfma_f32_32x32x16_bf16 (K = the tile's 16 samples). The reverse half's workgroup accumulates one
+// gradient partial in LDS with its waves taking turns (below); the one-kernel build accumulates per-wave
+// rows of `partials` (global, 4-wave build) or LDS regions (2-wave build). loss_grad_reduce_kernel sums
+// the rows in a fixed order: the gradients are bit-reproducible.
 #include <algorithm>
 #include <cstdlib>
 
@@ -65,8 +67,9 @@ static_assert(3 * IN + 2 <= 32, "layer-1 split operand fits one k-step");
 
 // PH: 0 = the fused kernel (forward jets, loss terms and reverse pass in one wave, one wave per SIMD);
 // 1 = the forward half (jets + per-sample loss terms and adjoints into p.adj; two waves per SIMD);
-// 2 = the reverse half (adjoints from p.adj, recompute + weight gradients; ~450 registers, one wave per SIMD:
-// at two waves per SIMD it spills ~220 registers). The reverse half accumulates the workgroup's gradient in
+// 2 = the reverse half (adjoints from p.adj, recompute + weight gradients; its layer loop unrolled, 357
+// registers, one wave per SIMD -- an 8-wave two-per-SIMD build spilled and measured slower, DESIGN.md
+// §4a). The reverse half accumulates the workgroup's gradient in
 // ONE LDS partial, its waves taking turns: at turn k wave w adds sub-block (w + k) % 4 of a layer's
 // gradient, a workgroup barrier between turns, so every address is summed in a fixed wave order
 // (deterministic) with no global atomics (~160 per tile in the fused kernel: its L2 atomic rate alone,
