@@ -5,8 +5,8 @@ tanh on layer 1), 1000 Euler-Maruyama steps, 100,000 chains per GPU for one y (y
 reference's seeded test set, tests/golden/data_scat.npz), weights = the fixture-trained checkpoint
 (tests/golden/ckpt_scat.npz; random init if absent -- timing does not depend on the weights).
 Headline arithmetic: the reference's fp32 (models/diffusion.py:38-42, nets.py:32-35), computed by the
-fp32x3 engine (every product as three fp16 MFMAs, W_hi h_hi + W_hi h_lo + W_lo h_hi, fp32 accumulation:
-csrc/dmip_x3.h). One "step" = one full sampling call (x0 draw + 1000 SDE steps + output in HBM). With
+fp32x3 engine (every product as three fp16 MFMAs, W_hi h_hi + W_hi h_lo + W_lo h_hi, fp32 accumulation;
+at this shape the k-major multi-tile kernel of csrc/dmip_x3k.h). One "step" = one full sampling call (x0 draw + 1000 SDE steps + output in HBM). With
 --gpus N the chains are sharded by global chain index (weak scaling: 100k chains per GPU) and the shards
 are gathered to every rank with one RCCL all_gather inside the timed region.
 
