@@ -81,6 +81,7 @@ def main():
             sched.step()
             if ep % max(1, a.epochs // 8) == 0 or ep == a.epochs - 1:
                 losses.append(float(loss))
+                print(f"[{tag}] epoch {ep}: loss {losses[-1]:.4g}", file=sys.stderr, flush=True)
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
         n_steps = 8 * a.epochs
