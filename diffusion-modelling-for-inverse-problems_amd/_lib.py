@@ -82,9 +82,8 @@ def _declare(lib):
     lib.dmip_abi_version.restype = _i32
     lib.dmip_sampler_supported.argtypes = [_i32, _i32, _i32, _i32, _i32]
     lib.dmip_sampler_supported_f32.argtypes = [_i32, _i32, _i32, _i32, _i32]
-    if hasattr(lib, "dmip_sampler_supported_precision"):
-        lib.dmip_sampler_supported_precision.argtypes = [_i32, _i32, _i32, _i32, _i32, _i32]
-        lib.dmip_sampler_supported_precision.restype = _i32
+    lib.dmip_sampler_supported_precision.argtypes = [_i32, _i32, _i32, _i32, _i32, _i32]  # ABI >= 6 (EXPORTED)
+    lib.dmip_sampler_supported_precision.restype = _i32
     lib.dmip_device_status.argtypes = [_c_void_p]
     lib.dmip_train_draws.argtypes = [_u64, _u64, _i64, _i32, _i32, ctypes.POINTER(DmipVpsde), ctypes.c_double, _f32,
                                      _c_void_p, _c_void_p, _c_void_p]
@@ -166,6 +165,10 @@ def lib():
                         f"dmip: HIP library not found at {LIB_PATH}; build it with "
                         "`python -c 'import __graft_entry__ as g; g.build()'` or `make` at the repo root")
                 handle = ctypes.CDLL(LIB_PATH)
+                missing = [n for n in EXPORTED if not hasattr(handle, n)]
+                if missing:
+                    raise RuntimeError(f"dmip: {LIB_PATH} is not ABI {ABI_VERSION}: missing {', '.join(missing)} "
+                                       "(rebuild with `make` at the repo root)")
                 _declare(handle)
                 _lib = handle
     return _lib

@@ -189,12 +189,16 @@ struct dmip_mlp {
   // the k-major engine's images (dmip_x3k.h; width 256, 3 hidden layers, xdim <= 4)
   char* x3k_stream = nullptr;     // [2 layers][8 k-steps][16 tiles][hi, lo][64][8] fp16
   char* x3k_out = nullptr;        // [8 k-steps][64][8]: rows 0..xdim-1 W_hi, rows 4..4+xdim-1 W_lo
+  // the paired-tile 32x32 engine's images (dmip_x3p.h; same shapes)
+  char* x3p_stream = nullptr;     // [16 chunks][32 KiB]
+  char* x3p_l1 = nullptr;         // [8 layer-1 tiles][64][8] | [2 hidden layers][8 bias tiles][64][8] fp16
+  float* x3p_ow = nullptr;        // f32 output rows [8][2][4][4][4] | init[16]
   ~dmip_mlp() {
     for (void* p : {(void*)ring_l1, (void*)hidden, (void*)ao_samp, (void*)ao_full, (void*)bias_hidden, (void*)bias_out_samp,
                     (void*)bias_out_full, (void*)a1_full, (void*)w1, (void*)b1, (void*)dps_l1, (void*)dps_w2,
                     (void*)dps_w3, (void*)dps_w4, (void*)dps_bias, (void*)f32_l1, (void*)f32_stream,
                     (void*)f32_bias, (void*)x3_l1, (void*)x3_l1_full, (void*)x3_stream, (void*)x3_bias,
-                    (void*)x3k_stream, (void*)x3k_out})
+                    (void*)x3k_stream, (void*)x3k_out, (void*)x3p_stream, (void*)x3p_l1, (void*)x3p_ow})
       if (p) (void)hipFree(p);
   }
 };
@@ -247,6 +251,84 @@ inline int x3_k1q(int nv) { return (3 * nv + 31) / 32; }
 void split_h(double v, uint16_t& hi, uint16_t& lo) {
   hi = f2h((float)v);
   lo = f2h((float)(v - (double)h2f(hi)));
+}
+
+// 32x32x16 fragments (dmip_x3p.h): lane l = i + 32 h holds A[row i][k-slot 8 h + j]; k-step s of a hidden layer
+// covers the previous layer's accumulator registers 8 (s & 1) .. + 7 of its output tile s >> 1
+inline int kperm32(int s, int h, int j) { return 32 * (s >> 1) + 16 * (s & 1) + 8 * (j >> 2) + 4 * h + (j & 3); }
+
+// the paired-tile engine's images of a [256]*3 CDE (dmip_x3p.h): the same hi / lo split and folded scales as
+// pack_x3_layer / pack_x3_l1 in the 32x32x16 fragment layout; hidden layer 1's bias (`init1`, already folded)
+// and hidden layer 2's (`init1`, `init2`: the folded inits of pack_x3_layer) as three-part fp16 A fragments per
+// output tile; the output layer in f32 (r-form fold: A = -2 W, init = b + sum_k W, in double)
+int pack_x3p(dmip_mlp* net, const float* const* weights, const float* const* biases, const float* init1,
+             const float* init2) {
+  const int W = net->width, IN = net->in_dim, D = net->xdim, OT = W / 32, KS = W / 16;
+  std::vector<uint16_t> l1((size_t)3 * OT * 512, 0);
+  std::vector<int> cols;
+  for (int k = 0; k < D; ++k) cols.push_back(k);
+  cols.push_back(IN - 1);
+  const int NV = (int)cols.size();
+  for (int o = 0; o < OT; ++o)
+    for (int l = 0; l < 64; ++l) {
+      const int i = l & 31, h = l >> 5;
+      for (int j = 0; j < 8; ++j) {
+        const int sl = 8 * h + j, n = sl / 3, pt = sl % 3;
+        if (n >= NV) continue;
+        uint16_t hi, lo;
+        split_h(kC * (double)weights[0][(size_t)(32 * o + i) * IN + cols[n]], hi, lo);
+        l1[((size_t)o * 64 + l) * 8 + j] = pt < 2 ? hi : lo;
+      }
+      for (int li = 1; li <= 2 && h == 0; ++li) {  // bias = hi + mid + lo in k-slots 0..2 (against ones)
+        const double v = (double)(li == 1 ? init1 : init2)[32 * o + i];
+        const uint16_t a = f2h((float)v);
+        const double r1 = v - (double)h2f(a);
+        const uint16_t b = f2h((float)r1);
+        const uint16_t c = f2h((float)(r1 - (double)h2f(b)));
+        uint16_t* dst = &l1[((size_t)(li * OT + o) * 64 + l) * 8];
+        dst[0] = a, dst[1] = b, dst[2] = c;
+      }
+    }
+  std::vector<char> stream;
+  std::vector<uint16_t> hi((size_t)W * W), lo((size_t)W * W), img((size_t)OT * KS * 1024);
+  for (int li = 1; li <= 2; ++li) {
+    for (int r = 0; r < W; ++r)
+      for (int k = 0; k < W; ++k)
+        split_h(-2.0 * kC * (double)weights[li][(size_t)r * W + k], hi[(size_t)r * W + k], lo[(size_t)r * W + k]);
+    size_t at = 0;
+    // hidden layer 1 k-major: chunk q, output tile o, k-step half e; hidden layer 2 output-major: chunk c, k-step s
+    for (int a = 0; a < OT; ++a)
+      for (int b = 0; b < KS; ++b)
+        for (int pt = 0; pt < 2; ++pt)
+          for (int l = 0; l < 64; ++l)
+            for (int j = 0; j < 8; ++j) {
+              const int row = li == 1 ? 32 * (b >> 1) + (l & 31) : 32 * a + (l & 31);
+              const int s = li == 1 ? 2 * a + (b & 1) : b;
+              const size_t src = (size_t)row * W + kperm32(s, l >> 5, j);
+              img[at++] = pt == 0 ? hi[src] : lo[src];
+            }
+    const char* p = (const char*)img.data();
+    stream.insert(stream.end(), p, p + img.size() * 2);
+  }
+  std::vector<float> ow((size_t)OT * 2 * 64 + 16, 0.0f);
+  for (int c = 0; c < OT; ++c)
+    for (int h = 0; h < 2; ++h)
+      for (int k = 0; k < D && k < 4; ++k)
+        for (int part = 0; part < 4; ++part)
+          for (int m = 0; m < 4; ++m)
+            ow[(((size_t)c * 2 + h) * 4 + k) * 16 + part * 4 + m] =
+                (float)(-2.0 * (double)weights[3][(size_t)k * W + 32 * c + 8 * part + 4 * h + m]);
+  for (int k = 0; k < D && k < 4; ++k) {
+    double acc = (double)biases[3][k];
+    for (int u = 0; u < W; ++u) acc += (double)weights[3][(size_t)k * W + u];
+    ow[(size_t)OT * 2 * 64 + k] = (float)acc;
+  }
+  std::vector<char> l1b(l1.size() * 2);
+  std::memcpy(l1b.data(), l1.data(), l1b.size());
+  int rc = DMIP_OK;
+  if ((rc = upload(&net->x3p_stream, stream)) || (rc = upload(&net->x3p_l1, l1b)) || (rc = upload(&net->x3p_ow, ow)))
+    return rc;
+  return DMIP_OK;
 }
 
 // layer-1 image over the input columns `cols` (scaled by c): input n at k-slots 3n, 3n+1, 3n+2 with
@@ -357,6 +439,7 @@ int pack_x3_net(dmip_mlp* net, const float* const* weights, const float* const* 
     std::vector<char> koutb(kout.size() * 2);
     std::memcpy(koutb.data(), kout.data(), koutb.size());
     if ((rc = upload(&net->x3k_stream, kstream)) || (rc = upload(&net->x3k_out, koutb))) return rc;
+    if (net->xdim <= 4 && (rc = pack_x3p(net, weights, biases, bias.data() + W, bias.data() + 2 * W))) return rc;
   }
   return DMIP_OK;
 }
@@ -753,6 +836,12 @@ static bool x3k_enabled() {
   const char* e = getenv("DMIP_X3K");
   return !(e && e[0] == '0');
 }
+// DMIP_X3P=1 selects the paired-tile 32x32 engine (dmip_x3p.h) instead of the 16x16 k-major one (dmip_x3k.h)
+// at its shape (in development: opt-in until it times faster on the device)
+static bool x3p_enabled() {
+  const char* e = getenv("DMIP_X3P");
+  return e && e[0] == '1';
+}
 
 // fp32-accurate split-fp16 samplers (dmip_x3.h): same loop, RNG and sharding as the other engines;
 // arguments already validated by em_sample_impl
@@ -803,8 +892,15 @@ static int em_sample_x3(int mode, const dmip_mlp* net0, const dmip_mlp* net1, co
   p.spin_limit = p.debug_flags ? (1u << 10) : (1u << 22);
   bool ok = false;
   hipError_t e;
-  if (mode == DMIP_SAMPLER_CDE && net0->x3k_stream && dmip::x3k_sampler_supported(mode, net0->width, net0->n_hidden, xdim) &&
-      x3k_enabled()) {
+  if (mode == DMIP_SAMPLER_CDE && net0->x3p_stream && dmip::x3p_sampler_supported(mode, net0->width, net0->n_hidden, xdim) &&
+      x3k_enabled() && x3p_enabled()) {
+    // the paired-tile 32x32 engine at its shape (dmip_x3p.h)
+    p.net[0].pstream = net0->x3p_stream;
+    p.net[0].pl1 = net0->x3p_l1;
+    p.net[0].pow = net0->x3p_ow;
+    e = dmip::launch_x3p_sampler(p, xdim, a.n_y, st, &ok);
+  } else if (mode == DMIP_SAMPLER_CDE && net0->x3k_stream &&
+             dmip::x3k_sampler_supported(mode, net0->width, net0->n_hidden, xdim) && x3k_enabled()) {
     // the k-major multi-tile engine at its shape (dmip_x3k.h)
     p.net[0].kstream = net0->x3k_stream;
     p.net[0].kout = net0->x3k_out;
@@ -1305,9 +1401,12 @@ static int pointer_device(const void* p) {
   hipPointerAttribute_t a{};
   int cur = 0;
   (void)hipGetDevice(&cur);
-  if (p && hipPointerGetAttributes(&a, p) == hipSuccess && a.device >= 0) return a.device;
-  (void)hipGetLastError();  // clear a sticky error from a non-device pointer
-  return cur;
+  if (!p) return cur;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();  // clear only the error this query left (a non-device pointer)
+    return cur;
+  }
+  return a.device >= 0 ? a.device : cur;
 }
 
 static void plan_free(dmip_train_plan* pl) {

@@ -253,6 +253,12 @@ struct X3Net {
   // [hi, lo][64][8] and the output layer as [k-step][64][8] with rows 0..D-1 = W_hi, 4..4+D-1 = W_lo
   const char* kstream = nullptr;
   const char* kout = nullptr;
+  // the paired-tile 32x32 engine (dmip_x3p.h; width 256, 3 hidden layers): 16 chunks of 32 KiB (hidden
+  // layer 1 k-major [q][o][e][hi, lo][64][8], hidden layer 2 output-major [c][s][hi, lo][64][8]), layer 1
+  // as [8 tiles][64][8], the output layer in f32 [c][lane half][row][4][4] + its init[16]
+  const char* pstream = nullptr;
+  const char* pl1 = nullptr;
+  const float* pow = nullptr;
 };
 
 struct X3SamplerParams {
@@ -291,6 +297,9 @@ bool x3_sampler_supported(int mode, int width, int n_hidden, int xdim, int ydim)
 // the k-major multi-tile engine (dmip_x3k.h): CDE, width 256, 3 hidden layers, xdim 2 or 3
 bool x3k_sampler_supported(int mode, int width, int n_hidden, int xdim);
 hipError_t launch_x3k_sampler(const X3SamplerParams& p, int xdim, int n_y, hipStream_t st, bool* ok);
+// the paired-tile 32x32 engine (dmip_x3p.h): CDE, width 256, 3 hidden layers, xdim 1..4
+bool x3p_sampler_supported(int mode, int width, int n_hidden, int xdim);
+hipError_t launch_x3p_sampler(const X3SamplerParams& p, int xdim, int n_y, hipStream_t st, bool* ok);
 hipError_t launch_x3_bias_prep(const X3BiasPrepParams& p, int n_y, hipStream_t st);
 // geometry of the x3 images (dmip_x3.h Shape) for the host packer
 int x3_chunk_bytes(int width);

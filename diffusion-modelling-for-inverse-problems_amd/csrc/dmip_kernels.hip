@@ -774,8 +774,10 @@ hipError_t alloc_handover(size_t slots, int d, hipStream_t st, char** buf, float
   if (e != hipSuccess) return e;
   *xfer = (float*)*buf;
   *xflag = (unsigned*)(*buf + state_bytes);
-  // state and flags zeroed: nothing in the buffer is ever uninitialised memory
-  return hipMemsetAsync(*buf, 0, state_bytes + slots * sizeof(unsigned), st);
+  // only the flags are zeroed: a consumer reads a slot's state only after its flag is set, and writes NaN
+  // (not the slot's contents) for a tile whose hand-over never arrived. (Zeroing the state too was ~5 MB of
+  // memset traffic per headline launch.)
+  return hipMemsetAsync(*xflag, 0, slots * sizeof(unsigned), st);
 }
 
 template <int MODE, int W, int NL, int D, int M, int NW, int R, bool RES>

@@ -5,15 +5,18 @@
 
 namespace dmip {
 
-// Development knob (not part of the ABI): DMIP_X3_DIAG=d (1..7) runs the timing ablation DIAG = d of the
-// width-256, xdim-3 CDE kernel (dmip_x3.h XEngine); see profiles/README.md.
+#ifdef DMIP_DIAG
+// Diagnostic library only (make diag; never the product build): DMIP_X3_DIAG=d (1..7) runs the timing ablation
+// DIAG = d of the width-256, xdim-3 CDE kernel (dmip_x3.h XEngine); see profiles/README.md.
 static int x3_diag() {
   const char* e = getenv("DMIP_X3_DIAG");
   return e ? atoi(e) : 0;
 }
+#endif
 
 hipError_t launch_x3_sampler_cde(const X3SamplerParams& p, int width, int xdim, int n_y, hipStream_t st, bool* ok) {
   *ok = true;
+#ifdef DMIP_DIAG
   if (width == 256 && xdim == 3 && !p.noise) {
     switch (x3_diag()) {
 #define DG(d) \
@@ -23,6 +26,7 @@ hipError_t launch_x3_sampler_cde(const X3SamplerParams& p, int width, int xdim, 
       default: break;
     }
   }
+#endif
 #define X(Wv, Dv) \
   if (width == Wv && xdim == Dv) return launch_x3_sampler_n<SAMPLER_CDE, Wv, Dv, 0>(p, n_y, st);
   X(64, 2) X(128, 2) X(256, 2) X(512, 2) X(64, 3) X(128, 3) X(256, 3) X(512, 3)

@@ -313,16 +313,17 @@ __global__ void __launch_bounds__(KWaves<NT>::NWV * 64, KWaves<NT>::NWV / 4) x3k
     if (sg.kind == 2) {  // resume the job the previous wave of the grid handed over
       const size_t slot = (size_t)yi * n_waves + gw - 1;
       const bool lost = handover_wait(p.xflag + slot, p.spin_limit, p.err, kErrHandover, lane);
+      // compact slot: one copy per chain (lane group 0 stored it), [tile][word][16 chains]
       const float* src = p.xfer + slot * (size_t)(NT * XT);
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
-        const float* st = src + t * XT;
+        const float* st = src + t * (D + 4) * 16;
 #pragma unroll
-        for (int k = 0; k < D; ++k) x[t][k] = lost ? __builtin_nanf("") : st[k * 64 + lane];
-        rng[t].s0 = __float_as_uint(st[(D + 0) * 64 + lane]);
-        rng[t].s1 = __float_as_uint(st[(D + 1) * 64 + lane]);
-        rng[t].s2 = __float_as_uint(st[(D + 2) * 64 + lane]);
-        rng[t].s3 = __float_as_uint(st[(D + 3) * 64 + lane]);
+        for (int k = 0; k < D; ++k) x[t][k] = lost ? __builtin_nanf("") : st[k * 16 + j];
+        rng[t].s0 = __float_as_uint(st[(D + 0) * 16 + j]);
+        rng[t].s1 = __float_as_uint(st[(D + 1) * 16 + j]);
+        rng[t].s2 = __float_as_uint(st[(D + 2) * 16 + j]);
+        rng[t].s3 = __float_as_uint(st[(D + 3) * 16 + j]);
       }
     } else {
 #pragma unroll
@@ -446,15 +447,17 @@ __global__ void __launch_bounds__(KWaves<NT>::NWV * 64, KWaves<NT>::NWV / 4) x3k
     if (sg.kind == 1) {  // hand the job over to the next wave of the grid
       const size_t slot = (size_t)yi * n_waves + gw;
       float* dst = p.xfer + slot * (size_t)(NT * XT);
+      if (g == 0) {  // the four lane groups hold identical copies of a chain's state: store one
 #pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        float* st = dst + t * XT;
+        for (int t = 0; t < NT; ++t) {
+          float* st = dst + t * (D + 4) * 16;
 #pragma unroll
-        for (int k = 0; k < D; ++k) st[k * 64 + lane] = x[t][k];
-        st[(D + 0) * 64 + lane] = __uint_as_float(rng[t].s0);
-        st[(D + 1) * 64 + lane] = __uint_as_float(rng[t].s1);
-        st[(D + 2) * 64 + lane] = __uint_as_float(rng[t].s2);
-        st[(D + 3) * 64 + lane] = __uint_as_float(rng[t].s3);
+          for (int k = 0; k < D; ++k) st[k * 16 + j] = x[t][k];
+          st[(D + 0) * 16 + j] = __uint_as_float(rng[t].s0);
+          st[(D + 1) * 16 + j] = __uint_as_float(rng[t].s1);
+          st[(D + 2) * 16 + j] = __uint_as_float(rng[t].s2);
+          st[(D + 3) * 16 + j] = __uint_as_float(rng[t].s3);
+        }
       }
       handover_publish(p.xflag + slot, lane, p.debug_flags);
     } else if (sg.kind != 3 && g == 0) {

@@ -321,7 +321,10 @@ class CDiffE(BaseClassDiffusionModel):
                 precision=None):
         """As BaseClassDiffusionModel.forward; `corrector_steps` > 0 adds Langevin corrector steps
         before every predictor step (predictor-corrector sampling, BASELINE config 3; see
-        dmip_em_sample_cdiffe in include/dmip.h for the definition)."""
+        dmip_em_sample_cdiffe in include/dmip.h for the definition). The step size takes the norms at
+        their expected values, eps = 2 alpha snr^2 var(T - t): `snr` is not score_sde's measured-norm snr
+        (that one measures |s| on the batch; for a trained score with |s| != sqrt(d)/std the same value
+        gives a different step)."""
         from . import parallel
         x = parallel.sample_sharded(self, y, num_samples, num_steps, mean, std,
                                     corrector_steps=corrector_steps, snr=snr, precision=precision)

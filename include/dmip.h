@@ -127,6 +127,9 @@ int dmip_em_sample_posterior(const dmip_mlp* prior, const dmip_mlp* likelihood, 
  *         size per time step, as score_sde's batch-averaged norms; a per-chain ratio diverges),
  *         x <- x + eps s + sqrt(2 eps) z, alpha = exp(-beta(T-t) delta) (score_sde's discrete VP
  *         alpha 1 - beta delta to first order, positive at any step count). 0 = plain EM.
+ *         snr is therefore NOT score_sde's measured-norm snr: score_sde measures |s| on the batch, so
+ *         for a trained score whose norm differs from sqrt(d)/std(T-t) the same snr value takes a
+ *         different step here than there (the step is a fixed function of t, shard-invariant).
  * Other arguments as dmip_em_sample (no injection). */
 int dmip_em_sample_cdiffe(const dmip_mlp* net, const dmip_vpsde* sde, const float* y_dev, int n_y, int ydim, int xdim,
                           int64_t n_chains, int64_t chain_offset, int num_steps, float mean, float stdv, uint64_t seed,

@@ -8,7 +8,7 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
 B=(python bench.py --precision fp32x3 --steps 3 --warmup 1 --no-cpu-baseline --no-fp32 --no-other-configs)
 for d in 0 1 2 4 6 7; do
-  DMIP_X3_DIAG=$d timeout -k 10 200 "${B[@]}" > "$OUT/diag_$d.log" 2>&1 || { echo "diag $d failed"; exit 3; }
+  DMIP_LIB=abv/diag/libdmip_diag.so DMIP_X3_DIAG=$d timeout -k 10 200 "${B[@]}" > "$OUT/diag_$d.log" 2>&1 || { echo "diag $d failed"; exit 3; }
   python -c "import json;d=json.loads(open('$OUT/diag_$d.log').read().strip().splitlines()[-1]);print('diag $d', round(d['roofline']['launch_ms'],2), 'ms')"
 done
 run_pass() {

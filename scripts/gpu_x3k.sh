@@ -18,8 +18,8 @@ run() {  # run <name> <env...>
 run nt3 DMIP_X3K_NT=3
 run nt2 DMIP_X3K_NT=2
 run onetile DMIP_X3K=0
-run nt3_noring DMIP_X3K_NT=3 DMIP_X3_DIAG=1
-run nt2_noring DMIP_X3K_NT=2 DMIP_X3_DIAG=1
+run nt3_noring DMIP_X3K_NT=3 DMIP_LIB=abv/diag/libdmip_diag.so DMIP_X3_DIAG=1
+run nt2_noring DMIP_X3K_NT=2 DMIP_LIB=abv/diag/libdmip_diag.so DMIP_X3_DIAG=1
 timeout -k 10 200 python scripts/bench_config5.py > "$OUT/config5.json" 2>&1 || { echo "config5 failed"; tail -5 "$OUT/config5.json"; exit 3; }
 tail -1 "$OUT/config5.json"
 timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -k "loss_grad or config5 or train_epoch" -v -s --timeout 120 \

@@ -1,6 +1,7 @@
-"""Per-phase cycle stamps of the k-major fp32x3 sampler (DMIP_X3_DIAG=2 build path; diagnostic only): the
+"""Per-phase cycle stamps of the k-major fp32x3 sampler (diagnostic library only: make diag, then
+DMIP_LIB=abv/diag/libdmip_diag.so DMIP_X3_DIAG=2): the
 headline workload (100k chains x 1000 steps, scatterometry CDE [256]^3), cycles per step and wave split into
-layer 1, hidden 1, hidden 2, output layer, EM update. One JSON line.   DMIP_X3_DIAG=2 python scripts/x3k_stamps.py"""
+layer 1, hidden 1, hidden 2, output layer, EM update. One JSON line.   DMIP_LIB=abv/diag/libdmip_diag.so DMIP_LIB=abv/diag/libdmip_diag.so DMIP_X3_DIAG=2 python scripts/x3k_stamps.py"""
 import importlib
 import json
 import os
@@ -14,7 +15,8 @@ sys.path.insert(0, ROOT)
 
 
 def main():
-    assert os.environ.get("DMIP_X3_DIAG") == "2"
+    assert os.environ.get("DMIP_X3_DIAG") == "2" and "diag" in os.environ.get("DMIP_LIB", "")
+    os.environ["DMIP_X3P"] = "0"  # the k-major engine, not the paired-tile default
     pkg = importlib.import_module("diffusion-modelling-for-inverse-problems_amd")
     dev = torch.device("cuda:0")
     torch.manual_seed(0)

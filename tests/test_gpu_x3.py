@@ -209,12 +209,13 @@ def test_x3_handover_timeout_is_reported_not_silent(dmip, golden, monkeypatch):
     m = _cde(dmip, "scat", golden("ckpt_scat.npz"))
     y = torch.from_numpy(golden("data_scat.npz")["y_test"][0]).to(DEV)
     monkeypatch.setenv("DMIP_DEBUG_NO_HANDOVER", "1")
-    x = m.sample_device(y, 50000, 4, seed=1, precision=PREC)
+    # more jobs than the grid has waves (the paired engine's 64-chain jobs: > 65,536 chains), so tiles are handed over
+    x = m.sample_device(y, 100000, 4, seed=1, precision=PREC)
     with pytest.raises(RuntimeError, match="hand-over"):
         dmip._lib.device_status(x.device)
     assert torch.isnan(x).any() and torch.isfinite(x).any()
     monkeypatch.delenv("DMIP_DEBUG_NO_HANDOVER")
-    x = m.sample_device(y, 50000, 4, seed=1, precision=PREC)
+    x = m.sample_device(y, 100000, 4, seed=1, precision=PREC)
     dmip._lib.device_status(x.device)
     assert torch.isfinite(x).all()
 
