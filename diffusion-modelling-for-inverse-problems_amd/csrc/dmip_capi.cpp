@@ -181,7 +181,9 @@ struct dmip_mlp {
   char* f32_stream = nullptr;     // [(L-1) W/16 + f32_ot chunks][W/16][64][4]
   float* f32_bias = nullptr;      // [(L-1)][W] | [16 f32_ot]
   int f32_k1q = 0, f32_ot = 0;
-  // fp32-accurate split-fp16 images (DMIP_PREC_F32X3, dmip_x3.h)
+  // fp32-accurate split-fp16 images (DMIP_PREC_F32X3, dmip_x3.h); none when a scaled weight or folded bias
+  // is outside fp16's range (x3_range: that magnitude, reported by em_sample_x3)
+  double x3_range = 0.0;
   char* x3_l1 = nullptr;          // [W/16][K1Q][64][8] fp16 over (x, t)
   char* x3_l1_full = nullptr;     // the same over every input column (X_Y_T networks: CDiffE)
   char* x3_stream = nullptr;      // hidden chunks | output chunk
@@ -376,10 +378,33 @@ void pack_x3_layer(const float* Wl, const float* bl, int n_rows, int W, int n_ti
           }
 }
 
+// largest magnitude the fp32x3 images would hold in fp16: layer 1 scaled by 2 log2(e), the hidden layers by
+// -2 * 2 log2(e), the output rows by -2 (r-form folds), the paired engine's folded hidden biases
+double x3_max_scaled(const dmip_mlp* net, const float* const* weights, const float* const* biases) {
+  const int W = net->width, L = net->n_hidden, IN = net->in_dim, OUT = net->out_dim;
+  double m = 0.0;
+  for (size_t i = 0; i < (size_t)W * IN; ++i) m = std::max(m, kC * std::fabs((double)weights[0][i]));
+  for (int li = 1; li < L; ++li) {
+    for (size_t i = 0; i < (size_t)W * W; ++i) m = std::max(m, 2.0 * kC * std::fabs((double)weights[li][i]));
+    for (int r = 0; r < W; ++r) {  // folded bias kC b + kC sum_k W (pack_x3_layer)
+      double acc = (double)biases[li][r];
+      for (int k = 0; k < W; ++k) acc += (double)weights[li][(size_t)r * W + k];
+      m = std::max(m, kC * std::fabs(acc));
+    }
+  }
+  for (size_t i = 0; i < (size_t)std::min(OUT, 16) * W; ++i) m = std::max(m, 2.0 * std::fabs((double)weights[L][i]));
+  return m;
+}
+
 int pack_x3_net(dmip_mlp* net, const float* const* weights, const float* const* biases) {
   const int W = net->width, L = net->n_hidden, IN = net->in_dim, OUT = net->out_dim, ST = W / 16;
   const int chunk = dmip::x3_chunk_bytes(W);
   if (chunk == 0) return DMIP_OK;  // no x3 kernels at this width
+  const double mx = x3_max_scaled(net, weights, biases);
+  if (!(mx <= 65504.0)) {  // beyond fp16 (or not finite): no split images; fp32x3 requests are refused
+    net->x3_range = std::isfinite(mx) ? mx : 1e300;
+    return DMIP_OK;
+  }
   std::vector<int> xt;
   for (int k = 0; k < net->xdim; ++k) xt.push_back(k);
   xt.push_back(IN - 1);
@@ -463,6 +488,9 @@ int dmip_device_status(void* stream) {
   if (v == dmip::kErrHandover)
     return fail(DMIP_ERR_HIP, "sampler: a split tile's hand-over never arrived (workgroups of the balanced schedule "
                               "were not co-resident); the affected chains were written as NaN");
+  if (v == dmip::kErrRange)
+    return fail(DMIP_ERR_HIP, "fp32x3 sampler: a chain's layer-1 input left the fp16 range of the split arithmetic "
+                              "(|x| > 65504); those chains are not fp32-accurate (use DMIP_PREC_F32)");
   return fail(DMIP_ERR_HIP, "device status " + std::to_string(v));
 }
 
@@ -847,6 +875,10 @@ static bool x3p_enabled() {
 // arguments already validated by em_sample_impl
 static int em_sample_x3(int mode, const dmip_mlp* net0, const dmip_mlp* net1, const SampleArgs& a) {
   const int xdim = a.xdim, ydim = a.ydim;
+  for (const dmip_mlp* n : {net0, net1})
+    if (n && n->x3_range > 0.0)
+      return fail(DMIP_ERR_UNSUPPORTED, "fp32x3: a weight is outside the fp16 range of the split engine (largest "
+                                        "scaled |w| " + std::to_string(n->x3_range) + " > 65504); use DMIP_PREC_F32");
   if (!dmip::x3_sampler_supported(mode, net0->width, net0->n_hidden, xdim, ydim) || !net0->x3_stream ||
       (mode == DMIP_SAMPLER_CDIFFE && !net0->x3_l1_full) || (net1 && !net1->x3_stream))
     return fail(DMIP_ERR_UNSUPPORTED, "no compiled f32x3 sampler (mode " + std::to_string(mode) + ") for width " +

@@ -71,6 +71,10 @@ struct SamplerParams {
 
 // device status codes written by kernels into the per-device status word
 constexpr unsigned kErrHandover = 1u;
+// a fp32x3 sampler's layer-1 input (chain state x, tau, CDiffE's y_t) left the fp16 range of its hi/lo split
+// (|v| > 65504): those chains are not fp32-accurate (dmip_device_status reports it; the Python estimators
+// resample with the exact-f32 engine)
+constexpr unsigned kErrRange = 2u;
 
 // hand-over state of a split tile, per grid wave: x[D] + the xoshiro128** state, one word per lane
 constexpr int sampler_xfer_words(int D) { return (D + 4) * 64; }

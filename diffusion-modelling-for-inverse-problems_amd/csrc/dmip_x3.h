@@ -364,6 +364,21 @@ __device__ __forceinline__ void l1_operand(const float (&v)[NV], int g, u32x4 (&
   }
 }
 
+// Range of the split: every layer-1 input v is carried as fp16 hi + lo, exact to ~2^-22 |v| for |v| <= 65504
+// (fp16's largest finite value; below 2^-14 hi is subnormal and the pair holds ~2^-24 absolute). A chain whose
+// input leaves it (a diverging trajectory) is flagged and reported through the device status word.
+template <int NV>
+__device__ __forceinline__ bool out_of_range(const float (&v)[NV]) {
+  bool o = false;
+#pragma unroll
+  for (int n = 0; n < NV; ++n) o |= __builtin_fabsf(v[n]) > 65504.0f;  // (false for NaN: a lost hand-over)
+  return o;
+}
+__device__ __forceinline__ void report_range(bool oor, unsigned* err, int lane) {
+  if (__builtin_amdgcn_ballot_w64(oor) != 0 && lane == 0)
+    __hip_atomic_store(err, kErrRange, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // ---------------------------------------------------------------------------- sampler kernel
 // The reverse-SDE loop (models/diffusion.py:27-46) with fp32-accurate networks:
 //   MODE_CDE        a = net(x, y, tau), y folded into the per-y layer-1 bias (f64 prep)
@@ -424,6 +439,7 @@ __global__ void __launch_bounds__(Shape<W>::NW * 64, Shape<W>::NW / 4) x3_sample
   const WaveSchedule sched(tiles_y, S, n_waves, gw);
   const size_t noise_step = (size_t)gridDim.y * p.n_chains * D;
   (void)ST;
+  bool oor = false;  // a layer-1 input out of the split's range (report_range)
 
   for (int sgi = 0; sgi < sched.n_seg; ++sgi) {
     const Seg sg = sched.segment(sgi);
@@ -479,6 +495,7 @@ __global__ void __launch_bounds__(Shape<W>::NW * 64, Shape<W>::NW / 4) x3_sample
       auto score = [&](const float (&vin)[C::NV], float (&a)[D]) __attribute__((always_inline)) {
         u32x4 b1[K1Q];
         l1_operand<C::NV, K1Q>(vin, g, b1);
+        oor |= out_of_range(vin);
         f32x4 out = eng.eval(0, b1);
         if constexpr (C::NNET > 1) out = out + eng.eval(1, b1);  // likelihood + prior, then g * (...)
 #pragma unroll
@@ -543,6 +560,7 @@ __global__ void __launch_bounds__(Shape<W>::NW * 64, Shape<W>::NW / 4) x3_sample
     }
   }
   eng.finish();
+  report_range(oor, p.err, lane);
 }
 
 }  // namespace x3

@@ -299,6 +299,7 @@ __global__ void __launch_bounds__(KWaves<NT>::NWV * 64, KWaves<NT>::NWV / 4) x3k
   const size_t noise_step = (size_t)gridDim.y * p.n_chains * D;
 
   uint64_t ph[6] = {0, 0, 0, 0, 0, 0};  // DIAG & 2: cycles per phase (L1, H1, H2, output, EM, barrier waits)
+  bool oor = false;                      // a layer-1 input out of the split's range (x3::report_range)
   for (int sgi = 0; sgi < sched.n_seg; ++sgi) {
     const Seg sg = sched.segment(sgi);
     long long c_loc[NT];
@@ -360,6 +361,7 @@ __global__ void __launch_bounds__(KWaves<NT>::NWV * 64, KWaves<NT>::NWV / 4) x3k
           for (int k = 0; k < D; ++k) v[k] = x[t][k];
           v[NV - 1] = cf.tau;
           x3::l1_operand<NV, 1>(v, g, b1[t]);
+          oor |= x3::out_of_range(v);
         }
 #pragma unroll
         for (int o = 0; o < ST; ++o) {
@@ -471,6 +473,7 @@ __global__ void __launch_bounds__(KWaves<NT>::NWV * 64, KWaves<NT>::NWV / 4) x3k
     }
   }
   wait_vmcnt<0>();  // the prefetched chunks of a step that never ran land before the workgroup exits
+  x3::report_range(oor, p.err, lane);
   if constexpr (DIAG & 2) {
     if (lane == 0) {
       uint64_t* dst = (uint64_t*)p.snap_out + ((size_t)yi * n_waves + gw) * 8;

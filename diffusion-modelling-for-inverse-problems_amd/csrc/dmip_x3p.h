@@ -232,6 +232,7 @@ struct PWave {
   float tau_next;
   float delta, sqrt_delta;
   bool first;  // first step of a segment: tile B has no previous step to complete
+  bool oor = false;  // a layer-1 input out of the split's range (x3::report_range)
   uint64_t ph[17], t_last;  // kDiag: cycles per ring chunk, barrier waits
 
   // ------------------------------------------------------------------ ring (dmip_x3k.h protocol)
@@ -412,6 +413,7 @@ struct PWave {
     v[D] = tau_n;
     u32x4 b[1];
     x3::l1_operand<D + 1, 1>(v, h, b);
+    oor |= x3::out_of_range(v);
     b1[T] = b[0];
     touch(b1[T]);
 #pragma unroll
@@ -496,6 +498,7 @@ struct PWave {
     v[D] = tau;
     u32x4 b[1];
     x3::l1_operand<D + 1, 1>(v, h, b);
+    oor |= x3::out_of_range(v);
     b1[0] = b[0];
     typedef __attribute__((address_space(3))) const u32x4* lds_u4;
     typedef __attribute__((address_space(3))) const float* lds_f;
@@ -701,6 +704,7 @@ __global__ void __launch_bounds__(NWV * 64, 1) x3p_sampler_kernel(X3SamplerParam
     }
   }
   wait_vmcnt<0>();  // the prefetched chunks of a step that never ran land before the workgroup exits
+  x3::report_range(e.oor, p.err, lane);
   if constexpr (kDiag) {
     if (lane == 0 && p.snap_out) {
       uint64_t* dst = (uint64_t*)p.snap_out + ((size_t)yi * n_waves + gw) * 18;

@@ -64,9 +64,30 @@ def sample_sharded(model, y, num_samples, num_steps, mean, std, seed=None, **sam
     dev = model._exec_device(y)
     seed = common_seed(_draw_seed() if seed is None else seed, dev)
     lo, hi = shard_range(num_samples, rank, ws)
-    local = model.sample_device(y, hi - lo, num_steps, mean, std, seed=seed, chain_offset=lo, **sampler_kwargs)
+    local = _sample_local(model, y, hi - lo, num_steps, mean, std, seed, lo, sampler_kwargs)
     full = gather_shards(local, num_samples, dev)
     return full[0] if torch.as_tensor(y).ndim == 1 else full
+
+
+def _sample_local(model, y, n, num_steps, mean, std, seed, lo, kw):
+    """This rank's shard. At the default precision (fp32x3: the reference's fp32 arithmetic from fp16 hi/lo
+    splits) a network or a trajectory outside the split's fp16 range -- a scaled weight, or a chain's layer-1
+    input, beyond 65504 -- is refused (at launch) or reported (device status) by the library; the shard is then
+    sampled again with the exact-f32 engine, so the default path never returns the split's inf/NaN where the
+    reference's fp32 stays finite. Decided per rank before the collective gather."""
+    import warnings
+    from . import _lib
+    default = kw.get("precision") is None and getattr(model, "precision", None) == "fp32x3"
+    try:
+        x = model.sample_device(y, n, num_steps, mean, std, seed=seed, chain_offset=lo, **kw)
+        if default:
+            _lib.device_status(x.device)
+        return x
+    except (ValueError, RuntimeError) as e:
+        if not (default and "fp16 range" in str(e)):
+            raise
+        warnings.warn(f"{e}; sampled with the exact-f32 engine instead", RuntimeWarning)
+        return model.sample_device(y, n, num_steps, mean, std, seed=seed, chain_offset=lo, **dict(kw, precision="fp32"))
 
 
 def map_sharded(n, fn, width):

@@ -50,6 +50,13 @@ typedef enum { DMIP_ACT_TANH_TWICE_FIRST = 0, DMIP_ACT_TANH = 1 } dmip_act;
  *                   2^-23.2 of sum |w h| measured against 2^-23.0 for an f32 fmaf chain), tanh by exp2 + rcp
  *                   at ~1 ulp (no polynomial). The reference-precision throughput mode (samplers; the
  *                   network forward runs the exact-f32 kernel).
+ *                   Range: the split holds a value to ~2^-22 relative for |v| <= 65504 (fp16's largest
+ *                   finite value) and to ~2^-24 absolute below 2^-14 (fp16 subnormals). The scaled weights
+ *                   (layer 1 x 2 log2(e), hidden layers x 4 log2(e), output rows x 2) and folded biases must
+ *                   fit: a network that does not is refused at sampling time (DMIP_ERR_UNSUPPORTED, "fp16
+ *                   range"). Every layer-1 input (chain state x, t; CDiffE's y_t) is checked in the kernel: a
+ *                   chain that leaves the range is reported by dmip_device_status ("fp16 range") -- those
+ *                   chains are not fp32-accurate. The Python estimators resample with DMIP_PREC_F32 then.
  * All three draw the same RNG stream per chain, so the modes are comparable chain by chain. */
 typedef enum { DMIP_PREC_BF16 = 0, DMIP_PREC_F32 = 1, DMIP_PREC_F32X3 = 2 } dmip_precision;
 

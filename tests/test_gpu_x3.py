@@ -261,3 +261,63 @@ def test_x3_posterior_parity_fp32_gate(dmip, golden, tag):
     r = M.parity_report(x, smp["samples"], smp["quantiles"], int(smp["n_total"]))
     print(f"\n[x3] parity {tag}: {r}")
     assert r["pass"], r
+
+
+# ------------------------------------------------------------- the split's fp16 range (include/dmip.h)
+@pytest.mark.parametrize("engine", ["x3k", "x3p", "x3"])
+def test_x3_weight_outside_fp16_range_refused_default_falls_back(dmip, golden, engine, monkeypatch):
+    """One hidden weight at 2e4 (x 4 log2(e) = 1.2e5 > 65504 in the split image): an explicit fp32x3 request is
+    refused with a clear error; the default precision samples with the exact-f32 engine instead, equal to it chain
+    by chain and to the float32 oracle."""
+    monkeypatch.setenv("DMIP_X3P", "1" if engine == "x3p" else "0")
+    if engine == "x3":
+        monkeypatch.setenv("DMIP_X3K", "0")
+    m = _cde(dmip, "scat", golden("ckpt_scat.npz"))
+    with torch.no_grad():
+        m.sde.a._modules["3"].weight[5, 7] = 2.0e4  # the first W x W layer (state_dict key 3)
+    y = torch.from_numpy(golden("samples_scat.npz")["y"]).to(DEV)
+    n, S = 600, 8
+    with pytest.raises(ValueError, match="fp16 range"):
+        m.sample_device(y, n, S, seed=3, precision=PREC)
+    torch.manual_seed(5)
+    with pytest.warns(RuntimeWarning, match="fp16 range"):
+        x = m(y, num_samples=n, num_steps=S)
+    torch.manual_seed(5)
+    xf = m(y, num_samples=n, num_steps=S, precision="fp32")
+    assert np.array_equal(x, xf)
+    seed = 77
+    xs = m.sample_device(y, n, S, seed=seed, precision="fp32")[0].cpu().numpy()
+    ref = O.cde_sample(_linear_params(m.sde.a), y.cpu().numpy(), n, S, seed)
+    e = _rel(xs, ref)
+    print(f"\n[x3] {engine} weight 2e4: exact-f32 fallback vs oracle {e:.2e}")
+    assert np.all(np.isfinite(x)) and e < 1e-4, e
+
+
+@pytest.mark.parametrize("engine", ["x3k", "x3p", "x3"])
+def test_x3_trajectory_outside_fp16_range_reported_default_falls_back(dmip, golden, engine, monkeypatch):
+    """An output bias of 1e6 drives every chain to |x| ~ 1e5-1e6 after one step (finite in fp32): the fp32x3
+    kernel flags the layer-1 inputs beyond 65504 through the device status word; the default precision resamples
+    with the exact-f32 engine, which matches the float32 oracle."""
+    monkeypatch.setenv("DMIP_X3P", "1" if engine == "x3p" else "0")
+    if engine == "x3":
+        monkeypatch.setenv("DMIP_X3K", "0")
+    m = _cde(dmip, "scat", golden("ckpt_scat.npz"))
+    with torch.no_grad():
+        m.sde.a._modules["7"].bias[:] = 1.0e6  # the output layer (state_dict key 7)
+    y = torch.from_numpy(golden("samples_scat.npz")["y"]).to(DEV)
+    n, S, seed = 600, 6, 91
+    x3 = m.sample_device(y, n, S, seed=seed, precision=PREC)
+    with pytest.raises(RuntimeError, match="fp16 range"):
+        dmip._lib.device_status(x3.device)
+    dmip._lib.device_status(x3.device)  # the status word was cleared
+    torch.manual_seed(6)
+    with pytest.warns(RuntimeWarning, match="fp16 range"):
+        x = m(y, num_samples=n, num_steps=S)
+    torch.manual_seed(6)
+    xf = m(y, num_samples=n, num_steps=S, precision="fp32")
+    assert np.array_equal(x, xf) and np.all(np.isfinite(x)) and np.abs(x).max() > 6.6e4
+    xs = m.sample_device(y, n, S, seed=seed, precision="fp32")[0].cpu().numpy()
+    ref = O.cde_sample(_linear_params(m.sde.a), y.cpu().numpy(), n, S, seed)
+    e = _rel(xs, ref)
+    print(f"\n[x3] {engine} |x| up to {np.abs(xs).max():.2e}: exact-f32 fallback vs oracle {e:.2e}")
+    assert e < 1e-4, e
