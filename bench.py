@@ -425,12 +425,36 @@ def other_configs(args, pkg, lib, dev):
         except Exception as e:  # noqa: BLE001 -- reported in the line, never fatal to the headline
             out[name] = {"error": f"{type(e).__name__}: {e}"}
 
+    try:  # configs[0]: the reference's own sampling call (main_diffusion_linear.py:74), host result included
+        zl = np.load(os.path.join(ROOT, "tests", "golden", "ckpt_lin.npz"))
+        ml = pkg.CDE(2, 2, [64] * 3)
+        ml.sde.a.load_state_dict({k.replace("_", "."): torch.from_numpy(zl[k]) for k in zl.files
+                                  if k.split("_")[0].isdigit()})
+        ml.sde.a.to(dev)
+        yl = torch.tensor([0.5, 1.0])
+        ts = []
+        for r in range(9):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            xs = ml(yl, num_samples=1000, num_steps=200)  # returns the host ndarray: D2H inside
+            ts.append(time.perf_counter() - t0)
+        med = float(np.median(ts[2:]))
+        out["config1_linear"] = {
+            "workload": "linear CDE [64]*3 (fixture weights), model(y, num_samples=1000, num_steps=200) -- "
+                        "main_diffusion_linear.py:74, default precision fp32x3, host ndarray returned (D2H included)",
+            "value": 1000 / med, "unit": "samples/s", "latency_ms_median_of_7": med * 1e3,
+            "latency_ms_min": min(ts[2:]) * 1e3, "cpu_reference_samples_per_s": 13400.0,
+            "cpu_reference": "BASELINE.md configs[0]: 0.075 s median of 5, 8-core Xeon, reference CPU torch",
+            "vs_cpu_reference": (1000 / med) / 13400.0, "finite": bool(np.all(np.isfinite(xs)))}
+    except Exception as e:  # noqa: BLE001
+        out["config1_linear"] = {"error": f"{type(e).__name__}: {e}"}
     sampler("config3_cdiffe_pc_per_gpu", "cdiffe-pc", 125000, 2, "fp32x3")
     sampler("config3_cdiffe_pc_per_gpu_fast", "cdiffe-pc", 125000, 2, "bf16")
     sampler("config4_dps", "dps", 262144, 1, "fp32")
     sampler("cde_reference_width_512", "cde", 100000, 2, "fp32x3", width=512)
     sampler("posterior_reference_width_512", "cde", 100000, 1, "fp32x3", width=512, posterior=True)
-    # CDiffE scatterometry at width 512 has no fp32x3 kernel (its 27-input layer 1 does not fit beside the ring)
+    # CDiffE scatterometry at width 512: fp32x3 with its 96 KiB split layer 1 streamed through the ring (L1R)
+    sampler("cdiffe_pc_reference_width_512", "cdiffe-pc", 100000, 1, "fp32x3", width=512)
     sampler("cdiffe_pc_reference_width_512_fast", "cdiffe-pc", 100000, 1, "bf16", width=512)
     try:
         tr = importlib.import_module(PKG + ".training")

@@ -187,6 +187,7 @@ struct dmip_mlp {
   char* x3_l1 = nullptr;          // [W/16][K1Q][64][8] fp16 over (x, t)
   char* x3_l1_full = nullptr;     // the same over every input column (X_Y_T networks: CDiffE)
   char* x3_stream = nullptr;      // hidden chunks | output chunk
+  char* x3_stream_l1r = nullptr;  // CDiffE at width 512: layer-1 chunks ([K1Q][W/16 tiles][64][8]) | x3_stream
   float* x3_bias = nullptr;       // [L W + 16]
   // the k-major engine's images (dmip_x3k.h; width 256, 3 hidden layers, xdim <= 4)
   char* x3k_stream = nullptr;     // [2 layers][8 k-steps][16 tiles][hi, lo][64][8] fp16
@@ -199,7 +200,8 @@ struct dmip_mlp {
     for (void* p : {(void*)ring_l1, (void*)hidden, (void*)ao_samp, (void*)ao_full, (void*)bias_hidden, (void*)bias_out_samp,
                     (void*)bias_out_full, (void*)a1_full, (void*)w1, (void*)b1, (void*)dps_l1, (void*)dps_w2,
                     (void*)dps_w3, (void*)dps_w4, (void*)dps_bias, (void*)f32_l1, (void*)f32_stream,
-                    (void*)f32_bias, (void*)x3_l1, (void*)x3_l1_full, (void*)x3_stream, (void*)x3_bias,
+                    (void*)f32_bias, (void*)x3_l1, (void*)x3_l1_full, (void*)x3_stream, (void*)x3_stream_l1r,
+                    (void*)x3_bias,
                     (void*)x3k_stream, (void*)x3k_out, (void*)x3p_stream, (void*)x3p_l1, (void*)x3p_ow})
       if (p) (void)hipFree(p);
   }
@@ -460,6 +462,16 @@ int pack_x3_net(dmip_mlp* net, const float* const* weights, const float* const* 
   if ((rc = upload(&net->x3_l1, l1b)) || (rc = upload(&net->x3_l1_full, l1fb)) || (rc = upload(&net->x3_stream, stream)) ||
       (rc = upload(&net->x3_bias, bias)))
     return rc;
+  const int k1q_full = x3_k1q(IN);
+  if (!l1f.empty() && ST * 1024 == chunk && ST * k1q_full * 1024 > 48 * 1024) {
+    // the sampler streams this layer 1 through the ring (dmip_x3.h L1R): chunk q = k-step q of every tile
+    std::vector<char> s1((size_t)k1q_full * chunk);
+    for (int q = 0; q < k1q_full; ++q)
+      for (int o = 0; o < ST; ++o)
+        std::memcpy(s1.data() + ((size_t)q * ST + o) * 1024, l1fb.data() + ((size_t)o * k1q_full + q) * 1024, 1024);
+    s1.insert(s1.end(), stream.begin(), stream.end());
+    if ((rc = upload(&net->x3_stream_l1r, s1))) return rc;
+  }
   if (kmajor) {
     std::vector<char> koutb(kout.size() * 2);
     std::memcpy(koutb.data(), kout.data(), koutb.size());
@@ -887,6 +899,7 @@ static int em_sample_x3(int mode, const dmip_mlp* net0, const dmip_mlp* net1, co
   hipStream_t st = (hipStream_t)a.stream;
   dmip::X3SamplerParams p{};
   p.net[0] = dmip::X3Net{mode == DMIP_SAMPLER_CDIFFE ? net0->x3_l1_full : net0->x3_l1, net0->x3_stream, net0->x3_bias};
+  if (mode == DMIP_SAMPLER_CDIFFE && net0->x3_stream_l1r) p.net[0].stream = net0->x3_stream_l1r;  // L1R layout
   if (net1) p.net[1] = dmip::X3Net{net1->x3_l1, net1->x3_stream, net1->x3_bias};
   p.n_hidden = net0->n_hidden;
   float* bias_y = nullptr;

@@ -63,11 +63,12 @@ constexpr int k1q_of(int nv) { return (3 * nv + 31) / 32; }
 constexpr int align16(int v) { return (v + 15) / 16 * 16; }
 
 // LDS: layer-1 images, biases (per network: layer 1 | hidden layers | output rows 0..15), the
-// observation (CDiffE), the ring.
-template <int W, int NNET, int K1Q, int M>
+// observation (CDiffE), the ring. L1R: layer 1 is not resident but streams through the ring ahead of the
+// hidden chunks (CDiffE at width 512: its 27-input split image is 96 KiB).
+template <int W, int NNET, int K1Q, int M, bool L1R = false>
 struct XLay {
   using S = Shape<W>;
-  static constexpr int L1_BYTES = S::ST * K1Q * 1024;
+  static constexpr int L1_BYTES = L1R ? 0 : S::ST * K1Q * 1024;
   static constexpr int BF = kMaxHidden * W + 16;  // bias floats per network
   static constexpr int L1 = 0;
   static constexpr int BIAS = L1 + NNET * L1_BYTES;
@@ -181,7 +182,7 @@ __device__ __forceinline__ float x3_act_r2(float zs) {
 // DIAG (timing ablations only, never on the product path; DMIP_X3_DIAG): bit 0 = no ring (no DMA, no
 // barrier: stale weights), bit 1 = hidden activations replaced by the split alone, bit 2 = the same for
 // layer 1's double tanh
-template <int W, int NNET, int K1Q, int R, int RING_OFF, int DIAG = 0>
+template <int W, int NNET, int K1Q, int R, int RING_OFF, int DIAG = 0, bool L1R = false>
 struct XEngine {
   using S = Shape<W>;
   static constexpr int ST = S::ST, KQ = S::KQ, CT = S::CT, NCH = S::NCH, NW = S::NW, PPW = S::PPW;
@@ -198,9 +199,13 @@ struct XEngine {
   int s_read;   // ring slot of the next chunk to consume
   int w, lane, g;
 
+  // chunks of layer 1 in the stream (L1R): k-step q of every output tile, ST KiB
+  static constexpr int NL1C = L1R ? K1Q : 0;
+  static_assert(!L1R || ST * 1024 == CHUNK, "a streamed layer-1 chunk is one k-step of all output tiles");
+
   __device__ __forceinline__ void init(int n_hidden) {
     nl = n_hidden;
-    ncn = (nl - 1) * NCH + 1;
+    ncn = NL1C + (nl - 1) * NCH + 1;
     c_issue = s_issue = s_read = 0;
   }
 
@@ -291,6 +296,42 @@ struct XEngine {
     for (int o = 0; o < ST; ++o) act_store<true>(acc[o], o, Oh, Ol);
   }
 
+  // layer 1 streamed through the ring (L1R): chunk q holds k-step q of all ST output tiles ([o][64][8]); all
+  // ST accumulators stay in registers over the K1Q chunks, then the double tanh of every tile
+  __device__ __forceinline__ void layer1_ring(int ni, const u32x4 (&b1)[K1Q], u32x4 (&Oh)[KQ], u32x4 (&Ol)[KQ]) {
+    f32x4 acc[ST];
+#pragma unroll
+    for (int o = 0; o < ST; ++o) acc[o] = bias4(ni, 0, o);
+    lgkm_drain();
+#pragma unroll
+    for (int q = 0; q < K1Q; ++q) {
+      const char* ch = chunk_sync();
+      const lds_cptr base = (lds_cptr)(ch + lane * 16);
+      u32x4 fa[4];
+      fa[0] = lds_rd<0>(base);
+      fa[1] = lds_rd<1024>(base);
+      fa[2] = lds_rd<2048>(base);
+      const u32x4 bq[1] = {b1[q]};
+      if (q + 1 < K1Q) l1_chain<1, ST, 3>(base, bq, acc, fa);
+      else l1_chain_act<0>(base, bq[0], acc, fa, Oh, Ol);  // each tile activated once complete
+    }
+  }
+  // the last layer-1 chunk: tile F's MFMA, then the double tanh of tile F - 2 (its MFMA retired), so the
+  // accumulators free progressively instead of all ST staying live beside the activated operands
+  template <int F>
+  __device__ __forceinline__ void l1_chain_act(lds_cptr base, const u32x4& b, f32x4 (&acc)[ST], u32x4 (&fa)[4],
+                                               u32x4 (&Oh)[KQ], u32x4 (&Ol)[KQ]) const {
+    if constexpr (F < ST + 2) {
+      if constexpr (F < ST) {
+        if constexpr (F + 3 < ST) fa[(F + 3) % 4] = lds_rd<(F + 3) * 1024>(base);
+        lds_wait1<cmin(ST - 1 - F, 3)>(fa[F % 4]);
+        acc[F] = mfma16(fa[F % 4], b, acc[F]);
+      }
+      if constexpr (F >= 2) act_store<true>(acc[F - 2], F - 2, Oh, Ol);
+      l1_chain_act<F + 1>(base, b, acc, fa, Oh, Ol);
+    }
+  }
+
   __device__ __forceinline__ void hidden(int ni, int li, const u32x4 (&Hh)[KQ], const u32x4 (&Hl)[KQ],
                                          u32x4 (&Oh)[KQ], u32x4 (&Ol)[KQ]) {
     f32x4 pend[CT];
@@ -326,7 +367,8 @@ struct XEngine {
   // one network: layer 1, the nl - 1 hidden layers (ping-pong), the output tile
   __device__ __forceinline__ f32x4 eval(int ni, const u32x4 (&b1)[K1Q]) {
     u32x4 Ah[KQ], Al[KQ], Bh[KQ], Bl[KQ];
-    layer1(ni, b1, Ah, Al);
+    if constexpr (L1R) layer1_ring(ni, b1, Ah, Al);
+    else layer1(ni, b1, Ah, Al);
     for (int li = 1; li < nl; li += 2) {
       hidden(ni, li, Ah, Al, Bh, Bl);
       if (li + 1 < nl) hidden(ni, li + 1, Bh, Bl, Ah, Al);
@@ -392,8 +434,10 @@ struct SamplerCfg {
   static constexpr int NNET = MODE == SAMPLER_POSTERIOR ? 2 : 1;
   static constexpr int NV = MODE == SAMPLER_CDIFFE ? D + M + 1 : D + 1;  // layer-1 inputs (y folded for CDE)
   static constexpr int K1Q = k1q_of(NV);
-  using L = XLay<W, NNET, K1Q, M>;
-  using E = XEngine<W, NNET, K1Q, L::R, L::RING, DIAG>;
+  // CDiffE's split layer 1 over all inputs streams through the ring when it would not fit resident
+  static constexpr bool L1R = MODE == SAMPLER_CDIFFE && Shape<W>::ST * K1Q * 1024 > 48 * 1024;
+  using L = XLay<W, NNET, K1Q, M, L1R>;
+  using E = XEngine<W, NNET, K1Q, L::R, L::RING, DIAG, L1R>;
 };
 
 template <int MODE, int W, int D, int M, bool NOISE, int DIAG = 0>

@@ -56,14 +56,13 @@ hipError_t launch_x3_sampler(const X3SamplerParams& p, int mode, int width, int 
 }
 
 // Compiled: widths 64 / 128 / 256 / 512, 1 to 3 hidden layers (a runtime count), xdim 2 or 3 (CDE,
-// Posterior: any ydim -- y is folded into layer 1's bias); CDiffE for (xdim, ydim) = (2, 2) at every
-// width and (3, 23) up to width 256 (its 27-input layer-1 image, 96 KiB at width 512, would leave no
-// room for the weight ring).
+// Posterior: any ydim -- y is folded into layer 1's bias); CDiffE for (xdim, ydim) = (2, 2) and (3, 23) at
+// every width (at width 512 the 27-input layer-1 image, 96 KiB, streams through the weight ring: L1R).
 bool x3_sampler_supported(int mode, int width, int n_hidden, int xdim, int ydim) {
   if (n_hidden < 1 || n_hidden > x3::kMaxHidden) return false;
   if (width != 64 && width != 128 && width != 256 && width != 512) return false;
   if (mode == SAMPLER_CDE || mode == SAMPLER_POSTERIOR) return xdim == 2 || xdim == 3;
-  if (mode == SAMPLER_CDIFFE) return (xdim == 2 && ydim == 2) || (xdim == 3 && ydim == 23 && width <= 256);
+  if (mode == SAMPLER_CDIFFE) return (xdim == 2 && ydim == 2) || (xdim == 3 && ydim == 23);
   return false;
 }
 

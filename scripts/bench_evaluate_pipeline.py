@@ -5,8 +5,9 @@ repeats: 3e10 chain-steps, one fused launch) followed by main_diffusion_scattero
 reverse KL, NLL of the MCMC and diffusion samples through the surrogate, the score MSE at t = 0 against
 -energy_grad), all through the package's reference-API functions. Prints one JSON line with the wall
 times and the metric means.
-Model: the fixture-trained CDE [256]^3 (tests/golden/ckpt_scat.npz).
-    python scripts/bench_evaluate_pipeline.py [--n-y 100] [--n 30000] [--repeats 10]"""
+Model: the fixture-trained CDE [256]^3 (tests/golden/ckpt_scat.npz), or --ckpt a CDE state_dict (.npz, e.g. one
+scripts/bench_posterior_e2e.py --recipe reference --save-cde wrote) of hidden width --width.
+    python scripts/bench_evaluate_pipeline.py [--n-y 100] [--n 30000] [--repeats 10] [--ckpt PATH --width 512]"""
 import argparse
 import importlib
 import json
@@ -30,6 +31,8 @@ def main():
     ap.add_argument("--repeats", type=int, default=10)
     ap.add_argument("--steps", type=int, default=200, help="SDE steps (the reference's default)")
     ap.add_argument("--metr-steps", type=int, default=1000)
+    ap.add_argument("--ckpt", default="", help="CDE state_dict (.npz) instead of the fixture")
+    ap.add_argument("--width", type=int, default=256)
     a = ap.parse_args()
     pkg = importlib.import_module("diffusion-modelling-for-inverse-problems_amd")
     ev = importlib.import_module("diffusion-modelling-for-inverse-problems_amd.evaluate")
@@ -41,8 +44,9 @@ def main():
     fm = fm.to(dev)
     _, ys = pr.generate_dataset_scatterometry(fm, prm["a"], prm["b"], size=100)
     ys = ys[:a.n_y].to(dev)
-    m = pkg.CDE(3, 23, [256] * 3)
-    m.sde.a.load_state_dict(state_from_npz(np.load(os.path.join(gold, "ckpt_scat.npz"))))
+    m = pkg.CDE(3, 23, [a.width] * 3)
+    ck = a.ckpt or os.path.join(gold, "ckpt_scat.npz")
+    m.sde.a.load_state_dict(state_from_npz(np.load(ck)))
     m.sde.a.to(dev)
     # warm-up (kernel images, handles)
     pkg.generate_gt_samples(fm, prm, ys[:1], None, 256, 1, 10, 0.5, seed=1)
@@ -72,7 +76,7 @@ def main():
         "ground_truth_s": t_gt, "ground_truth_chain_steps_per_s": chain_steps_gt / t_gt,
         "evaluate_s": t_ev, "evaluate_posterior_samples_per_s": samples / t_ev,
         "KL2_mean": float(kl), "NLPD_mean": float(nlpd), "MSE_mean": float(mse),
-        "model": "fixture-trained CDE [256]^3 (tests/golden/ckpt_scat.npz)"}), flush=True)
+        "model": f"CDE [{a.width}]^3 from {os.path.relpath(ck, ROOT)}"}), flush=True)
 
 
 if __name__ == "__main__":

@@ -16,7 +16,14 @@ Data: the reference's own generator (inverse-CDF prior samples pushed through th
 noise model, datasets.py:26-34), fresh each epoch; y = the reference's seeded y_test[i].
 Prints one JSON line: training steps / time / samples per second, and KL2 (75^3 bins on [-1.2, 1.2]^3,
 the reference metric) and per-dimension W1 against the MH ground truth.
-    python scripts/bench_posterior_e2e.py [--width 256] [--epochs 400] [--batch 8192]"""
+    python scripts/bench_posterior_e2e.py [--width 256] [--epochs 400] [--batch 8192]
+Recipes (CDE only, --save-cde writes the trained weights for scripts/bench_evaluate_pipeline.py --ckpt):
+  --recipe reference  config_scatterometry.yml as main_diffusion_scatterometry.py trains it: CDE [512]^3,
+                      PINNLoss (lam 0.01, lam2 0.001, FPE / L1, IC L2 against -energy_grad), Adam lr 1e-4 (no
+                      schedule), batch 1000, 20,000 epochs of 8 batches (datasets.py:26-34), debiased t;
+  --recipe fixture    the CPU fixture's recipe (tests/golden/make_golden.py train_ckpt): CDE [256]^3, DSMLoss,
+                      uniform t, batch 1000, Adam from lr 1e-3 on the cosine with floor 0.05, 18,560 epochs
+                      (its train_log) -- the control for the device-trained quality."""
 import argparse
 import importlib
 import json
@@ -47,7 +54,17 @@ def main():
     ap.add_argument("--snr-sweep", default="", help="comma-separated corrector snr values to score as well")
     ap.add_argument("--load-cdiffe", default="", help="sample a CDiffE checkpoint written by --save-cdiffe")
     ap.add_argument("--save-cdiffe", default="", help="write the trained CDiffE's state_dict here (.npz)")
+    ap.add_argument("--recipe", default="", choices=["", "reference", "fixture"])
+    ap.add_argument("--save-cde", default="", help="write the trained CDE's state_dict here (.npz)")
+    ap.add_argument("--no-dps", action="store_true")
     a = ap.parse_args()
+    if a.recipe:  # CDE only, at the recipe's own sizes
+        a.no_posterior = a.no_cdiffe = a.no_dps = True
+        a.batch = 1000
+        if a.recipe == "reference":
+            a.width, a.lr, a.epochs = 512, 1e-4, a.epochs if a.epochs != 400 else 20000
+        else:
+            a.width, a.lr, a.epochs = 256, 1e-3, a.epochs if a.epochs != 400 else 18560
     pkg = importlib.import_module("diffusion-modelling-for-inverse-problems_amd")
     ev = importlib.import_module("diffusion-modelling-for-inverse-problems_amd.evaluate")
     pr = importlib.import_module("diffusion-modelling-for-inverse-problems_amd.problems")
@@ -71,21 +88,26 @@ def main():
 
     def train(model, loss_fn, tag):
         opt = torch.optim.Adam(model.sde.a.parameters(), lr=a.lr)
-        sched = torch.optim.lr_scheduler.CosineAnnealingLR(opt, a.epochs)
+        sched = None if a.recipe else torch.optim.lr_scheduler.CosineAnnealingLR(opt, a.epochs)
         losses = []
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for ep in range(a.epochs):
+            if a.recipe == "fixture":  # make_golden.py train_ckpt: cosine over the run, floor 0.05
+                for gr in opt.param_groups:
+                    gr["lr"] = a.lr * (0.05 + 0.95 * 0.5 * (1 + np.cos(np.pi * ep / a.epochs)))
             loader = pr.get_dataloader_scatterometry(a.batch, fm, prm["a"], prm["b"], prm["lambd_bd"])
             loss, _ = model.train_epoch(opt, loss_fn, loader)
-            sched.step()
-            if ep % max(1, a.epochs // 8) == 0 or ep == a.epochs - 1:
+            if sched is not None:
+                sched.step()
+            if ep % max(1, a.epochs // (40 if a.recipe else 8)) == 0 or ep == a.epochs - 1:
                 losses.append(float(loss))
                 print(f"[{tag}] epoch {ep}: loss {losses[-1]:.4g}", file=sys.stderr, flush=True)
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
         n_steps = 8 * a.epochs
-        return {"model": tag, "width": a.width, "optimizer_steps": n_steps, "batch": a.batch,
+        return {"model": tag, "width": a.width, "optimizer_steps": n_steps, "batch": a.batch, "lr": a.lr,
+                "recipe": a.recipe or "device default (cosine lr)",
                 "train_s": el, "train_samples_per_s": n_steps * a.batch / el, "loss_trace": losses}
 
     out = {"metric": "scatterometry estimators trained and sampled on one GPU, quality vs MCMC",
@@ -106,15 +128,23 @@ def main():
     if not a.no_cde:
         cde = pkg.CDE(3, 23, [a.width] * 3)
         cde.sde.a.to(dev)
-        sp = lambda xx, yy: -pkg.energy_grad(xx, lambda v: pkg.get_log_posterior(v, fm, prm["a"], prm["b"], yy,
-                                                                                  prm["lambd_bd"]))[0]
-        lf = pkg.PINNLoss(sp, lam=0.01, lam2=0.001, pde_loss="FPE", ic_metric="L2", pde_metric="L1")
+        if a.recipe == "fixture":
+            cde.sde.debias = False  # uniform t (the fixture: sdeflow-light's debiased sampler is not vendored)
+            lf, tag = pkg.DSMLoss(), "CDE + DSMLoss (the CPU fixture's recipe)"
+        else:
+            sp = lambda xx, yy: -pkg.energy_grad(xx, lambda v: pkg.get_log_posterior(v, fm, prm["a"], prm["b"], yy,
+                                                                                      prm["lambd_bd"]))[0]
+            lf = pkg.PINNLoss(sp, lam=0.01, lam2=0.001, pde_loss="FPE", ic_metric="L2", pde_metric="L1")
+            tag = "CDE + PINNLoss (reference config losses, -energy_grad IC)"
         n0 = pkg._lib.calls.get("loss_grad_f32", 0)
-        r = train(cde, lf, "CDE + PINNLoss (reference config losses, -energy_grad IC)")
+        r = train(cde, lf, tag)
         r["fused_steps"] = pkg._lib.calls.get("loss_grad_f32", 0) - n0
         x = cde.sample_device(y, a.n, a.steps, seed=8)
         r["quality"] = score(x)
-        out["cde_pinn"] = r
+        out["cde_" + (a.recipe or "pinn")] = r
+        if a.save_cde:
+            sd = {k.replace(".", "_"): v.detach().cpu().numpy() for k, v in cde.sde.a.state_dict().items()}
+            np.savez(a.save_cde, **sd)
 
     if not a.no_cdiffe:
         cd = pkg.CDiffE(3, 23, [a.width] * 3)
@@ -141,6 +171,9 @@ def main():
             sd = {k.replace(".", "_"): v.detach().cpu().numpy() for k, v in cd.sde.a.state_dict().items()}
             np.savez(a.save_cdiffe, **sd)
 
+    if a.no_dps:
+        print(json.dumps(out), flush=True)
+        return
     dps = pkg.DPS(3, 23, [256] * 3, fm, prm)
     ck = os.path.join(gold, "ckpt_prior_scat.npz")
     z = np.load(ck)

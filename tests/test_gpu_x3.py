@@ -116,7 +116,8 @@ def test_x3_posterior_sampler_vs_oracle(dmip, W, NL, xd, yd):
     assert err < 1e-4, err
 
 
-@pytest.mark.parametrize("W,xd,yd", [(64, 2, 2), (256, 2, 2), (512, 2, 2), (64, 3, 23), (128, 3, 23), (256, 3, 23)])
+@pytest.mark.parametrize("W,xd,yd", [(64, 2, 2), (256, 2, 2), (512, 2, 2), (64, 3, 23), (128, 3, 23), (256, 3, 23),
+                                     (512, 3, 23)])
 def test_x3_cdiffe_sampler_vs_oracle(dmip, W, xd, yd):
     torch.manual_seed(3 * W + xd)
     m = dmip.CDiffE(xd, yd, [W] * 3)
@@ -132,9 +133,10 @@ def test_x3_cdiffe_sampler_vs_oracle(dmip, W, xd, yd):
     assert err < 1e-4, err
 
 
-def test_x3_cdiffe_predictor_corrector_vs_oracle(dmip):
+@pytest.mark.parametrize("W", [256, 512])
+def test_x3_cdiffe_predictor_corrector_vs_oracle(dmip, W):
     torch.manual_seed(11)
-    m = dmip.CDiffE(3, 23, [256] * 3)
+    m = dmip.CDiffE(3, 23, [W] * 3)
     with torch.no_grad():
         last = [l for l in m.sde.a if isinstance(l, torch.nn.Linear)][-1]
         last.weight.mul_(0.05)
@@ -148,17 +150,16 @@ def test_x3_cdiffe_predictor_corrector_vs_oracle(dmip):
     x0 = O.cdiffe_sample(params, y, n, S, seed)
     assert np.abs(ref - x0).max() > 1e-2  # the corrector moves the chains
     err = _rel(x, ref)
-    print(f"\n[x3] CDiffE PC: {err:.3e}")
+    print(f"\n[x3] CDiffE PC W={W}: {err:.3e}")
     assert err < 1e-4, err
 
 
-def test_x3_cdiffe_scat_width512_falls_back_to_exact_f32(dmip):
-    """CDiffE scatterometry at width 512 has no f32x3 kernel (layer-1 image too large): a fp32x3 request
-    runs the exact-f32 kernel (more accurate, never less)."""
+def test_x3_cdiffe_scat_width512_runs_fp32x3(dmip):
+    """CDiffE scatterometry at the reference width 512: its 96 KiB split layer 1 streams through the weight ring
+    (dmip_x3.h L1R), so a fp32x3 request runs the fp32x3 kernel (before round 4: the exact-f32 one)."""
     est = __import__("importlib").import_module("diffusion-modelling-for-inverse-problems_amd.estimators")
-    assert not dmip._lib.sampler_supported(512, 3, 3, 23, dmip._lib.DMIP_SAMPLER_CDIFFE, PREC)
-    assert est._fused_precision(PREC, dmip._lib.DMIP_SAMPLER_CDIFFE, 512, 3, 3, 23) == "fp32"
-    assert est._fused_precision("bf16", dmip._lib.DMIP_SAMPLER_CDIFFE, 512, 3, 3, 23) == "bf16"
+    assert dmip._lib.sampler_supported(512, 3, 3, 23, dmip._lib.DMIP_SAMPLER_CDIFFE, PREC)
+    assert est._fused_precision(PREC, dmip._lib.DMIP_SAMPLER_CDIFFE, 512, 3, 3, 23) == PREC
 
 
 # ------------------------------------------------------- the two fp32 engines over a long trajectory
@@ -190,7 +191,7 @@ def test_x3_shards_and_batches_bit_identical(dmip, cls):
 
 
 @pytest.mark.parametrize("cls,W,n", [("CDE", 256, 70001), ("CDE", 512, 40001), ("PosteriorDiffusionEstimator", 256, 70001),
-                                     ("CDiffE", 256, 70001)])
+                                     ("CDiffE", 256, 70001), ("CDiffE", 512, 40001)])
 def test_x3_balanced_schedule_matches_unsplit_runs(dmip, cls, W, n):
     """More chains than one GPU round: tiles split between waves through the balanced schedule; every
     chain equals a launch small enough to run each tile whole."""

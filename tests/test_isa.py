@@ -24,7 +24,8 @@ def isa(dmip):
 def test_every_kernel_found(isa):
     names = " ".join(isa)
     for k in ("em_sampler_kernel", "f32_sampler_kernel", "f32_forward_kernel", "mlp_forward_kernel",
-              "loss_grad_kernel", "mh_kernel", "dps_kernel", "x3_sampler_kernel", "x3k_sampler_kernel"):
+              "loss_grad_kernel", "mh_kernel", "dps_kernel", "x3_sampler_kernel", "x3k_sampler_kernel",
+              "x3p_sampler_kernel"):
         assert k in names, k
 
 
@@ -44,13 +45,19 @@ def test_bf16_samplers_have_no_scratch(isa):
 # (chain indices, output pointers) in scratch. Their loads and stores sit in the segment setup, the
 # hand-over epilogue and the snapshot branch, none in the step loop's hot path (checked in the ISA,
 # round 3); the cap keeps that from growing unnoticed.
-_SCRATCH_CAP = {"x3_sampler_kernel": 0, "x3k_sampler_kernel": 128, "loss_grad_kernel": 0}
+# The paired-tile kernels (x3p, 185 VGPRs + 256 AGPRs) have none. One-tile x3: none, except CDiffE (3, 23) at width
+# 512, whose layer 1 streams through the ring (L1R, one wave per SIMD at ~512 registers): ~17 dwords of segment
+# state (addresses, chain indices) spilled, reloaded in the segment setup and a handful of times per step.
+_SCRATCH_CAP = {"x3_sampler_kernel": 0, "x3k_sampler_kernel": 128, "loss_grad_kernel": 0, "x3p_sampler_kernel": 0}
+_SCRATCH_CAP_KERNEL = {"x3_sampler_kernelILi2ELi512ELi3ELi23E": 128}
 
 
 @pytest.mark.parametrize("family", list(_SCRATCH_CAP))
 def test_fp32x3_samplers_and_training_kernels_scratch(isa, family):
     kernels = {k: v for k, v in isa.items() if family in k}
     assert kernels, family
+    def cap(k):
+        return next((c for pat, c in _SCRATCH_CAP_KERNEL.items() if pat in k), _SCRATCH_CAP[family])
     over = {k: v["private_segment_fixed_size"] for k, v in kernels.items()
-            if v.get("private_segment_fixed_size", 0) > _SCRATCH_CAP[family]}
+            if v.get("private_segment_fixed_size", 0) > cap(k)}
     assert not over, over
