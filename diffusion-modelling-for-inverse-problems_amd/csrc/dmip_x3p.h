@@ -350,12 +350,19 @@ struct PWave {
   }
   template <int T, int O>
   __device__ __forceinline__ void q_act() {
+    float r[16];  // the tile's 16 activations stage by stage (see h2_out)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) r[i] = __builtin_amdgcn_exp2f(Q[T][O][i]);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) r[i] = 1.0f + r[i];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) r[i] = __builtin_amdgcn_rcpf(r[i]);
 #pragma unroll
     for (int e = 0; e < 2; ++e)
 #pragma unroll
       for (int dd = 0; dd < 4; ++dd) {
         uint32_t hh, ll;
-        act2(Q[T][O][8 * e + 2 * dd], Q[T][O][8 * e + 2 * dd + 1], hh, ll);
+        x3::split_pair(r[8 * e + 2 * dd], r[8 * e + 2 * dd + 1], hh, ll);
         // 224 of the 256 operand registers in AGPRs, beside hidden layer 2's two accumulators; the last
         // two k-steps of tile B (32 registers) in VGPRs
         if constexpr (T == 1 && O == OT - 1) {
@@ -375,11 +382,19 @@ struct PWave {
   // activate registers 4 part .. 4 part + 3 of hidden layer 2's output tile and add their output-row terms
   template <int T, int PART>
   __device__ __forceinline__ void h2_out(const f32x4 (&ow)[4]) {
+    // the four r-form activations stage by stage (exp2, add, rcp), so no instruction waits on the one before it
+    // (a transcendental's result read by the next instruction costs a wait state)
+    float r[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) r[m] = __builtin_amdgcn_exp2f(acc[T][4 * PART + m]);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) r[m] = 1.0f + r[m];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) r[m] = __builtin_amdgcn_rcpf(r[m]);
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
-      const float r = x3::x3_act_r(acc[T][4 * PART + m]);
 #pragma unroll
-      for (int k = 0; k < D; ++k) aP[T][k] = __builtin_fmaf(ow[k][m], r, aP[T][k]);
+      for (int k = 0; k < D; ++k) aP[T][k] = __builtin_fmaf(ow[k][m], r[m], aP[T][k]);
     }
 #pragma unroll
     for (int k = 0; k < D; ++k) touch(aP[T][k]);
