@@ -416,9 +416,14 @@ __device__ __forceinline__ bool out_of_range(const float (&v)[NV]) {
   for (int n = 0; n < NV; ++n) o |= __builtin_fabsf(v[n]) > 65504.0f;  // (false for NaN: a lost hand-over)
   return o;
 }
+// (compare-and-swap from 0: a hand-over timeout already recorded -- its NaN state would also read as out of
+// range -- keeps its own code)
 __device__ __forceinline__ void report_range(bool oor, unsigned* err, int lane) {
-  if (__builtin_amdgcn_ballot_w64(oor) != 0 && lane == 0)
-    __hip_atomic_store(err, kErrRange, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (__builtin_amdgcn_ballot_w64(oor) != 0 && lane == 0) {
+    unsigned expected = 0u;
+    __hip_atomic_compare_exchange_strong(err, &expected, kErrRange, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // ---------------------------------------------------------------------------- sampler kernel

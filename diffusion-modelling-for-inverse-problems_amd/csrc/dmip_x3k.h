@@ -299,7 +299,10 @@ __global__ void __launch_bounds__(KWaves<NT>::NWV * 64, KWaves<NT>::NWV / 4) x3k
   const size_t noise_step = (size_t)gridDim.y * p.n_chains * D;
 
   uint64_t ph[6] = {0, 0, 0, 0, 0, 0};  // DIAG & 2: cycles per phase (L1, H1, H2, output, EM, barrier waits)
-  bool oor = false;                      // a layer-1 input out of the split's range (x3::report_range)
+  // a chain state out of the split's range (x3::report_range), checked on each segment's final state: an
+  // input beyond fp16's range splits into inf / NaN halves, whose NaN the network carries to every later
+  // step (a per-step check held registers in the step loop and pushed a chain's RNG word to scratch)
+  bool oor = false;
   for (int sgi = 0; sgi < sched.n_seg; ++sgi) {
     const Seg sg = sched.segment(sgi);
     long long c_loc[NT];
@@ -361,7 +364,6 @@ __global__ void __launch_bounds__(KWaves<NT>::NWV * 64, KWaves<NT>::NWV / 4) x3k
           for (int k = 0; k < D; ++k) v[k] = x[t][k];
           v[NV - 1] = cf.tau;
           x3::l1_operand<NV, 1>(v, g, b1[t]);
-          oor |= x3::out_of_range(v);
         }
 #pragma unroll
         for (int o = 0; o < ST; ++o) {
@@ -446,6 +448,10 @@ __global__ void __launch_bounds__(KWaves<NT>::NWV * 64, KWaves<NT>::NWV / 4) x3k
         }
       }
     }
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int k = 0; k < D; ++k) oor |= !(__builtin_fabsf(x[t][k]) <= 65504.0f);  // NaN included
     if (sg.kind == 1) {  // hand the job over to the next wave of the grid
       const size_t slot = (size_t)yi * n_waves + gw;
       float* dst = p.xfer + slot * (size_t)(NT * XT);
