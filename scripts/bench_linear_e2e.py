@@ -8,7 +8,9 @@ shuffled batches of 1000 with fresh observation noise (datasets.py:44-54) = 135,
 `evaluate` (main_diffusion_linear.py:53-137): the first 100 test ys, 10 repeats x 30,000 posterior samples
 (200 SDE steps) against the analytic Gaussian posterior (KL2 of 75x75 histograms, NLPD, score MSE at t=0).
 The config file itself is not read (the reference tree is not on the GPU box); its values are restated here.
-    python scripts/bench_linear_e2e.py [--epochs 1500] [--n-y 100] [--n 30000]"""
+With --fixture: no training; the CPU-trained fixture CDE [64]^3 (tests/golden/ckpt_lin.npz, DSMLoss with uniform t,
+make_golden.py) is evaluated the same way, as the control for the trained model's scores.
+    python scripts/bench_linear_e2e.py [--epochs 1500] [--n-y 100] [--n 30000] [--fixture]"""
 import argparse
 import importlib
 import json
@@ -36,6 +38,7 @@ def main():
     ap.add_argument("--n-y", type=int, default=CONFIG["n_samples_y"])
     ap.add_argument("--n", type=int, default=CONFIG["n_samples_x"])
     ap.add_argument("--repeats", type=int, default=CONFIG["n_repeats"])
+    ap.add_argument("--fixture", action="store_true", help="evaluate the CPU-trained fixture checkpoint only")
     a = ap.parse_args()
     from sklearn.model_selection import train_test_split
     pkg = importlib.import_module("diffusion-modelling-for-inverse-problems_amd")
@@ -54,7 +57,13 @@ def main():
     ys = f(xs)
     x_train, x_test, y_train, y_test = train_test_split(xs.cpu(), ys.cpu(), train_size=CONFIG["train_size"],
                                                         random_state=CONFIG["random_state"])
-    model, loss_fn = fac.get_model_from_args(CONFIG, vars(f), f.score_posterior, f)
+    cfg = dict(CONFIG, hidden_layers=[64] * 3) if a.fixture else CONFIG
+    model, loss_fn = fac.get_model_from_args(cfg, vars(f), f.score_posterior, f)
+    if a.fixture:
+        sys.path.insert(0, __import__("os").path.join(ROOT, "tests"))
+        from conftest import state_from_npz
+        model.sde.a.load_state_dict(state_from_npz(np.load(__import__("os").path.join(ROOT, "tests", "golden", "ckpt_lin.npz"))))
+        a.epochs = 0
     model.sde.a.to(dev)
     opt = torch.optim.Adam(model.sde.a.parameters(), lr=CONFIG["lr"])
     x_train, y_train = x_train.to(dev), y_train.to(dev)
@@ -83,7 +92,8 @@ def main():
         t_ev = time.perf_counter() - t0
     print(json.dumps({
         "metric": "reference linear configuration trained and evaluated on one GPU",
-        "config": {k: CONFIG[k] for k in ("hidden_layers", "loss_fn", "lam", "lam2", "lr", "batch_size")},
+        "config": {k: cfg[k] for k in ("hidden_layers", "loss_fn", "lam", "lam2", "lr", "batch_size")},
+        "model": "CPU-trained fixture CDE [64]^3 (tests/golden/ckpt_lin.npz, DSMLoss)" if a.fixture else "trained here",
         "epochs": a.epochs, "optimizer_steps": n_steps, "fused_steps": fused, "train_s": t_train,
         "train_samples_per_s": n_steps * CONFIG["batch_size"] / t_train, "loss_trace": losses,
         "evaluate": {"n_y": a.n_y, "n_samples_x": a.n, "n_repeats": a.repeats, "sde_steps": 200,
