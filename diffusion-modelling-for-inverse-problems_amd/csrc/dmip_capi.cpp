@@ -428,12 +428,20 @@ int pack_x3_net(dmip_mlp* net, const float* const* weights, const float* const* 
     pack_x3_layer(weights[li], biases[li], W, W, ST, kC, img, bias.data() + (size_t)li * W);
     const char* b = (const char*)img.data();
     stream.insert(stream.end(), b, b + img.size() * 2);
-    if (kmajor)
+    if (kmajor && li == 1)
       for (int q = 0; q < KQ; ++q)
         for (int o = 0; o < ST; ++o) {
           const char* f = b + (((size_t)o * KQ + q) * 2) * 1024;
           kstream.insert(kstream.end(), f, f + 2048);
         }
+    if (kmajor && li == 2)  // two output halves, each k-major: chunk (h, q2) = k-steps 2 q2, 2 q2 + 1 of tiles 8h..8h+7
+      for (int h = 0; h < 2; ++h)
+        for (int q2 = 0; q2 < KQ / 2; ++q2)
+          for (int kk = 0; kk < 2; ++kk)
+            for (int o = 8 * h; o < 8 * h + 8; ++o) {
+              const char* f = b + (((size_t)o * KQ + 2 * q2 + kk) * 2) * 1024;
+              kstream.insert(kstream.end(), f, f + 2048);
+            }
   }
   const int orows = OUT < 16 ? OUT : 16;  // the samplers read output rows 0..15 (the x rows)
   pack_x3_layer(weights[L], biases[L], orows, W, 1, 1.0, img, bias.data() + (size_t)L * W);

@@ -16,6 +16,9 @@
 //   * 16 chunks per step on a 4-slot ring: chunk k of a step is always in slot k % 4, so every ring
 //     address, source offset and DMA destination is a compile-time constant; the DMA is
 //     buffer_load_dwordx4 ... lds with the image offset in an SGPR (no per-lane address arithmetic);
+//   * hidden layer 2 streams as two output halves (each k-major, two k-steps per chunk), so half 1 runs the
+//     output layer over half 0's finished units beside its MFMAs (layer2); ring fragments are read one o-step
+//     ahead, and the chains' RNG states wait in LDS through the step (the registers that layout needs);
 //   * the output layer (3 rows) is LDS-resident as one fragment per k-step: rows 0..D-1 hold W_hi, rows
 //     4..4+D-1 W_lo, so A . h_hi yields W_hi h_hi and W_lo h_hi in lane groups 0 and 1 and A . h_lo yields
 //     W_hi h_lo in group 0 (8 KiB instead of a 16-row hi + lo chunk).
@@ -36,6 +39,7 @@ constexpr int W = 256, ST = 16, KQ = 8, NH = 2;  // [256]*3: layer 1 + two W x W
 constexpr int CHUNK = 32768;                     // k-step q of a W x W layer: 16 tiles x (hi, lo) x 1 KiB
 constexpr int NCHUNK = NH * KQ;                  // ring chunks per step
 constexpr int R = 4;                             // ring slots
+constexpr int PF = 1;                            // ring fragment pairs read ahead (o-steps)
 // waves per workgroup: one per SIMD for 2-3 chain tiles per wave (up to 512 registers), two per SIMD for
 // one tile per wave (<= 256 registers: each wave's VALU chains issue between the other's MFMAs)
 template <int NT>
@@ -52,7 +56,10 @@ struct KLay {
   static constexpr int BF = (NH + 1) * W + 16;
   static constexpr int BIAS_BYTES = (BF * 4 + 15) / 16 * 16;
   static constexpr int RING = BIAS + BIAS_BYTES;
-  static constexpr int TOTAL = RING + R * CHUNK;
+  // the chains' RNG states, parked in LDS while the network is evaluated ([wave][tile][word][16 chains]): 12
+  // registers fewer through the step
+  static constexpr int RNGP = RING + R * CHUNK, RNGP_BYTES = 3072;
+  static constexpr int TOTAL = RNGP + RNGP_BYTES;
 };
 static_assert(KLay::TOTAL <= 160 * 1024, "LDS budget");
 
@@ -90,6 +97,7 @@ struct KEngine {
   static constexpr int NWV = KWaves<NT>::NWV, PPW = KWaves<NT>::PPW;
   char* lds;
   const char* ring_lane;  // ring base + 16 lane
+  const char* out_lane;   // resident output fragments + 16 lane
   __amdgpu_buffer_rsrc_t rs;
   unsigned voff;          // this wave's DMA pieces: w PPW KiB + 16 lane
   int w, g;
@@ -116,7 +124,7 @@ struct KEngine {
   // chunk K are read ahead at the end of chunk K - 1 (no LDS latency bubble at a chunk start), and the
   // barrier waits on nothing but the other waves (no lgkmcnt(0): every read of a refilled slot was consumed
   // by an MFMA whose operand wait has retired it).
-  __device__ __forceinline__ void start(u32x4 (&fpre)[2][2]) const {
+  __device__ __forceinline__ void start(u32x4 (&fpre)[PF][2]) const {
     if constexpr (!(DIAG & 1)) {
       issue<0, 0>();
       issue<1, 1>();
@@ -125,12 +133,12 @@ struct KEngine {
     }
     barrier();
     const x3::lds_cptr b0 = (x3::lds_cptr)ring_lane;
-    fpre[0][0] = x3::lds_rd<0>(b0);
-    fpre[0][1] = x3::lds_rd<1024>(b0);
-    fpre[1][0] = x3::lds_rd<2048>(b0);
-    fpre[1][1] = x3::lds_rd<3072>(b0);
-    x3::lds_wait2<0>(fpre[1][0], fpre[1][1]);
-    x3::lds_wait2<0>(fpre[0][0], fpre[0][1]);
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {
+      fpre[i][0] = x3::lds_rd<0>(b0 + i * 2048);
+      fpre[i][1] = x3::lds_rd<1024>(b0 + i * 2048);
+      x3::lds_wait2<0>(fpre[i][0], fpre[i][1]);
+    }
   }
 
   __device__ __forceinline__ void barrier() const {
@@ -164,7 +172,7 @@ struct KEngine {
   // fragment pairs of the layer's first chunk on entry, of the next chunk on exit.
   template <int LI, bool IN_L1>
   __device__ __forceinline__ void layer(const f32x4 (&In)[NT][ST], f32x4 (&Out)[NT][ST], u32x4 (&Hh)[NT],
-                                        u32x4 (&Hl)[NT], u32x4 (&fpre)[2][2]) const {
+                                        u32x4 (&Hl)[NT], u32x4 (&fpre)[PF][2]) const {
 #pragma unroll
     for (int o = 0; o < ST; ++o) {
       const f32x4 b = bias4(LI, o);
@@ -176,20 +184,20 @@ struct KEngine {
 
   template <int LI, bool IN_L1, int Q>
   __device__ __forceinline__ void chunk(const f32x4 (&In)[NT][ST], f32x4 (&Out)[NT][ST], u32x4 (&Hh)[NT],
-                                        u32x4 (&Hl)[NT], u32x4 (&fpre)[2][2]) const {
+                                        u32x4 (&Hl)[NT], u32x4 (&fpre)[PF][2]) const {
     if constexpr (Q < KQ) {
       constexpr int K = (LI - 1) * KQ + Q;  // chunk index in the step
       const x3::lds_cptr base = (x3::lds_cptr)(ring_lane + (K % R) * CHUNK);
       const x3::lds_cptr nbase = (x3::lds_cptr)(ring_lane + ((K + 1) % R) * CHUNK);
       u32x4 Nh[NT], Nl[NT];
-      u32x4 f[3][2];
-      f[0][0] = fpre[0][0], f[0][1] = fpre[0][1];
-      f[1][0] = fpre[1][0], f[1][1] = fpre[1][1];
+      u32x4 f[PF + 1][2];
+#pragma unroll
+      for (int i = 0; i < PF; ++i) f[i][0] = fpre[i][0], f[i][1] = fpre[i][1];
       ostep<LI, IN_L1, Q, 0>(base, nbase, In, Out, Hh, Hl, Nh, Nl, f, fpre);
       // the next chunk's first fragments (read at o-steps 14 and 15) are complete before they leave the
       // chunk: an asm load's registers must not be copied before its data lands
-      x3::lds_wait2<0>(fpre[0][0], fpre[0][1]);
-      x3::lds_wait2<0>(fpre[1][0], fpre[1][1]);
+#pragma unroll
+      for (int i = 0; i < PF; ++i) x3::lds_wait2<0>(fpre[i][0], fpre[i][1]);
       if constexpr (Q + 1 < KQ) {
 #pragma unroll
         for (int t = 0; t < NT; ++t) Hh[t] = Nh[t], Hl[t] = Nl[t];
@@ -207,23 +215,16 @@ struct KEngine {
   template <int LI, bool IN_L1, int Q, int O>
   __device__ __forceinline__ void ostep(x3::lds_cptr base, x3::lds_cptr nbase, const f32x4 (&In)[NT][ST],
                                         f32x4 (&Out)[NT][ST], const u32x4 (&Hh)[NT], const u32x4 (&Hl)[NT],
-                                        u32x4 (&Nh)[NT], u32x4 (&Nl)[NT], u32x4 (&f)[3][2],
-                                        u32x4 (&fpre)[2][2]) const {
+                                        u32x4 (&Nh)[NT], u32x4 (&Nl)[NT], u32x4 (&f)[PF + 1][2],
+                                        u32x4 (&fpre)[PF][2]) const {
     if constexpr (O < ST) {
       constexpr int K = (LI - 1) * KQ + Q;
-      if constexpr (O + 2 < ST) {
-        f[(O + 2) % 3][0] = x3::lds_rd<(O + 2) * 2048>(base);
-        f[(O + 2) % 3][1] = x3::lds_rd<(O + 2) * 2048 + 1024>(base);
-      } else {  // the next chunk's fragment O + 2 - 16 (its barrier has passed at O = 8)
-        fpre[O + 2 - ST][0] = x3::lds_rd<(O + 2 - ST) * 2048>(nbase);
-        fpre[O + 2 - ST][1] = x3::lds_rd<(O + 2 - ST) * 2048 + 1024>(nbase);
-      }
-      x3::lds_wait2<4>(f[O % 3][0], f[O % 3][1]);  // two younger fragment pairs are always in flight
+      ring_pre<O>(base, nbase, f, fpre);
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
-        Out[t][O] = mfma16(f[O % 3][0], Hl[t], Out[t][O]);
-        Out[t][O] = mfma16(f[O % 3][1], Hh[t], Out[t][O]);
-        Out[t][O] = mfma16(f[O % 3][0], Hh[t], Out[t][O]);
+        Out[t][O] = mfma16(f[O % (PF + 1)][0], Hl[t], Out[t][O]);
+        Out[t][O] = mfma16(f[O % (PF + 1)][1], Hh[t], Out[t][O]);
+        Out[t][O] = mfma16(f[O % (PF + 1)][0], Hh[t], Out[t][O]);
       }
       if constexpr (Q + 1 < KQ && O < 4 * NT) {
         constexpr int t = O / 4, d = O % 4;
@@ -236,16 +237,142 @@ struct KEngine {
         Nh[t][d] = h;
         Nl[t][d] = l;
       }
-      if constexpr (O == 8) sync_mid<(K + 1) % NCHUNK>();
-      if constexpr (!(DIAG & 1) && PPW == 8 && O == 9) {
-        issue_piece<(K + R - 1) % NCHUNK, (K + R - 1) % R, 0>();
-        issue_piece<(K + R - 1) % NCHUNK, (K + R - 1) % R, 1>();
-      }
-      if constexpr (!(DIAG & 1) && PPW == 8 && O >= 10)
-        issue_piece<(K + R - 1) % NCHUNK, (K + R - 1) % R, O - 8>();
-      if constexpr (!(DIAG & 1) && PPW == 4 && O >= 9 && O < 13)
-        issue_piece<(K + R - 1) % NCHUNK, (K + R - 1) % R, O - 9>();
+      ring_post<K, O>();
       ostep<LI, IN_L1, Q, O + 1>(base, nbase, In, Out, Hh, Hl, Nh, Nl, f, fpre);
+    }
+  }
+
+  // the ring's part of o-step O: the fragment pair two o-steps ahead (across the chunk boundary at O = 14, 15:
+  // the next chunk's, whose barrier has passed at O = 8), then the wait for this o-step's pair
+  template <int O>
+  __device__ __forceinline__ void ring_pre(x3::lds_cptr base, x3::lds_cptr nbase, u32x4 (&f)[PF + 1][2],
+                                           u32x4 (&fpre)[PF][2]) const {
+    if constexpr (O + PF < ST) {
+      f[(O + PF) % (PF + 1)][0] = x3::lds_rd<(O + PF) * 2048>(base);
+      f[(O + PF) % (PF + 1)][1] = x3::lds_rd<(O + PF) * 2048 + 1024>(base);
+    } else {
+      fpre[O + PF - ST][0] = x3::lds_rd<(O + PF - ST) * 2048>(nbase);
+      fpre[O + PF - ST][1] = x3::lds_rd<(O + PF - ST) * 2048 + 1024>(nbase);
+    }
+    // PF younger fragment pairs are in flight (an output-fragment read between them only makes it stricter)
+    x3::lds_wait2<2 * PF>(f[O % (PF + 1)][0], f[O % (PF + 1)][1]);
+  }
+  // B(K + 1) at O = 8; LDS-DMA pieces of chunk K + 3 at O = 9..15
+  template <int K, int O>
+  __device__ __forceinline__ void ring_post() const {
+    if constexpr (O == 8) sync_mid<(K + 1) % NCHUNK>();
+    if constexpr (!(DIAG & 1) && PPW == 8 && O == 9) {
+      issue_piece<(K + R - 1) % NCHUNK, (K + R - 1) % R, 0>();
+      issue_piece<(K + R - 1) % NCHUNK, (K + R - 1) % R, 1>();
+    }
+    if constexpr (!(DIAG & 1) && PPW == 8 && O >= 10)
+      issue_piece<(K + R - 1) % NCHUNK, (K + R - 1) % R, O - 8>();
+    if constexpr (!(DIAG & 1) && PPW == 4 && O >= 9 && O < 13)
+      issue_piece<(K + R - 1) % NCHUNK, (K + R - 1) % R, O - 9>();
+  }
+
+  // ---- hidden layer 2 in two output halves (ring chunks 8..11: output tiles 0..7; 12..15: tiles 8..15), each
+  // k-major with two k-steps per chunk: o-step O of chunk (H, Q2) is tile 8 H + O % 8 at k-step 2 Q2 + O / 8.
+  // Half 0 activates the layer's input just in time (k-step k + 1 beside k-step k's eight o-steps) and keeps
+  // every k-step's operands; half 1 reuses them and runs the output layer's first four k-steps (units 0..127,
+  // half 0's finished tiles) beside its MFMAs, a pair of units per o-step. Each output element still
+  // accumulates its k-steps in ascending order, and the output layer its k-steps too: bit-identical to the
+  // one-pass layer. What stays outside the ring is the output layer's last four k-steps.
+  __device__ __forceinline__ void layer2(const f32x4 (&In)[NT][ST], f32x4 (&Out)[NT][ST], const u32x4 (&Hh)[NT],
+                                         const u32x4 (&Hl)[NT], u32x4 (&fpre)[PF][2], f32x4 (&oH)[NT],
+                                         f32x4 (&oL)[NT]) const {
+    u32x4 Ah[KQ][NT], Al[KQ][NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) Ah[0][t] = Hh[t], Al[0][t] = Hl[t];
+#pragma unroll
+    for (int o = 0; o < ST / 2; ++o) {
+      const f32x4 b = bias4(2, o);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) Out[t][o] = b;
+    }
+    u32x4 fo, eh, el;
+    chunk2<0, 0>(In, Out, Ah, Al, fpre, oH, oL, fo, eh, el);
+#pragma unroll
+    for (int o = ST / 2; o < ST; ++o) {
+      const f32x4 b = bias4(2, o);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) Out[t][o] = b;
+    }
+    chunk2<1, 0>(In, Out, Ah, Al, fpre, oH, oL, fo, eh, el);
+  }
+
+  template <int H, int Q2>
+  __device__ __forceinline__ void chunk2(const f32x4 (&In)[NT][ST], f32x4 (&Out)[NT][ST], u32x4 (&Ah)[KQ][NT],
+                                         u32x4 (&Al)[KQ][NT], u32x4 (&fpre)[PF][2], f32x4 (&oH)[NT],
+                                         f32x4 (&oL)[NT], u32x4& fo, u32x4& eh, u32x4& el) const {
+    if constexpr (Q2 < KQ / 2) {
+      constexpr int K = KQ + (KQ / 2) * H + Q2;
+      const x3::lds_cptr base = (x3::lds_cptr)(ring_lane + (K % R) * CHUNK);
+      const x3::lds_cptr nbase = (x3::lds_cptr)(ring_lane + ((K + 1) % R) * CHUNK);
+      u32x4 f[PF + 1][2];
+#pragma unroll
+      for (int i = 0; i < PF; ++i) f[i][0] = fpre[i][0], f[i][1] = fpre[i][1];
+      ostep2<H, Q2, 0>(base, nbase, In, Out, Ah, Al, f, fpre, oH, oL, fo, eh, el);
+#pragma unroll
+      for (int i = 0; i < PF; ++i) x3::lds_wait2<0>(fpre[i][0], fpre[i][1]);
+      chunk2<H, Q2 + 1>(In, Out, Ah, Al, fpre, oH, oL, fo, eh, el);
+    }
+  }
+
+  template <int H, int Q2, int O>
+  __device__ __forceinline__ void ostep2(x3::lds_cptr base, x3::lds_cptr nbase, const f32x4 (&In)[NT][ST],
+                                         f32x4 (&Out)[NT][ST], u32x4 (&Ah)[KQ][NT], u32x4 (&Al)[KQ][NT],
+                                         u32x4 (&f)[PF + 1][2], u32x4 (&fpre)[PF][2], f32x4 (&oH)[NT], f32x4 (&oL)[NT],
+                                         u32x4& fo, u32x4& eh, u32x4& el) const {
+    if constexpr (O < ST) {
+      constexpr int K = KQ + (KQ / 2) * H + Q2;
+      constexpr int o = (ST / 2) * H + O % 8, k = 2 * Q2 + O / 8;
+      ring_pre<O>(base, nbase, f, fpre);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        Out[t][o] = mfma16(f[O % (PF + 1)][0], Al[k][t], Out[t][o]);
+        Out[t][o] = mfma16(f[O % (PF + 1)][1], Ah[k][t], Out[t][o]);
+        Out[t][o] = mfma16(f[O % (PF + 1)][0], Ah[k][t], Out[t][o]);
+      }
+      if constexpr (H == 0 && k + 1 < KQ) {  // pairs O % 8 and 8 + O % 8 of k-step k + 1
+        act_pair<k + 1, O % 8>(In, Ah, Al);
+        act_pair<k + 1, 8 + O % 8>(In, Ah, Al);
+      }
+      if constexpr (H == 1) {  // output-layer pair G = 16 Q2 + O: unit (q, t) = (G / 4 / NT, G / 4 % NT), pair G % 4
+        constexpr int G = 16 * Q2 + O, u = G / 4, d = G % 4, q = u / NT, t = u % NT;
+        if constexpr (q < KQ / 2) {
+          // the unit's output fragment, read at its first pair (after this o-step's ring reads) and waited
+          // for at its last: the three later o-steps' ring reads (two each) are younger
+          if constexpr (d == 0) fo = x3::lds_rd<q * 1024>((x3::lds_cptr)out_lane);
+          const f32x4& z = Out[t][2 * q + d / 2];
+          constexpr int e = 2 * (d % 2);
+          uint32_t h, l;
+          x3::split_pair(x3::x3_act_r(z[e]), x3::x3_act_r(z[e + 1]), h, l);
+          eh[d] = h;
+          el[d] = l;
+          if constexpr (d == 3) {
+            x3::lds_wait1<6>(fo);
+            oH[t] = mfma16(fo, eh, oH[t]);
+            oL[t] = mfma16(fo, el, oL[t]);
+          }
+        }
+      }
+      ring_post<K, O>();
+      ostep2<H, Q2, O + 1>(base, nbase, In, Out, Ah, Al, f, fpre, oH, oL, fo, eh, el);
+    }
+  }
+
+  // activate operand pair P = (t, d) of k-step k (hidden layer 2's input) into Ah[k][t][d], Al[k][t][d]
+  template <int k, int P>
+  __device__ __forceinline__ void act_pair(const f32x4 (&In)[NT][ST], u32x4 (&Ah)[KQ][NT],
+                                           u32x4 (&Al)[KQ][NT]) const {
+    if constexpr (P < 4 * NT) {
+      constexpr int t = P / 4, d = P % 4, e = 2 * (d % 2);
+      const f32x4& z = In[t][2 * k + d / 2];
+      uint32_t h, l;
+      x3::split_pair(x3::x3_act_r(z[e]), x3::x3_act_r(z[e + 1]), h, l);
+      Ah[k][t][d] = h;
+      Al[k][t][d] = l;
     }
   }
 };
@@ -269,6 +396,7 @@ __global__ void __launch_bounds__(KWaves<NT>::NWV * 64, KWaves<NT>::NWV / 4) x3k
   KEngine<D, NT, NOISE, DIAG> eng;
   eng.lds = lds;
   eng.ring_lane = lds + L::RING + lane * 16;
+  eng.out_lane = lds + L::OUT + lane * 16;
   eng.rs = __builtin_amdgcn_make_buffer_rsrc((void*)p.net[0].kstream, 0, NCHUNK * CHUNK, 0x00020000);
   eng.voff = (unsigned)(w * PPW * 1024 + lane * 16);
   eng.w = w;
@@ -284,7 +412,7 @@ __global__ void __launch_bounds__(KWaves<NT>::NWV * 64, KWaves<NT>::NWV / 4) x3k
     for (int i = threadIdx.x; i < L::BF; i += NWV * 64) bl[i] = i < W ? p.bias_y[(size_t)yi * W + i] : p.net[0].bias[i];
     __syncthreads();
   }
-  u32x4 fpre[2][2];  // the first fragment pairs of the next ring chunk (read ahead across phases)
+  u32x4 fpre[PF][2];  // the first fragment pairs of the next ring chunk (read ahead across phases)
   eng.start(fpre);
   const char* l1_lane = lds + L::L1 + lane * 16;
   const char* out_lane = lds + L::OUT + lane * 16;
@@ -312,8 +440,20 @@ __global__ void __launch_bounds__(KWaves<NT>::NWV * 64, KWaves<NT>::NWV / 4) x3k
       c_loc[t] = (long long)(sg.job >= 0 ? sg.job : 0) * JC + 16 * t + j;
       valid[t] = sg.job >= 0 && c_loc[t] < p.n_chains;
     }
-    Rng rng[NT];
     float x[NT][D];
+    // wave-private LDS slots of the tiles' RNG states: lane group 0 writes, every lane reads its chain's words
+    uint32_t* rng_park = (uint32_t*)(lds + L::RNGP) + w * NT * 64;
+    static_assert(KWaves<NT>::NWV * NT * 256 <= KLay::RNGP_BYTES, "RNG parking space");
+    auto park = [&](int t, const Rng& r) {
+      if (g == 0) {
+        uint32_t* d = rng_park + t * 64;
+        d[j] = r.s0, d[16 + j] = r.s1, d[32 + j] = r.s2, d[48 + j] = r.s3;
+      }
+    };
+    auto unpark = [&](int t) {
+      const uint32_t* d = rng_park + t * 64;
+      return Rng{d[j], d[16 + j], d[32 + j], d[48 + j]};
+    };
     if (sg.kind == 2) {  // resume the job the previous wave of the grid handed over
       const size_t slot = (size_t)yi * n_waves + gw - 1;
       const bool lost = handover_wait(p.xflag + slot, p.spin_limit, p.err, kErrHandover, lane);
@@ -324,23 +464,22 @@ __global__ void __launch_bounds__(KWaves<NT>::NWV * 64, KWaves<NT>::NWV / 4) x3k
         const float* st = src + t * (D + 4) * 16;
 #pragma unroll
         for (int k = 0; k < D; ++k) x[t][k] = lost ? __builtin_nanf("") : st[k * 16 + j];
-        rng[t].s0 = __float_as_uint(st[(D + 0) * 16 + j]);
-        rng[t].s1 = __float_as_uint(st[(D + 1) * 16 + j]);
-        rng[t].s2 = __float_as_uint(st[(D + 2) * 16 + j]);
-        rng[t].s3 = __float_as_uint(st[(D + 3) * 16 + j]);
+        park(t, Rng{__float_as_uint(st[(D + 0) * 16 + j]), __float_as_uint(st[(D + 1) * 16 + j]),
+                    __float_as_uint(st[(D + 2) * 16 + j]), __float_as_uint(st[(D + 3) * 16 + j])});
       }
     } else {
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
-        rng[t] = rng_init(p.seed, (uint64_t)(p.chain_offset + c_loc[t]), (uint64_t)yi);
+        Rng rng = rng_init(p.seed, (uint64_t)(p.chain_offset + c_loc[t]), (uint64_t)yi);
         float n0[D];
         if constexpr (NOISE) {
           const float* src = p.noise + ((size_t)yi * p.n_chains + (valid[t] ? c_loc[t] : 0)) * D;
 #pragma unroll
           for (int k = 0; k < D; ++k) n0[k] = src[k];
         } else {
-          rng_normals<D>(rng[t], n0);
+          rng_normals<D>(rng, n0);
         }
+        park(t, rng);
 #pragma unroll
         for (int k = 0; k < D; ++k) x[t][k] = __fadd_rn(__fmul_rn(n0[k], p.stdv), p.mean);
       }
@@ -385,18 +524,22 @@ __global__ void __launch_bounds__(KWaves<NT>::NWV * 64, KWaves<NT>::NWV / 4) x3k
       if constexpr (DIAG & 2) t2 = stamp(), ph[1] += t2 - t1;
 #pragma unroll
       for (int t = 0; t < NT; ++t) act_kstep<false>(Q[t][0], Q[t][1], Hh[t], Hl[t]);
+      // ---- hidden layer 2 (ring chunks 8..15, two output halves) with the output layer's first half
+      // (resident output fragments: rows 0..D-1 W_hi, 4..4+D-1 W_lo)
       f32x4 P2[NT][ST];
-      eng.template layer<2, false>(Q, P2, Hh, Hl, fpre);
-      uint64_t t3 = 0;
-      if constexpr (DIAG & 2) t3 = stamp(), ph[2] += t3 - t2;
-      // ---- output layer (resident): rows 0..D-1 W_hi, 4..4+D-1 W_lo
       f32x4 oH[NT], oL[NT];
       {
         const f32x4 bo = g == 0 ? eng.bias4(NH + 1, 0) : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
         for (int t = 0; t < NT; ++t) oH[t] = bo, oL[t] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+      }
+      eng.layer2(Q, P2, Hh, Hl, fpre, oH, oL);
+      uint64_t t3 = 0;
+      if constexpr (DIAG & 2) t3 = stamp(), ph[2] += t3 - t2;
+      // ---- the output layer's second half (units 128..255)
+      {
 #pragma unroll
-        for (int q = 0; q < KQ; ++q) {
+        for (int q = KQ / 2; q < KQ; ++q) {
           const u32x4 fo = *(const u32x4*)(out_lane + q * 1024);
 #pragma unroll
           for (int t = 0; t < NT; ++t) {
@@ -425,7 +568,9 @@ __global__ void __launch_bounds__(KWaves<NT>::NWV * 64, KWaves<NT>::NWV / 4) x3k
 #pragma unroll
           for (int k = 0; k < D; ++k) xi[k] = src[k];
         } else {
-          rng_normals<D>(rng[t], xi);
+          Rng rng = unpark(t);
+          rng_normals<D>(rng, xi);
+          park(t, rng);
         }
 #pragma unroll
         for (int k = 0; k < D; ++k) x[t][k] = em_update(x[t][k], a[k], xi[k], cf, p.delta, p.sqrt_delta);
@@ -461,10 +606,11 @@ __global__ void __launch_bounds__(KWaves<NT>::NWV * 64, KWaves<NT>::NWV / 4) x3k
           float* st = dst + t * (D + 4) * 16;
 #pragma unroll
           for (int k = 0; k < D; ++k) st[k * 16 + j] = x[t][k];
-          st[(D + 0) * 16 + j] = __uint_as_float(rng[t].s0);
-          st[(D + 1) * 16 + j] = __uint_as_float(rng[t].s1);
-          st[(D + 2) * 16 + j] = __uint_as_float(rng[t].s2);
-          st[(D + 3) * 16 + j] = __uint_as_float(rng[t].s3);
+          const Rng rng = unpark(t);
+          st[(D + 0) * 16 + j] = __uint_as_float(rng.s0);
+          st[(D + 1) * 16 + j] = __uint_as_float(rng.s1);
+          st[(D + 2) * 16 + j] = __uint_as_float(rng.s2);
+          st[(D + 3) * 16 + j] = __uint_as_float(rng.s3);
         }
       }
       handover_publish(p.xflag + slot, lane, p.debug_flags);
