@@ -168,7 +168,7 @@ struct KEngine {
 
   // one W x W layer, k-major: In (f32 pre-activations of the previous layer, NT x 16 tiles) -> Out.
   // Hh/Hl hold k-step 0's operands on entry (activated by the caller); k-step q + 1's are activated
-  // from In during chunk q, a slice per output tile beside that tile's MFMAs. fpre: the first two
+  // from In during chunk q, a slice per output tile beside that tile's MFMAs. fpre: the first PF
   // fragment pairs of the layer's first chunk on entry, of the next chunk on exit.
   template <int LI, bool IN_L1>
   __device__ __forceinline__ void layer(const f32x4 (&In)[NT][ST], f32x4 (&Out)[NT][ST], u32x4 (&Hh)[NT],
@@ -194,7 +194,7 @@ struct KEngine {
 #pragma unroll
       for (int i = 0; i < PF; ++i) f[i][0] = fpre[i][0], f[i][1] = fpre[i][1];
       ostep<LI, IN_L1, Q, 0>(base, nbase, In, Out, Hh, Hl, Nh, Nl, f, fpre);
-      // the next chunk's first fragments (read at o-steps 14 and 15) are complete before they leave the
+      // the next chunk's first fragments (read at the last PF o-steps) are complete before they leave the
       // chunk: an asm load's registers must not be copied before its data lands
 #pragma unroll
       for (int i = 0; i < PF; ++i) x3::lds_wait2<0>(fpre[i][0], fpre[i][1]);
@@ -206,8 +206,8 @@ struct KEngine {
     }
   }
 
-  // o-step O of chunk K = (LI, Q): tile O's 3 NT MFMAs (fragments read 2 tiles ahead -- across the chunk
-  // boundary at O = 14, 15 -- by explicit ds_read_b128 with counted lgkmcnt waits; left to itself the
+  // o-step O of chunk K = (LI, Q): tile O's 3 NT MFMAs (fragments read PF tiles ahead -- across the chunk
+  // boundary at the last PF o-steps -- by explicit ds_read_b128 with counted lgkmcnt waits; left to itself the
   // compiler hoists all 32 reads to the chunk's top, 128 more registers), beside one slice of the work the
   // chunk carries: the activation of k-step Q + 1's operand pair (t, d) = (O / 4, O % 4) for O < 4 NT;
   // B(K + 1) at O = 8; LDS-DMA pieces of chunk K + 3 at O = 9..15. (The asm reads and waits are scheduling
@@ -242,7 +242,7 @@ struct KEngine {
     }
   }
 
-  // the ring's part of o-step O: the fragment pair two o-steps ahead (across the chunk boundary at O = 14, 15:
+  // the ring's part of o-step O: the fragment pair PF o-steps ahead (across the chunk boundary at the last PF o-steps:
   // the next chunk's, whose barrier has passed at O = 8), then the wait for this o-step's pair
   template <int O>
   __device__ __forceinline__ void ring_pre(x3::lds_cptr base, x3::lds_cptr nbase, u32x4 (&f)[PF + 1][2],
