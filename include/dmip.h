@@ -54,9 +54,11 @@ typedef enum { DMIP_ACT_TANH_TWICE_FIRST = 0, DMIP_ACT_TANH = 1 } dmip_act;
  *                   finite value) and to ~2^-24 absolute below 2^-14 (fp16 subnormals). The scaled weights
  *                   (layer 1 x 2 log2(e), hidden layers x 4 log2(e), output rows x 2) and folded biases must
  *                   fit: a network that does not is refused at sampling time (DMIP_ERR_UNSUPPORTED, "fp16
- *                   range"). Every layer-1 input (chain state x, t; CDiffE's y_t) is checked in the kernel: a
- *                   chain that leaves the range is reported by dmip_device_status ("fp16 range") -- those
- *                   chains are not fp32-accurate. The Python estimators resample with DMIP_PREC_F32 then.
+ *                   range"). The layer-1 inputs (chain state x, t; CDiffE's y_t) are checked in the kernel --
+ *                   at every step, or (the headline CDE engine) on each segment's final state, where an input
+ *                   that left the range shows as non-finite or > 65504: a chain that leaves the range is
+ *                   reported by dmip_device_status ("fp16 range") -- those chains are not fp32-accurate. The
+ *                   Python estimators resample with DMIP_PREC_F32 then.
  * All three draw the same RNG stream per chain, so the modes are comparable chain by chain. */
 typedef enum { DMIP_PREC_BF16 = 0, DMIP_PREC_F32 = 1, DMIP_PREC_F32X3 = 2 } dmip_precision;
 
