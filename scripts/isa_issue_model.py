@@ -1,7 +1,8 @@
 """Static issue-cost model of a sampler kernel's step loop (no GPU): extracts the kernel's gfx950 ISA from a
 libdmip.so and prices every MFMA gap as max(MFMA cycles, 8 + the issue costs of the instructions placed in
 it), with MI355X_MICROARCH.md's per-instruction constants (transcendental 8, other VALU / s_nop / LDS / VMEM
-issue 4, SALU 1). Prints the modelled cycles between consecutive s_barriers (one per ring chunk).
+issue 4, SALU 1). Prints the modelled cycles between consecutive s_barriers (one per ring chunk), then the whole
+step loop (the innermost backward branch enclosing every MFMA of the kernel) with its scratch accesses.
     python scripts/isa_issue_model.py <libdmip.so> <kernel-symbol-substring> [mfma_cycles=16]"""
 import re
 import subprocess
@@ -59,6 +60,32 @@ def model(lines, mc):
     return n, tot + pre
 
 
+def step_loop(L, mc):
+    """(MFMAs, modelled cycles, scratch instructions) of the innermost loop that holds every MFMA."""
+    addr = []
+    for l in L:
+        mm = re.search(r"//\s*([0-9A-F]{12}):", l)
+        addr.append(int(mm.group(1), 16) if mm else None)
+    mf = [i for i, l in enumerate(L) if "v_mfma" in l]
+    best = None
+    for i, l in enumerate(L):
+        mm = re.match(r"\s+s_(cbranch_\w+|branch)\s+(\d+)", l)
+        if not mm or addr[i] is None:
+            continue
+        off = int(mm.group(2))
+        off = off - 65536 if off >= 32768 else off
+        tgt = addr[i] + 4 + off * 4
+        if tgt < addr[i] and tgt in addr:
+            j = addr.index(tgt)
+            if all(j <= x <= i for x in mf) and (best is None or i - j < best[1] - best[0]):
+                best = (j, i)
+    if best is None:
+        return None
+    j, i = best
+    n, c = model(L[j:i], mc)
+    return n, c, sum(1 for l in L[j:i] if "scratch_" in l)
+
+
 def main():
     so, sym = sys.argv[1], sys.argv[2]
     mc = int(sys.argv[3]) if len(sys.argv) > 3 else 16
@@ -70,6 +97,9 @@ def main():
         tot += c
         print(f"{a:6d} mfma {n:4d} modelled {c:6d} (floor {n * mc})")
     print("chunks total", tot)
+    sl = step_loop(L, mc)
+    if sl:
+        print(f"step loop: {sl[0]} MFMAs, modelled {sl[1]} cycles, {sl[2]} scratch instructions")
 
 
 if __name__ == "__main__":
