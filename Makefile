@@ -5,7 +5,7 @@ HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-parameter
 F32OBJS := $(CSRC)/dmip_f32.o $(CSRC)/dmip_f32_cde.o $(CSRC)/dmip_f32_post.o $(CSRC)/dmip_f32_cdiffe.o
-X3OBJS := $(CSRC)/dmip_x3.o $(CSRC)/dmip_x3_cde.o $(CSRC)/dmip_x3_post.o $(CSRC)/dmip_x3_cdiffe.o $(CSRC)/dmip_x3k.o $(CSRC)/dmip_x3p.o
+X3OBJS := $(CSRC)/dmip_x3.o $(CSRC)/dmip_x3_cde.o $(CSRC)/dmip_x3_post.o $(CSRC)/dmip_x3_cdiffe.o $(CSRC)/dmip_x3k.o
 OBJS := $(CSRC)/dmip_kernels.o $(CSRC)/dmip_train.o $(CSRC)/dmip_eval.o $(CSRC)/dmip_surrogate.o $(CSRC)/dmip_gemm.o $(CSRC)/dmip_jets.o $(CSRC)/dmip_step.o $(F32OBJS) $(X3OBJS) $(CSRC)/dmip_capi.o
 HDRS := $(CSRC)/dmip_device.h $(CSRC)/dmip_internal.h include/dmip.h
 
@@ -53,26 +53,30 @@ $(CSRC)/dmip_x3_%.o: $(CSRC)/dmip_x3_%.hip $(CSRC)/dmip_x3.h $(HDRS)
 $(CSRC)/dmip_x3k.o: $(CSRC)/dmip_x3k.hip $(CSRC)/dmip_x3k.h $(CSRC)/dmip_x3.h $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -fno-slp-vectorize -c $< -o $@
 
-# the paired-tile 32x32 fp32x3 CDE engine (width 256, the default at its shape)
-$(CSRC)/dmip_x3p.o: $(CSRC)/dmip_x3p.hip $(CSRC)/dmip_x3p.h $(CSRC)/dmip_x3.h $(HDRS)
-	$(HIPCC) $(HIPFLAGS) -fno-slp-vectorize -c $< -o $@
-
 $(CSRC)/dmip_capi.o: $(CSRC)/dmip_capi.cpp $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(PKG)/libdmip.so: $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(OBJS) -o $@
 
-# diagnostic library (never the product): the samplers' timing ablations and per-phase cycle stamps behind
+# A/B + diagnostic library (never the product): the samplers' timing ablations and per-phase cycle stamps behind
 # -DDMIP_DIAG (DMIP_X3_DIAG for the x3 / x3k engines, scripts/x3k_stamps.py) and -DDMIP_X3P_DIAG (the paired
-# engine's per-chunk stamps, scripts/x3p_stamps.py); load it with DMIP_LIB=abv/diag/libdmip_diag.so
+# engine's per-chunk stamps, scripts/x3p_stamps.py), and the paired-tile 32x32 fp32x3 engine (dmip_x3p.h,
+# opt-in DMIP_X3P=1; it measured slower than x3k, so libdmip.so does not hold it). Load it with
+# DMIP_LIB=abv/diag/libdmip_diag.so (tests/test_gpu_x3p.py runs there)
 DIAG_DIR := abv/diag
-DIAG_SRCS := dmip_x3_cde dmip_x3k dmip_x3p
+DIAG_SRCS := dmip_x3_cde dmip_x3k dmip_capi
 diag: $(DIAG_DIR)/libdmip_diag.so
-$(DIAG_DIR)/%_diag.o: $(CSRC)/%.hip $(CSRC)/dmip_x3k.h $(CSRC)/dmip_x3p.h $(CSRC)/dmip_x3.h $(HDRS)
+$(DIAG_DIR)/%_diag.o: $(CSRC)/%.hip $(CSRC)/dmip_x3k.h $(CSRC)/dmip_x3.h $(HDRS)
 	@mkdir -p $(DIAG_DIR)
-	$(HIPCC) $(HIPFLAGS) -fno-slp-vectorize -DDMIP_DIAG -DDMIP_X3P_DIAG -c $< -o $@
-$(DIAG_DIR)/libdmip_diag.so: $(filter-out $(patsubst %,$(CSRC)/%.o,$(DIAG_SRCS)),$(OBJS)) $(patsubst %,$(DIAG_DIR)/%_diag.o,$(DIAG_SRCS))
+	$(HIPCC) $(HIPFLAGS) -fno-slp-vectorize -DDMIP_DIAG -c $< -o $@
+$(DIAG_DIR)/dmip_x3p_diag.o: $(CSRC)/dmip_x3p.hip $(CSRC)/dmip_x3p.h $(CSRC)/dmip_x3.h $(HDRS)
+	@mkdir -p $(DIAG_DIR)
+	$(HIPCC) $(HIPFLAGS) -fno-slp-vectorize -DDMIP_X3P_DIAG -c $< -o $@
+$(DIAG_DIR)/dmip_capi_diag.o: $(CSRC)/dmip_capi.cpp $(HDRS)
+	@mkdir -p $(DIAG_DIR)
+	$(HIPCC) $(HIPFLAGS) -DDMIP_WITH_X3P -c $< -o $@
+$(DIAG_DIR)/libdmip_diag.so: $(filter-out $(patsubst %,$(CSRC)/%.o,$(DIAG_SRCS)),$(OBJS)) $(patsubst %,$(DIAG_DIR)/%_diag.o,$(DIAG_SRCS)) $(DIAG_DIR)/dmip_x3p_diag.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@
 
 # microbenchmarks (scripts/ubench): built here, never committed
@@ -101,4 +105,4 @@ clean:
 	rm -f $(OBJS) $(PKG)/libdmip.so $(UBENCH)
 	rm -rf $(ASAN_DIR)
 
-.PHONY: all clean ubench asan
+.PHONY: all clean ubench asan diag

@@ -56,17 +56,17 @@ F_PRIOR = flops_per_sample_step(XDIM + 1, WIDTH, NH, XDIM)
 
 # the headline workload's sampler kernel per precision (+ its per-y prep kernel, inside the HIP events)
 KERNELS = {"fp32x3": "x3k_sampler_kernel<3,3,false> (+x3_bias_prep)",
-           "bf16": "em_sampler_kernel<0,256,3,3,0,8,4,false> (+a1_prep)",
+           "fp16": "em_sampler_kernel<0,256,3,3,0,8,4,false> (+a1_prep)",
            "fp32": "f32_sampler_kernel<0,256,3,0,false> (+f32_l1_prep)"}
-KERNEL_MATCH = {"fp32x3": "x3k_sampler_kernel", "bf16": "em_sampler_kernel", "fp32": "f32_sampler_kernel"}
+KERNEL_MATCH = {"fp32x3": "x3k_sampler_kernel", "fp16": "em_sampler_kernel", "fp32": "f32_sampler_kernel"}
 ARITH = {
     "fp32x3": "fp32-accurate: every product as three fp16 MFMAs W_hi h_hi + W_hi h_lo + W_lo h_hi "
               "(v_mfma_f32_16x16x32_f16, fp32 accumulation; 2^-23.2 of sum|w h| per product vs 2^-23.0 for an fp32 "
               "fmaf chain, profiles/r3_mfma_f16_check.txt), tanh by exp2 + rcp (~1 ulp); fp32 chain state / SDE update",
-    "bf16": "16-bit MFMA operands (layer 1: bf16 over split hi+lo inputs, ~fp32; hidden and output layers: fp16 "
+    "fp16": "16-bit MFMA operands (layer 1: bf16 over split hi+lo inputs, ~fp32; hidden and output layers: fp16 "
             "weights and activations), fp32 accumulate; fp32 chain state / SDE update",
     "fp32": "exact f32 MFMA (v_mfma_f32_16x16x4_f32, an fmaf chain), libm tanh; fp32 chain state / SDE update"}
-DTYPE = {"fp32x3": "fp32", "bf16": "fp16", "fp32": "fp32"}
+DTYPE = {"fp32x3": "fp32", "fp16": "fp16", "fp32": "fp32"}
 
 
 def executed_flops_per_sample_step(precision, in_dim=XDIM + YDIM + 1, w=WIDTH, nh=NH, out=XDIM):
@@ -84,7 +84,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="cde", choices=["cde", "cdiffe-pc", "dps"])
-    ap.add_argument("--precision", default="fp32x3", choices=["fp32x3", "bf16", "fp32"],
+    ap.add_argument("--precision", default="fp32x3", choices=["fp32x3", "fp16", "bf16", "fp32"],
                     help="headline arithmetic (default: fp32x3, the reference's fp32 at the fp16 matrix rate)")
     ap.add_argument("--chains", type=int, default=100000, help="chains per GPU (weak scaling)")
     ap.add_argument("--chains-total", type=int, default=0, help="total chains over all GPUs (strong scaling)")
@@ -102,7 +102,10 @@ def parse():
     ap.add_argument("--master-port", type=int, default=29511)
     ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)  # CPU/gloo launcher test only
     ap.add_argument("--stub-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)  # launcher fail-fast test
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.precision == "bf16":  # deprecated alias of the 16-bit sampler engine (its hidden layers are fp16)
+        a.precision = "fp16"
+    return a
 
 
 # ------------------------------------------------------------------------------ launcher
@@ -309,7 +312,7 @@ class Workload:
             self.kw = {"corrector_steps": 1, "snr": 0.16, "precision": args.precision}
             self.flops_sample_step = 2 * flops_per_sample_step(XDIM + YDIM + 1, WIDTH, NH, XDIM + YDIM)
             self.peak = PEAK_F32_TFLOPS if args.precision == "fp32" else PEAK_BF16_TFLOPS
-            self.kernel = {"fp32x3": "x3_sampler_kernel<2,256,3,23,false>", "bf16": "em_sampler_kernel<2,256,3,3,23,8,4,false>",
+            self.kernel = {"fp32x3": "x3_sampler_kernel<2,256,3,23,false>", "fp16": "em_sampler_kernel<2,256,3,3,23,8,4,false>",
                            "fp32": "f32_sampler_kernel<2,256,3,23,false>"}[args.precision] + " (CDiffE + Langevin corrector)"
             self.workload = "scatterometry CDiffE predictor-corrector (BASELINE configs[2])"
         else:  # dps
@@ -379,7 +382,7 @@ def other_configs(args, pkg, lib, dev):
     import torch
     out = {}
 
-    fam = {"fp32x3": "x3_sampler_kernel", "bf16": "em_sampler_kernel", "fp32": "f32_sampler_kernel"}
+    fam = {"fp32x3": "x3_sampler_kernel", "fp16": "em_sampler_kernel", "fp32": "f32_sampler_kernel"}
 
     def sampler(name, workload, chains, reps, precision, **kw):
         try:
@@ -449,13 +452,13 @@ def other_configs(args, pkg, lib, dev):
     except Exception as e:  # noqa: BLE001
         out["config1_linear"] = {"error": f"{type(e).__name__}: {e}"}
     sampler("config3_cdiffe_pc_per_gpu", "cdiffe-pc", 125000, 2, "fp32x3")
-    sampler("config3_cdiffe_pc_per_gpu_fast", "cdiffe-pc", 125000, 2, "bf16")
+    sampler("config3_cdiffe_pc_per_gpu_fast", "cdiffe-pc", 125000, 2, "fp16")
     sampler("config4_dps", "dps", 262144, 1, "fp32")
     sampler("cde_reference_width_512", "cde", 100000, 2, "fp32x3", width=512)
     sampler("posterior_reference_width_512", "cde", 100000, 1, "fp32x3", width=512, posterior=True)
     # CDiffE scatterometry at width 512: fp32x3 with its 96 KiB split layer 1 streamed through the ring (L1R)
     sampler("cdiffe_pc_reference_width_512", "cdiffe-pc", 100000, 1, "fp32x3", width=512)
-    sampler("cdiffe_pc_reference_width_512_fast", "cdiffe-pc", 100000, 1, "bf16", width=512)
+    sampler("cdiffe_pc_reference_width_512_fast", "cdiffe-pc", 100000, 1, "fp16", width=512)
     try:
         tr = importlib.import_module(PKG + ".training")
         torch.manual_seed(0)
@@ -606,8 +609,8 @@ def main_worker(args):
         line["ks_vs_ref"] = ks_field(rep)
         line["w1_vs_ref"] = w1_field(rep)
         line["parity"] = {"pass": rep["pass"]} if rep else None
-    if args.workload == "cde" and prec != "bf16" and not args.no_fast:
-        line["fast_mode"] = side_mode(wl, args, dist, world, dev, lib, metrics, "bf16", args.fast_steps, S, flops_launch)
+    if args.workload == "cde" and prec != "fp16" and not args.no_fast:
+        line["fast_mode"] = side_mode(wl, args, dist, world, dev, lib, metrics, "fp16", args.fast_steps, S, flops_launch)
     if args.workload == "cde" and prec != "fp32" and not args.no_fp32:
         line["fp32_mode"] = side_mode(wl, args, dist, world, dev, lib, metrics, "fp32", args.fp32_steps, S, flops_launch)
     if rank == 0 and world == 1 and args.workload == "cde" and not args.no_other_configs:

@@ -18,8 +18,11 @@ LIB_PATH = os.environ.get("DMIP_LIB", os.path.join(_HERE, "libdmip.so"))
 DMIP_OK, DMIP_ERR_INVALID, DMIP_ERR_UNSUPPORTED, DMIP_ERR_HIP, DMIP_ERR_ALLOC = range(5)
 DMIP_INPUT_X_Y_T, DMIP_INPUT_X_T = 0, 1
 DMIP_ACT_TANH_TWICE_FIRST, DMIP_ACT_TANH = 0, 1
-DMIP_PREC_BF16, DMIP_PREC_F32, DMIP_PREC_F32X3 = 0, 1, 2
-PRECISIONS = {"bf16": DMIP_PREC_BF16, "fp32": DMIP_PREC_F32, "fp32x3": DMIP_PREC_F32X3}
+DMIP_PREC_FP16, DMIP_PREC_F32, DMIP_PREC_F32X3 = 0, 1, 2
+# DMIP_PREC_BF16 (include/dmip.h): the same value -- the config-5 training kernel's split-bf16 arithmetic, and the
+# samplers' deprecated name of DMIP_PREC_FP16 (their 16-bit engine computes its hidden and output layers in fp16)
+DMIP_PREC_BF16 = DMIP_PREC_FP16
+PRECISIONS = {"fp16": DMIP_PREC_FP16, "bf16": DMIP_PREC_BF16, "fp32": DMIP_PREC_F32, "fp32x3": DMIP_PREC_F32X3}
 DMIP_SAMPLER_CDE, DMIP_SAMPLER_POSTERIOR, DMIP_SAMPLER_CDIFFE = 0, 1, 2
 ABI_VERSION = 6
 DMIP_LOSS_DSM, DMIP_LOSS_DSM_PDE, DMIP_LOSS_PINN, DMIP_LOSS_PINN2 = 0, 1, 2, 3
@@ -233,8 +236,9 @@ class MlpHandle:
 
 
 def precision_code(precision):
-    """'bf16' (16-bit MFMA operands, the fastest mode), 'fp32x3' (fp32-accurate products as three fp16 MFMAs,
-    the reference-precision throughput mode) or 'fp32' (exact f32 MFMA, bit-level parity mode)."""
+    """'fp16' (16-bit MFMA operands, the fastest mode: split-bf16 layer 1, fp16 hidden and output layers; 'bf16' is
+    its deprecated name), 'fp32x3' (fp32-accurate products as three fp16 MFMAs, the reference-precision throughput
+    mode) or 'fp32' (exact f32 MFMA, bit-level parity mode)."""
     if precision not in PRECISIONS:
         raise ValueError(f"precision must be one of {sorted(PRECISIONS)}, got {precision!r}")
     return PRECISIONS[precision]
@@ -247,7 +251,7 @@ def mlp_forward(handle, x, y, t, out, y_stride, t_stride, precision="fp32"):
 
 
 def em_sample(handle, sde, y, n_chains, chain_offset, num_steps, mean, std, seed, out, noise=None,
-              precision="bf16"):
+              precision="fp16"):
     calls["em_sample"] += 1
     n_y, ydim = y.shape
     check(lib().dmip_em_sample(handle.h, ctypes.byref(sde), ptr(y), n_y, ydim, handle.xdim,
@@ -257,7 +261,7 @@ def em_sample(handle, sde, y, n_chains, chain_offset, num_steps, mean, std, seed
 
 
 def em_sample_posterior(prior, likelihood, sde, y, n_chains, chain_offset, num_steps, mean, std, seed, out,
-                        precision="bf16"):
+                        precision="fp16"):
     calls["em_sample_posterior"] += 1
     n_y, ydim = y.shape
     check(lib().dmip_em_sample_posterior(prior.h, likelihood.h, ctypes.byref(sde), ptr(y), n_y, ydim,
@@ -267,7 +271,7 @@ def em_sample_posterior(prior, likelihood, sde, y, n_chains, chain_offset, num_s
 
 
 def em_sample_cdiffe(handle, sde, y, n_chains, chain_offset, num_steps, mean, std, seed, out, corrector_steps=0,
-                     snr=0.16, precision="bf16"):
+                     snr=0.16, precision="fp16"):
     calls["em_sample_cdiffe"] += 1
     n_y, ydim = y.shape
     check(lib().dmip_em_sample_cdiffe(handle.h, ctypes.byref(sde), ptr(y), n_y, ydim, handle.xdim,
@@ -277,7 +281,7 @@ def em_sample_cdiffe(handle, sde, y, n_chains, chain_offset, num_steps, mean, st
 
 
 def em_sample_snapshots(mode, net, prior, sde, y, n_chains, chain_offset, num_steps, mean, std, seed, snapshot_every,
-                        snaps, out, corrector_steps=0, snr=0.16, precision="bf16"):
+                        snaps, out, corrector_steps=0, snr=0.16, precision="fp16"):
     """dmip_em_sample_snapshots: the fused sampler of `mode` that also writes x after every
     snapshot_every-th step into snaps [num_steps // snapshot_every][n_y][n_chains][xdim]."""
     calls["em_sample_snapshots"] = calls.get("em_sample_snapshots", 0) + 1
@@ -290,14 +294,30 @@ def em_sample_snapshots(mode, net, prior, sde, y, n_chains, chain_offset, num_st
                                          stream_of(y.device)))
 
 
-def sampler_supported(width, n_hidden, xdim, ydim=0, mode=DMIP_SAMPLER_CDE, precision="bf16"):
+def sampler_supported(width, n_hidden, xdim, ydim=0, mode=DMIP_SAMPLER_CDE, precision="fp16"):
     return bool(lib().dmip_sampler_supported_precision(precision_code(precision), mode, width, n_hidden, xdim, ydim))
 
 
 def device_status(device):
     """Synchronise the device's current stream and raise if a kernel reported an asynchronous failure
-    (dmip_device_status: today the balanced sampler's hand-over timeout)."""
+    (dmip_device_status: the balanced sampler's hand-over timeout, or an fp32x3 chain outside the fp16 range).
+    Reading clears the status word."""
     check(lib().dmip_device_status(stream_of(device)))
+
+
+def is_range_error(e):
+    """The fp32x3 split's fp16-range refusal (pack time, ValueError) or report (device status, RuntimeError)."""
+    return isinstance(e, (ValueError, RuntimeError)) and "fp16 range" in str(e)
+
+
+def clear_range_status(device):
+    """Read and clear the device status word before a launch whose range report will be read: a stale fp16-range
+    report of an earlier launch (whose caller did not read it) is dropped; any other stale failure raises."""
+    try:
+        device_status(device)
+    except RuntimeError as e:
+        if not is_range_error(e):
+            raise
 
 
 def rng_normals(seed, chain_offset, stream_id, n_chains, n_pairs, out):

@@ -257,6 +257,7 @@ void split_h(double v, uint16_t& hi, uint16_t& lo) {
   lo = f2h((float)(v - (double)h2f(hi)));
 }
 
+#ifdef DMIP_WITH_X3P
 // 32x32x16 fragments (dmip_x3p.h): lane l = i + 32 h holds A[row i][k-slot 8 h + j]; k-step s of a hidden layer
 // covers the previous layer's accumulator registers 8 (s & 1) .. + 7 of its output tile s >> 1
 inline int kperm32(int s, int h, int j) { return 32 * (s >> 1) + 16 * (s & 1) + 8 * (j >> 2) + 4 * h + (j & 3); }
@@ -335,6 +336,8 @@ int pack_x3p(dmip_mlp* net, const float* const* weights, const float* const* bia
   return DMIP_OK;
 }
 
+#endif  // DMIP_WITH_X3P
+
 // layer-1 image over the input columns `cols` (scaled by c): input n at k-slots 3n, 3n+1, 3n+2 with
 // A = [W_hi, W_hi, W_lo] (the kernel's B = [v_hi, v_lo, v_hi])
 std::vector<uint16_t> pack_x3_l1(const float* W1, int W, int in_dim, const std::vector<int>& cols) {
@@ -381,28 +384,38 @@ void pack_x3_layer(const float* Wl, const float* bl, int n_rows, int W, int n_ti
 }
 
 // largest magnitude the fp32x3 images would hold in fp16: layer 1 scaled by 2 log2(e), the hidden layers by
-// -2 * 2 log2(e), the output rows by -2 (r-form folds), the paired engine's folded hidden biases
-double x3_max_scaled(const dmip_mlp* net, const float* const* weights, const float* const* biases) {
+// -2 * 2 log2(e), the output rows by -2 (r-form folds). The folded hidden biases stay f32 (x3_bias) in the
+// product engines, so they do not limit them (only the A/B paired engine stores them in fp16: x3p_bias_range)
+double x3_max_scaled(const dmip_mlp* net, const float* const* weights) {
   const int W = net->width, L = net->n_hidden, IN = net->in_dim, OUT = net->out_dim;
   double m = 0.0;
   for (size_t i = 0; i < (size_t)W * IN; ++i) m = std::max(m, kC * std::fabs((double)weights[0][i]));
-  for (int li = 1; li < L; ++li) {
+  for (int li = 1; li < L; ++li)
     for (size_t i = 0; i < (size_t)W * W; ++i) m = std::max(m, 2.0 * kC * std::fabs((double)weights[li][i]));
-    for (int r = 0; r < W; ++r) {  // folded bias kC b + kC sum_k W (pack_x3_layer)
+  for (size_t i = 0; i < (size_t)std::min(OUT, 16) * W; ++i) m = std::max(m, 2.0 * std::fabs((double)weights[L][i]));
+  return m;
+}
+
+#ifdef DMIP_WITH_X3P
+// the paired engine's fp16 folded hidden biases kC (b + sum_k W) (pack_x3p): their largest magnitude
+double x3p_bias_range(const dmip_mlp* net, const float* const* weights, const float* const* biases) {
+  const int W = net->width, L = net->n_hidden;
+  double m = 0.0;
+  for (int li = 1; li < L; ++li)
+    for (int r = 0; r < W; ++r) {
       double acc = (double)biases[li][r];
       for (int k = 0; k < W; ++k) acc += (double)weights[li][(size_t)r * W + k];
       m = std::max(m, kC * std::fabs(acc));
     }
-  }
-  for (size_t i = 0; i < (size_t)std::min(OUT, 16) * W; ++i) m = std::max(m, 2.0 * std::fabs((double)weights[L][i]));
   return m;
 }
+#endif
 
 int pack_x3_net(dmip_mlp* net, const float* const* weights, const float* const* biases) {
   const int W = net->width, L = net->n_hidden, IN = net->in_dim, OUT = net->out_dim, ST = W / 16;
   const int chunk = dmip::x3_chunk_bytes(W);
   if (chunk == 0) return DMIP_OK;  // no x3 kernels at this width
-  const double mx = x3_max_scaled(net, weights, biases);
+  const double mx = x3_max_scaled(net, weights);
   if (!(mx <= 65504.0)) {  // beyond fp16 (or not finite): no split images; fp32x3 requests are refused
     net->x3_range = std::isfinite(mx) ? mx : 1e300;
     return DMIP_OK;
@@ -484,7 +497,11 @@ int pack_x3_net(dmip_mlp* net, const float* const* weights, const float* const* 
     std::vector<char> koutb(kout.size() * 2);
     std::memcpy(koutb.data(), kout.data(), koutb.size());
     if ((rc = upload(&net->x3k_stream, kstream)) || (rc = upload(&net->x3k_out, koutb))) return rc;
-    if (net->xdim <= 4 && (rc = pack_x3p(net, weights, biases, bias.data() + W, bias.data() + 2 * W))) return rc;
+#ifdef DMIP_WITH_X3P
+    if (net->xdim <= 4 && x3p_bias_range(net, weights, biases) <= 65504.0 &&
+        (rc = pack_x3p(net, weights, biases, bias.data() + W, bias.data() + 2 * W)))
+      return rc;
+#endif
   }
   return DMIP_OK;
 }
@@ -516,6 +533,11 @@ int dmip_device_status(void* stream) {
 
 int dmip_abi_version(void) { return DMIP_ABI_VERSION; }
 
+#ifdef DMIP_WITH_X3P
+// not ABI: present only in the A/B library (make diag), which also holds the paired-tile engine (DMIP_X3P=1)
+int dmip_x3p_available(void) { return 1; }
+#endif
+
 int dmip_sampler_supported(int mode, int width, int n_hidden, int xdim, int ydim) {
   return dmip::sampler_shape_supported(mode, width, n_hidden, xdim, ydim) ? 1 : 0;
 }
@@ -526,7 +548,7 @@ int dmip_sampler_supported_f32(int mode, int width, int n_hidden, int xdim, int 
 
 int dmip_sampler_supported_precision(int precision, int mode, int width, int n_hidden, int xdim, int ydim) {
   switch (precision) {
-    case DMIP_PREC_BF16: return dmip::sampler_shape_supported(mode, width, n_hidden, xdim, ydim) ? 1 : 0;
+    case DMIP_PREC_FP16: return dmip::sampler_shape_supported(mode, width, n_hidden, xdim, ydim) ? 1 : 0;
     case DMIP_PREC_F32: return dmip::f32_sampler_supported(mode, width, n_hidden, xdim, ydim) ? 1 : 0;
     case DMIP_PREC_F32X3: return dmip::x3_sampler_supported(mode, width, n_hidden, xdim, ydim) ? 1 : 0;
     default: return 0;
@@ -739,7 +761,7 @@ int dmip_mlp_destroy(dmip_mlp* net) {
 int dmip_mlp_forward(const dmip_mlp* net, const float* x_dev, const float* y_dev, int64_t y_stride,
                      const float* t_dev, int t_stride, int64_t n, float* out_dev, int precision, void* stream) {
   if (!net || !x_dev || !t_dev || !out_dev) return fail(DMIP_ERR_INVALID, "null argument");
-  if (precision != DMIP_PREC_BF16 && precision != DMIP_PREC_F32 && precision != DMIP_PREC_F32X3)
+  if (precision != DMIP_PREC_FP16 && precision != DMIP_PREC_F32 && precision != DMIP_PREC_F32X3)
     return fail(DMIP_ERR_INVALID, "unknown precision");
   if (n < 0) return fail(DMIP_ERR_INVALID, "n < 0");
   if (n == 0) return DMIP_OK;
@@ -884,12 +906,15 @@ static bool x3k_enabled() {
   const char* e = getenv("DMIP_X3K");
   return !(e && e[0] == '0');
 }
-// DMIP_X3P=1 selects the paired-tile 32x32 engine (dmip_x3p.h) instead of the 16x16 k-major one (dmip_x3k.h)
-// at its shape (in development: opt-in until it times faster on the device)
+#ifdef DMIP_WITH_X3P
+// A/B library only (make diag): DMIP_X3P=1 selects the paired-tile 32x32 engine (dmip_x3p.h) instead of the
+// 16x16 k-major one (dmip_x3k.h) at its shape. It measured slower (profiles/r4_ab_x3p_vs_x3k.json), so the
+// product library libdmip.so does not contain it.
 static bool x3p_enabled() {
   const char* e = getenv("DMIP_X3P");
   return e && e[0] == '1';
 }
+#endif
 
 // fp32-accurate split-fp16 samplers (dmip_x3.h): same loop, RNG and sharding as the other engines;
 // arguments already validated by em_sample_impl
@@ -945,14 +970,17 @@ static int em_sample_x3(int mode, const dmip_mlp* net0, const dmip_mlp* net1, co
   p.spin_limit = p.debug_flags ? (1u << 10) : (1u << 22);
   bool ok = false;
   hipError_t e;
+#ifdef DMIP_WITH_X3P
   if (mode == DMIP_SAMPLER_CDE && net0->x3p_stream && dmip::x3p_sampler_supported(mode, net0->width, net0->n_hidden, xdim) &&
       x3k_enabled() && x3p_enabled()) {
-    // the paired-tile 32x32 engine at its shape (dmip_x3p.h)
+    // the paired-tile 32x32 engine at its shape (dmip_x3p.h; A/B library only)
     p.net[0].pstream = net0->x3p_stream;
     p.net[0].pl1 = net0->x3p_l1;
     p.net[0].pow = net0->x3p_ow;
     e = dmip::launch_x3p_sampler(p, xdim, a.n_y, st, &ok);
-  } else if (mode == DMIP_SAMPLER_CDE && net0->x3k_stream &&
+  } else
+#endif
+  if (mode == DMIP_SAMPLER_CDE && net0->x3k_stream &&
              dmip::x3k_sampler_supported(mode, net0->width, net0->n_hidden, xdim) && x3k_enabled()) {
     // the k-major multi-tile engine at its shape (dmip_x3k.h)
     p.net[0].kstream = net0->x3k_stream;
@@ -972,7 +1000,7 @@ static int em_sample_impl(int mode, const dmip_mlp* net0, const dmip_mlp* net1, 
   const int xdim = a.xdim, ydim = a.ydim;
   if (!net0 || !a.sde || !a.y_dev || !a.x_out_dev || (mode == DMIP_SAMPLER_POSTERIOR && !net1))
     return fail(DMIP_ERR_INVALID, "null argument");
-  if (a.precision != DMIP_PREC_BF16 && a.precision != DMIP_PREC_F32 && a.precision != DMIP_PREC_F32X3)
+  if (a.precision != DMIP_PREC_FP16 && a.precision != DMIP_PREC_F32 && a.precision != DMIP_PREC_F32X3)
     return fail(DMIP_ERR_INVALID, "unknown precision");
   if (a.noise_dev && mode != DMIP_SAMPLER_CDE) return fail(DMIP_ERR_INVALID, "noise injection: CDE sampler only");
   if (net0->layout != DMIP_INPUT_X_Y_T) return fail(DMIP_ERR_INVALID, "sampler needs an x,y,t network");
@@ -1139,7 +1167,7 @@ int dmip_em_sample_stamps(const dmip_mlp* net, const dmip_vpsde* sde, const floa
                           uint64_t* stamps_dev, void* stream) {
   if (!stamps_dev) return fail(DMIP_ERR_INVALID, "null stamps buffer");
   const SampleArgs a{sde,  y_dev, n_y,  ydim,           xdim,    n_chains,  0,      num_steps,
-                     0.0f, 1.0f,  seed, DMIP_PREC_BF16, nullptr, x_out_dev, stream, stamps_dev};
+                     0.0f, 1.0f,  seed, DMIP_PREC_FP16, nullptr, x_out_dev, stream, stamps_dev};
   return em_sample_impl(DMIP_SAMPLER_CDE, net, nullptr, a);
 }
 

@@ -301,7 +301,8 @@ bool x3_sampler_supported(int mode, int width, int n_hidden, int xdim, int ydim)
 // the k-major multi-tile engine (dmip_x3k.h): CDE, width 256, 3 hidden layers, xdim 2 or 3
 bool x3k_sampler_supported(int mode, int width, int n_hidden, int xdim);
 hipError_t launch_x3k_sampler(const X3SamplerParams& p, int xdim, int n_y, hipStream_t st, bool* ok);
-// the paired-tile 32x32 engine (dmip_x3p.h): CDE, width 256, 3 hidden layers, xdim 1..4
+// the paired-tile 32x32 engine (dmip_x3p.h; A/B library only, opt-in DMIP_X3P=1): CDE, width 256, 3 hidden
+// layers, xdim 2 or 3
 bool x3p_sampler_supported(int mode, int width, int n_hidden, int xdim);
 hipError_t launch_x3p_sampler(const X3SamplerParams& p, int xdim, int n_y, hipStream_t st, bool* ok);
 hipError_t launch_x3_bias_prep(const X3BiasPrepParams& p, int n_y, hipStream_t st);

@@ -142,12 +142,22 @@ __device__ __forceinline__ const bf16x8& frag(const char* base, int idx, int lan
   return *(const bf16x8*)(base + (idx * 64 + lane) * 16);
 }
 
-// element (unit row, sample col) of a transposed scratch block: row stride RSV; the unpadded layout
-// (RSV = 16, 32-byte rows) swaps the two 16-byte halves of rows 8..15 mod 16, so that the rows 8 apart a
-// ds_read_b128 lane group or a put_t row group touches fall in different banks
+// element (unit row, sample col) of a transposed scratch block: row stride RSV. The unpadded layout (RSV = 16,
+// 32-byte rows, the reverse half) is swizzled for both of its access patterns (MI355X_MICROARCH.md §LDS):
+//  * put_t's ds_write_b16 (lane groups of 32, bank = dword mod 32): lanes 0-31 write rows r and r + 4 of an
+//    8-row group, so those must sit in different 8-bank quarters of the 128-byte bank row: within each 8-row
+//    group row r takes 32-byte block pi(r) = 2 (r & 3) + (r >> 2) (rows 0-3 even blocks, rows 4-7 odd);
+//  * tread's ds_read_b128 (lane groups of 16, bank = dword mod 64): a group reads rows {0-3, 12-15, 20-27} (or
+//    {4-11, 16-19, 28-31}) of a 32-row block, same 16-byte half; with pi two of those rows share a block mod
+//    8, one in an even and one in an odd 8-row group, so the two 16-byte halves of rows 8..15 mod 16 swap.
+// Every group then touches distinct banks (round 3's swizzle alone left put_t's rows r, r + 4 colliding:
+// SQ_LDS_BANK_CONFLICT 2.49M per dispatch, 45 % of LDS-active cycles, profiles/r4_pmc_config5_reverse.json)
 template <int RSV>
 __device__ __forceinline__ int sidx(int row, int col) {
-  if constexpr (RSV == 16) return row * 16 + (((col >> 3) ^ ((row >> 3) & 1)) << 3) + (col & 7);
+  if constexpr (RSV == 16) {
+    const int blk = (row & ~7) | ((row & 3) << 1) | ((row >> 2) & 1);
+    return blk * 16 + (((col >> 3) ^ ((row >> 3) & 1)) << 3) + (col & 7);
+  }
   return row * RSV + col;
 }
 

@@ -495,6 +495,7 @@ __global__ void __launch_bounds__(Shape<W>::NW * 64, Shape<W>::NW / 4) x3_sample
     const long long c_local = (long long)(sg.job >= 0 ? sg.job : 0) * 16 + j;
     const bool valid = sg.job >= 0 && c_local < p.n_chains;
     const long long c_rd = valid ? c_local : 0;
+    const bool live = sg.kind != 3 && valid;  // a chain whose result is kept (idle segments and padded lanes are not)
     Rng rng;
     float x[D];
     if (sg.kind == 2) {  // resume the tile the previous wave of the grid handed over
@@ -544,7 +545,7 @@ __global__ void __launch_bounds__(Shape<W>::NW * 64, Shape<W>::NW / 4) x3_sample
       auto score = [&](const float (&vin)[C::NV], float (&a)[D]) __attribute__((always_inline)) {
         u32x4 b1[K1Q];
         l1_operand<C::NV, K1Q>(vin, g, b1);
-        oor |= out_of_range(vin);
+        oor |= live && out_of_range(vin);  // only chains whose results are returned
         f32x4 out = eng.eval(0, b1);
         if constexpr (C::NNET > 1) out = out + eng.eval(1, b1);  // likelihood + prior, then g * (...)
 #pragma unroll

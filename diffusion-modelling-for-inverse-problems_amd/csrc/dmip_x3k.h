@@ -593,10 +593,11 @@ __global__ void __launch_bounds__(KWaves<NT>::NWV * 64, KWaves<NT>::NWV / 4) x3k
         }
       }
     }
+    // only chains whose results are returned: an idle segment's dummy tile and padded lanes may diverge freely
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
-      for (int k = 0; k < D; ++k) oor |= !(__builtin_fabsf(x[t][k]) <= 65504.0f);  // NaN included
+      for (int k = 0; k < D; ++k) oor |= sg.kind != 3 && valid[t] && !(__builtin_fabsf(x[t][k]) <= 65504.0f);  // NaN included
     if (sg.kind == 1) {  // hand the job over to the next wave of the grid
       const size_t slot = (size_t)yi * n_waves + gw;
       float* dst = p.xfer + slot * (size_t)(NT * XT);

@@ -233,6 +233,7 @@ struct PWave {
   float delta, sqrt_delta;
   bool first;  // first step of a segment: tile B has no previous step to complete
   bool oor = false;  // a layer-1 input out of the split's range (x3::report_range)
+  bool live[2] = {false, false};  // the segment's tiles hold returned chains (not idle, not padded lanes)
   uint64_t ph[17], t_last;  // kDiag: cycles per ring chunk, barrier waits
 
   // ------------------------------------------------------------------ ring (dmip_x3k.h protocol)
@@ -428,7 +429,7 @@ struct PWave {
     v[D] = tau_n;
     u32x4 b[1];
     x3::l1_operand<D + 1, 1>(v, h, b);
-    oor |= x3::out_of_range(v);
+    oor |= live[T] && x3::out_of_range(v);
     b1[T] = b[0];
     touch(b1[T]);
 #pragma unroll
@@ -513,7 +514,7 @@ struct PWave {
     v[D] = tau;
     u32x4 b[1];
     x3::l1_operand<D + 1, 1>(v, h, b);
-    oor |= x3::out_of_range(v);
+    oor |= live[0] && x3::out_of_range(v);
     b1[0] = b[0];
     typedef __attribute__((address_space(3))) const u32x4* lds_u4;
     typedef __attribute__((address_space(3))) const float* lds_f;
@@ -617,6 +618,7 @@ __global__ void __launch_bounds__(NWV * 64, 1) x3p_sampler_kernel(X3SamplerParam
     for (int t = 0; t < 2; ++t) {
       c_loc[t] = (long long)(sg.job >= 0 ? sg.job : 0) * JC + 32 * t + j;
       valid[t] = sg.job >= 0 && c_loc[t] < p.n_chains;
+      e.live[t] = sg.kind != 3 && valid[t];
     }
     if (sg.kind == 2) {  // resume the job the previous wave of the grid handed over
       const size_t slot = (size_t)yi * n_waves + gw - 1;

@@ -12,10 +12,10 @@ Precision (`model.precision`, or `precision=` per call; default from $DMIP_PRECI
              (W_hi h_hi + W_hi h_lo + W_lo h_hi, fp32 accumulation; csrc/dmip_x3.h), tanh by exp2 + rcp.
              Error per product 2^-23 of sum |w h|, as an fp32 fmaf chain. The default.
   "fp32"   -- exact f32 (v_mfma_f32_16x16x4_f32, an fmaf chain, libm tanh): the bit-level parity mode.
-  "bf16"   -- 16-bit MFMA operands (fp16 hidden and output layers, split-bf16 layer 1): the fastest
-             mode, ~1e-3 relative per network evaluation.
+  "fp16"   -- 16-bit MFMA operands (fp16 hidden and output layers, split-bf16 layer 1): the fastest
+             mode, ~1e-3 relative per network evaluation. ("bf16" is its deprecated name.)
 A shape without a fused kernel in the requested precision runs the next more accurate one that has one
-(bf16 -> fp32x3 -> fp32). Shapes with no fused kernel at all step through per-step launches of the
+(fp16 -> fp32x3 -> fp32). Shapes with no fused kernel at all step through per-step launches of the
 network kernel (dmip_mlp_forward, exact f32) with the SDE update as device tensor ops and the kernels'
 chain-keyed RNG (so sharding stays bit-identical there too).
 There is no CPU sampling path: without a HIP device the samplers raise.
@@ -50,19 +50,26 @@ def _draw_seed():
     return int(torch.randint(0, 2 ** 62, (1,)).item())
 
 
+def canonical_precision(precision):
+    """The sampler precision's name: "bf16" is the deprecated name of "fp16" (the 16-bit engine computes its
+    hidden and output layers in fp16)."""
+    return "fp16" if precision == "bf16" else precision
+
+
 def default_precision():
-    return os.environ.get("DMIP_PRECISION", "fp32x3")
+    return canonical_precision(os.environ.get("DMIP_PRECISION", "fp32x3"))
 
 
 # a precision whose fused kernel is missing for a shape falls back to a more accurate one, never a less
-# accurate one: bf16 -> fp32x3 -> fp32
-_MORE_ACCURATE = {"bf16": ("fp32x3", "fp32"), "fp32x3": ("fp32",), "fp32": ()}
+# accurate one: fp16 -> fp32x3 -> fp32
+_MORE_ACCURATE = {"fp16": ("fp32x3", "fp32"), "fp32x3": ("fp32",), "fp32": ()}
 
 
 def _fused_precision(precision, mode, width, n_hidden, xdim, ydim):
     """The precision a fused kernel runs this shape in: the requested one, else the next more accurate
     one that is compiled (_MORE_ACCURATE); None when none is (per-step loop)."""
     _lib.precision_code(precision)
+    precision = canonical_precision(precision)
     for prec in (precision,) + _MORE_ACCURATE[precision]:
         if _lib.sampler_supported(width, n_hidden, xdim, ydim, mode, prec):
             return prec
@@ -76,7 +83,7 @@ class BaseClassDiffusionModel:
         self.xdim = xdim
         self.ydim = ydim
         self.sde = None
-        self.precision = default_precision()  # "fp32x3" | "fp32" | "bf16": arithmetic of the sampler's networks
+        self.precision = default_precision()  # "fp32x3" | "fp32" | "fp16": arithmetic of the sampler's networks
 
     def __call__(self, *args, **kwargs):
         return self.forward(*args, **kwargs)
@@ -143,7 +150,7 @@ class BaseClassDiffusionModel:
         """Device-resident samples (n_y, num_samples, xdim) for ys (n_y, ydim) -- no host copy.
         `chain_offset` selects a shard of a larger run; `noise` injects standard normals
         (num_steps + 1, n_y, num_samples, xdim) (slot 0 -> x0) in place of the internal RNG;
-        `precision` ("fp32x3" | "fp32" | "bf16") overrides self.precision."""
+        `precision` ("fp32x3" | "fp32" | "fp16") overrides self.precision."""
         raise NotImplementedError
 
     def _prepare(self, y, num_samples, num_steps, nets):

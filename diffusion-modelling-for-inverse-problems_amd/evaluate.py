@@ -78,7 +78,8 @@ def evaluate_scatterometry(model, ys, forward_model, out_dir, plot_ys, n_samples
 
     def one_y(i):
         y = ys[i]
-        x_pred = model.sample_device(y.expand(n_repeats, -1), n_samples_x, num_steps)  # (R, N, 3)
+        # (R, N, 3); the default precision's fp16-range guard (parallel.sample_checked) -- this rank's own y
+        x_pred = parallel.sample_checked(model, y.expand(n_repeats, -1), n_samples_x, num_steps, 0, 1)
         x_true = torch.stack([torch.as_tensor(load(i, j)).to(device=dev, dtype=torch.float32)
                               for j in range(n_repeats)])
         inflated = y[None, :].expand(x_true.shape[1], -1)
@@ -123,7 +124,7 @@ def evaluate_linear(model, ys, forward_model, out_dir, plot_ys, n_samples_x=5000
     def one_y(i):
         y = ys[i]
         posterior = forward_model.get_posterior(y.cpu(), device='cpu')
-        x_pred = model.sample_device(y.expand(n_repeats, -1), n_samples_x, num_steps)  # (R, N, 2)
+        x_pred = parallel.sample_checked(model, y.expand(n_repeats, -1), n_samples_x, num_steps, 0, 1)  # (R, N, 2)
         x_true = posterior.sample((n_repeats, n_samples_x)).to(device=dev, dtype=torch.float32)
         nll_t = nll_d = mse = 0.0
         for j in range(n_repeats):

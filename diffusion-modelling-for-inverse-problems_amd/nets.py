@@ -8,7 +8,8 @@ and the next Linear and shifts the numbering.
 
 Evaluation on a HIP device with autograd off goes to the fused MFMA kernel
 (libdmip dmip_mlp_forward) -- in exact f32 by default (`dmip_precision = "fp32"`, the reference's own
-arithmetic, e.g. for the evaluate drivers' score MSE), or with bf16 operands (`"bf16"`); the weights
+arithmetic, e.g. for the evaluate drivers' score MSE), or with 16-bit operands (`"fp16"`: split-bf16 layer 1,
+fp16 hidden and output layers; `"bf16"` is its deprecated name); the weights
 are packed once per parameter snapshot. Autograd (the training losses) uses the eager module chain.
 """
 import collections
@@ -35,7 +36,7 @@ class _TanhChainMLP(nn.Sequential):
         super().__init__(collections.OrderedDict(mods))
         self.act = activation
         self._dmip = None
-        self.dmip_precision = "fp32"  # arithmetic of the HIP forward (dmip_mlp_forward): "fp32" or "bf16"
+        self.dmip_precision = "fp32"  # arithmetic of the HIP forward (dmip_mlp_forward): "fp32" or "fp16"
 
     # -------------------------------------------------------------- packed HIP weights
     def linear_layers(self):

@@ -70,24 +70,56 @@ def sample_sharded(model, y, num_samples, num_steps, mean, std, seed=None, **sam
 
 
 def _sample_local(model, y, n, num_steps, mean, std, seed, lo, kw):
-    """This rank's shard. At the default precision (fp32x3: the reference's fp32 arithmetic from fp16 hi/lo
-    splits) a network or a trajectory outside the split's fp16 range -- a scaled weight, or a chain's layer-1
-    input, beyond 65504 -- is refused (at launch) or reported (device status) by the library; the shard is then
-    sampled again with the exact-f32 engine, so the default path never returns the split's inf/NaN where the
-    reference's fp32 stays finite. Decided per rank before the collective gather."""
+    """This rank's shard (sample_checked, the fallback decided by all ranks together)."""
+    return sample_checked(model, y, n, num_steps, mean, std, seed=seed, chain_offset=lo, agree=any_rank, **kw)
+
+
+def any_rank(flag):
+    """True on every rank when `flag` is true on any rank (one all_reduce MAX of a scalar; no-op at world size 1)."""
+    _, ws = world()
+    if ws == 1:
+        return bool(flag)
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+    buf = torch.tensor([1 if flag else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(buf, op=dist.ReduceOp.MAX)
+    return bool(buf.item())
+
+
+def sample_checked(model, y, n, num_steps, mean, std, seed=None, chain_offset=0, agree=None, **kw):
+    """model.sample_device(...) with the default precision's fp16-range guard.
+
+    At the default precision (fp32x3: the reference's fp32 arithmetic from fp16 hi/lo splits) a network or a
+    trajectory outside the split's fp16 range -- a scaled weight, or a returned chain's layer-1 input, beyond
+    65504 -- is refused (at launch) or reported (device status word) by the library; the call is then sampled
+    again with the exact-f32 engine, so the default path never returns the split's inf/NaN where the reference's
+    fp32 stays finite. The status word is cleared before the launch (a stale range report of an earlier launch
+    is not this call's) and read after it. `agree(flag) -> bool` makes the decision collective: under
+    sample_sharded every rank resamples if any rank's shard left the range, so the gathered union is always one
+    engine's chains (bit-identical to the 1-GPU run). An explicit `precision` keeps the error."""
     import warnings
     from . import _lib
     default = kw.get("precision") is None and getattr(model, "precision", None) == "fp32x3"
+    if not default:
+        return model.sample_device(y, n, num_steps, mean, std, seed=seed, chain_offset=chain_offset, **kw)
+    if seed is None:  # one seed for both attempts: the fallback resamples the same chains
+        from .estimators import _draw_seed
+        seed = _draw_seed()
+    dev = model._exec_device(y)
+    _lib.clear_range_status(dev)
+    err = None
     try:
-        x = model.sample_device(y, n, num_steps, mean, std, seed=seed, chain_offset=lo, **kw)
-        if default:
-            _lib.device_status(x.device)
-        return x
+        x = model.sample_device(y, n, num_steps, mean, std, seed=seed, chain_offset=chain_offset, **kw)
+        _lib.device_status(x.device)
     except (ValueError, RuntimeError) as e:
-        if not (default and "fp16 range" in str(e)):
+        if not _lib.is_range_error(e):
             raise
-        warnings.warn(f"{e}; sampled with the exact-f32 engine instead", RuntimeWarning)
-        return model.sample_device(y, n, num_steps, mean, std, seed=seed, chain_offset=lo, **dict(kw, precision="fp32"))
+        err = e
+    out_of_range = agree(err is not None) if agree is not None else err is not None
+    if not out_of_range:
+        return x
+    warnings.warn(f"{err or 'fp16 range (another rank)'}; sampled with the exact-f32 engine instead", RuntimeWarning)
+    return model.sample_device(y, n, num_steps, mean, std, seed=seed, chain_offset=chain_offset,
+                               **dict(kw, precision="fp32"))
 
 
 def map_sharded(n, fn, width):

@@ -38,13 +38,16 @@ typedef enum { DMIP_INPUT_X_Y_T = 0, DMIP_INPUT_X_T = 1 } dmip_input_layout;
 typedef enum { DMIP_ACT_TANH_TWICE_FIRST = 0, DMIP_ACT_TANH = 1 } dmip_act;
 
 /* Arithmetic of the network GEMMs; the chain state, the schedule and the SDE update are fp32 in both.
- *   DMIP_PREC_BF16  16-bit MFMA operands, fp32 accumulation: layer 1 is a bf16 MFMA over split hi+lo
+ *   DMIP_PREC_FP16  16-bit MFMA operands, fp32 accumulation: layer 1 is a bf16 MFMA over split hi+lo
  *                   bf16 inputs (~fp32), the hidden and output layers fp16 MFMAs over fp16 weights and
  *                   activations (3 more mantissa bits than bf16 at the same rate); tanh by exp2 + rcp,
- *                   layer 1's double tanh in packed fp16. The throughput mode (BASELINE headline).
+ *                   layer 1's double tanh in packed fp16. The throughput mode.
+ *                   DMIP_PREC_BF16 is the same value: for the samplers and the network forward a deprecated
+ *                   name of DMIP_PREC_FP16; for the config-5 training kernel (dmip_loss_grad,
+ *                   dmip_train_plan_desc) the name of what it computes (split-bf16 products).
  *   DMIP_PREC_F32   exact f32: every product and sum in f32 (v_mfma_f32_16x16x4_f32, an fmaf chain),
  *                   libm-accurate tanh -- the reference's own arithmetic (nets.py:32-35 in fp32).
- *                   The bit-level parity mode; ~1/10 of the bf16 throughput.
+ *                   The bit-level parity mode; ~1/10 of the fp16 throughput.
  *   DMIP_PREC_F32X3 fp32-accurate at the fp16 matrix rate: every product as the three-term fp16 split
  *                   W_hi h_hi + W_hi h_lo + W_lo h_hi on v_mfma_f32_16x16x32_f16 (fp32 accumulation; error
  *                   2^-23.2 of sum |w h| measured against 2^-23.0 for an f32 fmaf chain), tanh by exp2 + rcp
@@ -52,15 +55,20 @@ typedef enum { DMIP_ACT_TANH_TWICE_FIRST = 0, DMIP_ACT_TANH = 1 } dmip_act;
  *                   network forward runs the exact-f32 kernel).
  *                   Range: the split holds a value to ~2^-22 relative for |v| <= 65504 (fp16's largest
  *                   finite value) and to ~2^-24 absolute below 2^-14 (fp16 subnormals). The scaled weights
- *                   (layer 1 x 2 log2(e), hidden layers x 4 log2(e), output rows x 2) and folded biases must
- *                   fit: a network that does not is refused at sampling time (DMIP_ERR_UNSUPPORTED, "fp16
+ *                   (layer 1 x 2 log2(e), hidden layers x 4 log2(e), output rows x 2) must fit (the folded
+ *                   biases stay f32): a network that does not is refused at sampling time (DMIP_ERR_UNSUPPORTED, "fp16
  *                   range"). The layer-1 inputs (chain state x, t; CDiffE's y_t) are checked in the kernel --
  *                   at every step, or (the headline CDE engine) on each segment's final state, where an input
  *                   that left the range shows as non-finite or > 65504: a chain that leaves the range is
  *                   reported by dmip_device_status ("fp16 range") -- those chains are not fp32-accurate. The
  *                   Python estimators resample with DMIP_PREC_F32 then.
  * All three draw the same RNG stream per chain, so the modes are comparable chain by chain. */
-typedef enum { DMIP_PREC_BF16 = 0, DMIP_PREC_F32 = 1, DMIP_PREC_F32X3 = 2 } dmip_precision;
+typedef enum {
+  DMIP_PREC_FP16 = 0,
+  DMIP_PREC_F32 = 1,
+  DMIP_PREC_F32X3 = 2,
+  DMIP_PREC_BF16 = DMIP_PREC_FP16 /* see above: the training kernel's split-bf16; the samplers' deprecated name */
+} dmip_precision;
 
 /* VariancePreservingSDE (sdes.py:9-19): beta(t) = beta_min + (beta_max - beta_min) t. */
 typedef struct {

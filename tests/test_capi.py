@@ -58,8 +58,11 @@ def test_supported_shapes(lib, dmip):
     assert sup(512, 3, 3, 23, C, "fp32x3")  # round 4: CDiffE's 27-input layer 1 streams through the ring (L1R)
     assert not sup(256, 4, 3, 23, 0, "fp32x3")
     assert not sup(96, 3, 3, 23, 0, "fp32x3") and not sup(256, 3, 3, 5, C, "fp32x3")
+    # the 16-bit engine's name is "fp16" (its hidden and output layers); "bf16" is its deprecated alias
+    assert sup(256, 3, 3, 23, 0, "fp16") == sup(256, 3, 3, 23, 0, "bf16") == True
+    assert dmip._lib.precision_code("fp16") == dmip._lib.precision_code("bf16") == dmip._lib.DMIP_PREC_FP16
     with pytest.raises(ValueError):
-        sup(256, 3, 3, 23, 0, "fp16")
+        sup(256, 3, 3, 23, 0, "f16")
 
 
 def test_precision_rejected_before_launch(lib, dmip):

@@ -29,8 +29,28 @@ def _need_gpu():
 
 @pytest.fixture(autouse=True)
 def _x3k_engine(monkeypatch):
-    """The paired-tile engine (dmip_x3p.h) is the default at this shape; these tests pin the k-major one."""
+    """The k-major engine is the default at this shape; DMIP_X3P=0 keeps it so under the A/B library too, whose
+    opt-in paired-tile engine (dmip_x3p.h) would take the shape with DMIP_X3P=1."""
     monkeypatch.setenv("DMIP_X3P", "0")
+
+
+def test_x3p_ab_engine_in_diag_library():
+    """The A/B paired-tile engine's own tests (tests/test_gpu_x3p.py) in ONE child process on the A/B library
+    (the product library does not hold that engine; the library is chosen at import)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    diag = os.path.join(root, "abv", "diag", "libdmip_diag.so")
+    if not os.path.exists(diag):
+        pytest.skip("A/B library not built (make diag)")
+    env = dict(os.environ, DMIP_LIB=diag)
+    r = subprocess.run([sys.executable, "-u", "-m", "pytest", os.path.join(root, "tests", "test_gpu_x3p.py"), "-x", "-q",
+                        "-m", "gpu", "-p", "no:cacheprovider", "--timeout", "300", "--timeout-method", "thread"],
+                       cwd=root, env=env, capture_output=True, text=True, timeout=900)
+    print(r.stdout[-3000:])
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+    assert " passed" in r.stdout and "skipped" not in r.stdout.splitlines()[-1], r.stdout[-500:]
 
 
 def _params(net):

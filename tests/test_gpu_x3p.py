@@ -1,7 +1,9 @@
 """The paired-tile 32x32 fp32x3 CDE engine (csrc/dmip_x3p.h: one wave per SIMD with two 32-chain tiles in
 ping-pong, layer 1 fused into hidden layer 1 (k-major), hidden layer 2 output-major into an exact-f32 output
-layer) -- the default path of `CDE.sample_device` at the headline shape (hidden_layers [256]*3). Needs an
-MI355X: `pytest -m gpu`.
+layer). An A/B engine: it measured slower than the k-major engine (profiles/r4_ab_x3p_vs_x3k.json), so only
+the A/B library (`make diag`, abv/diag/libdmip_diag.so) holds it, opt-in with DMIP_X3P=1. This module runs
+in a child process on that library (tests/test_gpu_x3k.py::test_x3p_ab_engine_in_diag_library) and skips
+when the loaded library is the product one. Needs an MI355X: `pytest -m gpu`.
 
 Gates (the fp32 engines' own, test_gpu_x3.py): the float32 oracle on the same chains within 1e-4 of
 max(1, |x|); the 16x16 k-major engine (DMIP_X3P=0; the same split hidden layers, its output layer split into
@@ -23,9 +25,11 @@ PREC = "fp32x3"
 
 
 @pytest.fixture(scope="module", autouse=True)
-def _need_gpu():
+def _need_gpu(dmip):
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
+    if not hasattr(dmip._lib.lib(), "dmip_x3p_available"):
+        pytest.skip("the paired engine is in the A/B library only (DMIP_LIB=abv/diag/libdmip_diag.so)")
 
 
 @pytest.fixture(autouse=True)
