@@ -60,19 +60,21 @@ $(PKG)/libdmip.so: $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(OBJS) -o $@
 
 # A/B + diagnostic library (never the product): the samplers' timing ablations and per-phase cycle stamps behind
-# -DDMIP_DIAG (DMIP_X3_DIAG for the x3 / x3k engines, scripts/x3k_stamps.py) and -DDMIP_X3P_DIAG (the paired
-# engine's per-chunk stamps, scripts/x3p_stamps.py), and the paired-tile 32x32 fp32x3 engine (dmip_x3p.h,
-# opt-in DMIP_X3P=1; it measured slower than x3k, so libdmip.so does not hold it). Load it with
-# DMIP_LIB=abv/diag/libdmip_diag.so (tests/test_gpu_x3p.py runs there)
+# -DDMIP_DIAG (run-time DMIP_X3_DIAG for the x3 / x3k engines, scripts/x3k_stamps.py), and the paired-tile 32x32
+# fp32x3 engine (dmip_x3p.h, opt-in DMIP_X3P=1; it measured slower than x3k, so libdmip.so does not hold it).
+# Load it with DMIP_LIB=abv/diag/libdmip_diag.so (tests/test_gpu_x3p.py runs there). The paired engine's
+# per-chunk stamps (scripts/x3p_stamps.py) replace its snapshots, so they need their own build:
+# make diag X3P_DIAG=-DDMIP_X3P_DIAG
 DIAG_DIR := abv/diag
 DIAG_SRCS := dmip_x3_cde dmip_x3k dmip_capi
 diag: $(DIAG_DIR)/libdmip_diag.so
 $(DIAG_DIR)/%_diag.o: $(CSRC)/%.hip $(CSRC)/dmip_x3k.h $(CSRC)/dmip_x3.h $(HDRS)
 	@mkdir -p $(DIAG_DIR)
 	$(HIPCC) $(HIPFLAGS) -fno-slp-vectorize -DDMIP_DIAG -c $< -o $@
+X3P_DIAG ?=
 $(DIAG_DIR)/dmip_x3p_diag.o: $(CSRC)/dmip_x3p.hip $(CSRC)/dmip_x3p.h $(CSRC)/dmip_x3.h $(HDRS)
 	@mkdir -p $(DIAG_DIR)
-	$(HIPCC) $(HIPFLAGS) -fno-slp-vectorize -DDMIP_X3P_DIAG -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) -fno-slp-vectorize $(X3P_DIAG) -c $< -o $@
 $(DIAG_DIR)/dmip_capi_diag.o: $(CSRC)/dmip_capi.cpp $(HDRS)
 	@mkdir -p $(DIAG_DIR)
 	$(HIPCC) $(HIPFLAGS) -DDMIP_WITH_X3P -c $< -o $@

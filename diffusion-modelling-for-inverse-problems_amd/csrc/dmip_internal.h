@@ -285,6 +285,7 @@ struct X3SamplerParams {
   unsigned int* err;
   unsigned int spin_limit;
   int debug_flags;
+  const float* coef;          // x3k: per-step (tau, beta, g, 0) [num_steps][4] of step_coef (its launch fills it)
 };
 
 struct X3BiasPrepParams {

@@ -21,7 +21,15 @@
 //     ahead, and the chains' RNG states wait in LDS through the step (the registers that layout needs);
 //   * the output layer (3 rows) is LDS-resident as one fragment per k-step: rows 0..D-1 hold W_hi, rows
 //     4..4+D-1 W_lo, so A . h_hi yields W_hi h_hi and W_lo h_hi in lane groups 0 and 1 and A . h_lo yields
-//     W_hi h_lo in group 0 (8 KiB instead of a 16-row hi + lo chunk).
+//     W_hi h_lo in group 0 (8 KiB instead of a 16-row hi + lo chunk);
+//   * the step's work that does not depend on the network leaves the matrix-idle phases (round 5): the EM
+//     update's normals are drawn inside hidden layer 2's last chunk (free of output-layer work), lane group t
+//     drawing chain tile t's (one Box-Muller pass for all NT tiles instead of NT), and parked in LDS beside the
+//     RNG states; the step coefficients (tau, beta, g) come from a per-launch table (scalar loads) instead of
+//     a division and an f64 square root per step; the output rows' partial sums meet by v_permlane16/32_swap
+//     (no LDS round trip); the resident layer-1 image holds lane groups 0-1 only (groups 2-3 of the layer-1
+//     B operand are zero k-slots, so those lanes read group 0-1's finite weights), which frees the LDS for
+//     the normals.
 // The hidden layers accumulate each output element in the order of dmip_x3.h (k-steps ascending; per
 // k-step hi.h_lo, lo.h_hi, hi.h_hi): bit-identical hidden activations; the output layer's three partial
 // sums are added at the end ((hi.h_hi + hi.h_lo) + lo.h_hi), within an ulp of the one-chain order.
@@ -50,7 +58,9 @@ struct KWaves {
 static_assert(NCHUNK % R == 0, "static ring: chunk k of every step in slot k % R");
 
 struct KLay {
-  static constexpr int L1 = 0, L1_BYTES = ST * 1024;      // [16 tiles][64 lanes][8 fp16] (K1Q = 1)
+  // [16 tiles][32 lanes][8 fp16] (K1Q = 1): lanes 32-63 hold k-slots 16-31, zero in the B operand of every
+  // x3k shape (3 (D + 1) <= 15 slots), so they read lanes 0-31's (finite) fragments instead
+  static constexpr int L1 = 0, L1_BYTES = ST * 512;
   static constexpr int OUT = L1 + L1_BYTES, OUT_BYTES = KQ * 1024;  // [8 k-steps][64][8]
   static constexpr int BIAS = OUT + OUT_BYTES;            // floats: c(b1 + W1_y y) | hidden 1 | hidden 2 | out[16]
   static constexpr int BF = (NH + 1) * W + 16;
@@ -59,7 +69,9 @@ struct KLay {
   // the chains' RNG states, parked in LDS while the network is evaluated ([wave][tile][word][16 chains]): 12
   // registers fewer through the step
   static constexpr int RNGP = RING + R * CHUNK, RNGP_BYTES = 3072;
-  static constexpr int TOTAL = RNGP + RNGP_BYTES;
+  // the EM update's normals of the step, drawn in hidden layer 2 ([wave][tile][k][16 chains] floats, k < 3)
+  static constexpr int NRM = RNGP + RNGP_BYTES, NRM_BYTES = 2304;
+  static constexpr int TOTAL = NRM + NRM_BYTES;
 };
 static_assert(KLay::TOTAL <= 160 * 1024, "LDS budget");
 
@@ -101,6 +113,8 @@ struct KEngine {
   __amdgpu_buffer_rsrc_t rs;
   unsigned voff;          // this wave's DMA pieces: w PPW KiB + 16 lane
   int w, g;
+  uint32_t* rng_park;  // this wave's parked RNG states [tile][word][16 chains]
+  float* nrm;          // this wave's normals of the step [tile][k][16 chains]
   mutable uint64_t ph_vm = 0, ph_bar = 0;  // DIAG & 2: cycles in the ring's vmcnt waits and barriers
 
   // piece Q of chunk C of the step image into slot S (LDS-DMA: 1 KiB per wave-instruction)
@@ -338,6 +352,7 @@ struct KEngine {
         act_pair<k + 1, O % 8>(In, Ah, Al);
         act_pair<k + 1, 8 + O % 8>(In, Ah, Al);
       }
+      if constexpr (H == 1 && Q2 == KQ / 2 - 1 && !NOISE) rng_slice<O>(rs_);
       if constexpr (H == 1) {  // output-layer pair G = 16 Q2 + O: unit (q, t) = (G / 4 / NT, G / 4 % NT), pair G % 4
         constexpr int G = 16 * Q2 + O, u = G / 4, d = G % 4, q = u / NT, t = u % NT;
         if constexpr (q < KQ / 2) {
@@ -359,6 +374,56 @@ struct KEngine {
       }
       ring_post<K, O>();
       ostep2<H, Q2, O + 1>(base, nbase, In, Out, Ah, Al, f, fpre, oH, oL, fo, eh, el);
+    }
+  }
+
+  // ---- the EM update's normals, drawn in hidden layer 2's last chunk (chunk (1, KQ/2 - 1) holds no output-layer
+  // work for any NT): lane group t < NT draws chain tile t's D normals from its parked RNG state (the draws
+  // rng_normals<D> makes, in the same order), parks the state again and leaves the normals in LDS for the EM
+  // update, which every lane group reads. One Box-Muller pass serves all NT tiles.
+  struct RngSlice {
+    Rng r;
+    uint32_t a, b;
+    float u2, rad;
+    float n[4];
+  };
+  mutable RngSlice rs_;
+  // rng_normal_pair (dmip_device.h) cut into one dependent stage per o-step -- the same operations in the same
+  // order, so the same bits -- so that each stage sits beside its o-step's MFMAs: O = 0 unpark, then per pair
+  // P (base 1 + 4 P): the two xoshiro words, the uniforms and log2, the square root, cos / sin; O = 9 park
+  template <int O>
+  __device__ __forceinline__ void rng_slice(RngSlice& st) const {
+    static_assert(D <= 4, "two normal pairs");
+    const int tg = g < NT ? g : NT - 1;  // lane groups beyond the tiles repeat the last tile's draw, unstored
+    const int j = threadIdx.x & 15;
+    if constexpr (O == 0) {
+      const uint32_t* d = rng_park + tg * 64;
+      st.r = Rng{d[j], d[16 + j], d[32 + j], d[48 + j]};
+    }
+    constexpr int P = (O - 1) / 4, E = (O - 1) % 4;
+    if constexpr (O >= 1 && P < (D + 1) / 2) {
+      if constexpr (E == 0) {
+        st.a = rng_next(st.r);
+        st.b = rng_next(st.r);
+      } else if constexpr (E == 1) {
+        const float u1 = 1.0f - (float)(st.a >> 8) * 0x1p-24f;
+        st.u2 = (float)(st.b >> 8) * 0x1p-24f;
+        st.rad = -1.3862943611198906f * __log2f(u1);
+      } else if constexpr (E == 2) {
+        st.rad = __fsqrt_rn(st.rad);  // sqrt(-2 ln u1)
+      } else {
+        st.n[2 * P] = st.rad * __builtin_amdgcn_cosf(st.u2);
+        st.n[2 * P + 1] = st.rad * __builtin_amdgcn_sinf(st.u2);
+      }
+    }
+    if constexpr (O == 9) {
+      if (g < NT) {
+        uint32_t* d = rng_park + g * 64;
+        d[j] = st.r.s0, d[16 + j] = st.r.s1, d[32 + j] = st.r.s2, d[48 + j] = st.r.s3;
+        float* o = nrm + g * (D * 16);
+#pragma unroll
+        for (int k = 0; k < D; ++k) o[k * 16 + j] = st.n[k];
+      }
     }
   }
 
@@ -401,10 +466,12 @@ __global__ void __launch_bounds__(KWaves<NT>::NWV * 64, KWaves<NT>::NWV / 4) x3k
   eng.voff = (unsigned)(w * PPW * 1024 + lane * 16);
   eng.w = w;
   eng.g = g;
+  eng.rng_park = (uint32_t*)(lds + L::RNGP) + w * NT * 64;
+  eng.nrm = (float*)(lds + L::NRM) + w * NT * D * 16;
   {
-    const uint4* s1 = (const uint4*)p.net[0].l1;
+    const uint4* s1 = (const uint4*)p.net[0].l1;  // [16 tiles][64 lanes] -> lanes 0-31 of each tile
     uint4* d1 = (uint4*)(lds + L::L1);
-    for (int e = threadIdx.x; e < L::L1_BYTES / 16; e += NWV * 64) d1[e] = s1[e];
+    for (int e = threadIdx.x; e < L::L1_BYTES / 16; e += NWV * 64) d1[e] = s1[(e >> 5) * 64 + (e & 31)];
     const uint4* so = (const uint4*)p.net[0].kout;
     uint4* dout = (uint4*)(lds + L::OUT);
     for (int e = threadIdx.x; e < L::OUT_BYTES / 16; e += NWV * 64) dout[e] = so[e];
@@ -414,7 +481,7 @@ __global__ void __launch_bounds__(KWaves<NT>::NWV * 64, KWaves<NT>::NWV / 4) x3k
   }
   u32x4 fpre[PF][2];  // the first fragment pairs of the next ring chunk (read ahead across phases)
   eng.start(fpre);
-  const char* l1_lane = lds + L::L1 + lane * 16;
+  const char* l1_lane = lds + L::L1 + (lane & 31) * 16;  // lanes 32-63: zero k-slots of B (KLay::L1)
   const char* out_lane = lds + L::OUT + lane * 16;
 
   const int S = p.num_steps;
@@ -441,9 +508,11 @@ __global__ void __launch_bounds__(KWaves<NT>::NWV * 64, KWaves<NT>::NWV / 4) x3k
       valid[t] = sg.job >= 0 && c_loc[t] < p.n_chains;
     }
     float x[NT][D];
-    // wave-private LDS slots of the tiles' RNG states: lane group 0 writes, every lane reads its chain's words
-    uint32_t* rng_park = (uint32_t*)(lds + L::RNGP) + w * NT * 64;
+    // wave-private LDS slots of the tiles' RNG states: lane group 0 writes at a segment's start, lane group t
+    // draws tile t's normals in hidden layer 2 (KEngine::rng_slice), every lane reads its chain's words
+    uint32_t* rng_park = eng.rng_park;
     static_assert(KWaves<NT>::NWV * NT * 256 <= KLay::RNGP_BYTES, "RNG parking space");
+    static_assert(KWaves<NT>::NWV * NT * 3 * 64 <= KLay::NRM_BYTES, "normals space");
     auto park = [&](int t, const Rng& r) {
       if (g == 0) {
         uint32_t* d = rng_park + t * 64;
@@ -488,7 +557,8 @@ __global__ void __launch_bounds__(KWaves<NT>::NWV * 64, KWaves<NT>::NWV / 4) x3k
     int snap_next = p.snap_every > 0 ? (sg.s0 / p.snap_every + 1) * p.snap_every : -1;
     for (int i0 = sg.s0; i0 < sg.s1; ++i0) {
       const int i = sg.kind == 3 ? 0 : i0;  // idle steps: a dummy job at step 0, discarded
-      const StepCoef cf = step_coef(i, S, p.T, p.bmin, p.bdiff);
+      const float4 c4 = ((const float4*)p.coef)[i];  // step_coef(i, ...) of this launch (x3k_coef_kernel)
+      const StepCoef cf{c4.x, c4.y, c4.z};
       uint64_t t0 = 0;
       if constexpr (DIAG & 2) t0 = stamp();
 
@@ -506,7 +576,7 @@ __global__ void __launch_bounds__(KWaves<NT>::NWV * 64, KWaves<NT>::NWV / 4) x3k
         }
 #pragma unroll
         for (int o = 0; o < ST; ++o) {
-          const u32x4 a = *(const u32x4*)(l1_lane + o * 1024);
+          const u32x4 a = *(const u32x4*)(l1_lane + o * 512);
           const f32x4 b = eng.bias4(0, o);
 #pragma unroll
           for (int t = 0; t < NT; ++t) P[t][o] = mfma16(a, b1[t][0], b);
@@ -558,19 +628,25 @@ __global__ void __launch_bounds__(KWaves<NT>::NWV * 64, KWaves<NT>::NWV / 4) x3k
         float a[D];
 #pragma unroll
         for (int k = 0; k < D; ++k) {
-          const float lo_w = __shfl(oH[t][k], j + 16, 64);  // W_lo h_hi of row k (lane group 1)
-          const float v = (oH[t][k] + oL[t][k]) + lo_w;
-          a[k] = __shfl(v, j, 64);
+          // lane group 0 holds W_hi h_hi (oH) and W_hi h_lo (oL) of row k, group 1 W_lo h_hi (oH): permlane16_swap
+          // brings groups 0 and 1 together in both (groups 2-3 likewise, zero rows), permlane32_swap copies
+          // lanes 0-31's sum to lanes 32-63 -- the order (hi.h_hi + hi.h_lo) + lo.h_hi of the earlier shuffles
+          const auto sh = __builtin_amdgcn_permlane16_swap(__float_as_uint(oH[t][k]), __float_as_uint(oH[t][k]),
+                                                           false, false);
+          const auto sl = __builtin_amdgcn_permlane16_swap(__float_as_uint(oL[t][k]), __float_as_uint(oL[t][k]),
+                                                           false, false);
+          const float v = (__uint_as_float(sh[0]) + __uint_as_float(sl[0])) + __uint_as_float(sh[1]);
+          a[k] = __uint_as_float(__builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false,
+                                                                  false)[0]);
         }
         float xi[D];
         if constexpr (NOISE) {
           const float* src = p.noise + noise_step * (i + 1) + ((size_t)yi * p.n_chains + (valid[t] ? c_loc[t] : 0)) * D;
 #pragma unroll
           for (int k = 0; k < D; ++k) xi[k] = src[k];
-        } else {
-          Rng rng = unpark(t);
-          rng_normals<D>(rng, xi);
-          park(t, rng);
+        } else {  // drawn in hidden layer 2 (KEngine::rng_slice)
+#pragma unroll
+          for (int k = 0; k < D; ++k) xi[k] = eng.nrm[(t * D + k) * 16 + j];
         }
 #pragma unroll
         for (int k = 0; k < D; ++k) x[t][k] = em_update(x[t][k], a[k], xi[k], cf, p.delta, p.sqrt_delta);
@@ -641,6 +717,17 @@ __global__ void __launch_bounds__(KWaves<NT>::NWV * 64, KWaves<NT>::NWV / 4) x3k
 
 }  // namespace x3k
 
+// the launch's step coefficients: coef[i] = step_coef(i) (the kernel loads them instead of recomputing a division
+// and an f64 square root at every step; the same device function, so the same bits)
+template <int DUMMY = 0>
+__global__ void x3k_coef_kernel(float4* coef, int S, float T, float bmin, float bdiff) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < S) {
+    const StepCoef c = step_coef(i, S, T, bmin, bdiff);
+    coef[i] = make_float4(c.tau, c.beta, c.g, 0.0f);
+  }
+}
+
 template <int D, int NT, bool NOISE, int DIAG = 0>
 inline hipError_t launch_x3k_sampler_t(const X3SamplerParams& p, int n_y, hipStream_t st) {
   constexpr int NWV = x3k::KWaves<NT>::NWV;
@@ -655,8 +742,18 @@ inline hipError_t launch_x3k_sampler_t(const X3SamplerParams& p, int n_y, hipStr
   // hand-over slots of NT tiles: (NT (D + 4) - 4 + 4) 64 words each
   hipError_t e = alloc_handover((size_t)g * n_y * NWV, NT * (D + 4) - 4, st, &buf, &q.xfer, &q.xflag);
   if (e != hipSuccess) return e;
+  const int S = p.num_steps > 0 ? p.num_steps : 1;
+  float4* coef = nullptr;
+  if ((e = hipMallocAsync((void**)&coef, (size_t)S * sizeof(float4), st)) != hipSuccess) {
+    (void)hipFreeAsync(buf, st);
+    return e;
+  }
+  hipLaunchKernelGGL(x3k_coef_kernel<0>, dim3((unsigned)((S + 255) / 256)), dim3(256), 0, st, coef, S, p.T, p.bmin,
+                     p.bdiff);
+  q.coef = (const float*)coef;
   hipLaunchKernelGGL(kern, dim3((unsigned)g, (unsigned)n_y), dim3(NWV * 64), 0, st, q);
   e = hipGetLastError();
+  (void)hipFreeAsync(coef, st);
   (void)hipFreeAsync(buf, st);
   return e;
 }

@@ -134,3 +134,21 @@ def test_x3p_snapshots(dmip):
     _, ref_snaps = O.cde_sample(_params(m.sde.a), yy, 700, 6, 99, snapshots={2, 4, 6})
     for k in range(3):
         assert _rel(sn1[k, 0].cpu().numpy(), ref_snaps[(k + 1) * 2]) < 1e-4
+
+
+def test_x3p_trajectory_outside_fp16_range_reported(dmip, golden):
+    """The paired engine's range guard (an output bias of 1e6: |x| ~ 1e5-1e6 after one step): the device status
+    word reports it for an explicit fp32x3 request, and the default precision resamples in exact f32."""
+    m = dmip.CDE(3, 23, [256] * 3)
+    m.sde.a.load_state_dict(state_from_npz(golden("ckpt_scat.npz")))
+    with torch.no_grad():
+        m.sde.a._modules["7"].bias[:] = 1.0e6
+    y = torch.from_numpy(golden("samples_scat.npz")["y"]).to(DEV)
+    x3 = m.sample_device(y, 600, 6, seed=91, precision=PREC)
+    with pytest.raises(RuntimeError, match="fp16 range"):
+        dmip._lib.device_status(x3.device)
+    torch.manual_seed(6)
+    with pytest.warns(RuntimeWarning, match="fp16 range"):
+        x = m(y, num_samples=600, num_steps=6)
+    torch.manual_seed(6)
+    assert np.array_equal(x, m(y, num_samples=600, num_steps=6, precision="fp32"))
