@@ -442,6 +442,56 @@ struct KEngine {
   }
 };
 
+// Layer 1's B operand of every chain tile, branch-free: input n takes k-slots 3n, 3n + 1, 3n + 2 as
+// [v_hi, v_lo, v_hi] (x3::l1_operand's layout and bits: split_pair rounds as its casts do); lane group 0 holds
+// k-slots 0-7, group 1 slots 8-15, groups 2-3 zero (3 (D + 1) <= 12 slots). x3::l1_operand selected the 16-bit
+// slots per lane group through exec-mask branches; here whole dwords are masked in.
+template <int D, int NT>
+__device__ __forceinline__ void l1_operands(const float (&x)[NT][D], float tau, int g, u32x4 (&b)[NT]) {
+  static_assert(D == 2 || D == 3, "x3k shapes");
+  const uint32_t m0 = g == 0 ? 0xFFFFFFFFu : 0u, m1 = g == 1 ? 0xFFFFFFFFu : 0u;
+  // (lo half of a, lo half of b) and (hi half of a, hi half of b)
+  auto lo2 = [](uint32_t a, uint32_t b) { return __builtin_amdgcn_perm(b, a, 0x05040100u); };
+  auto hi2 = [](uint32_t a, uint32_t b) { return __builtin_amdgcn_perm(b, a, 0x07060302u); };
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    uint32_t H01, L01, H23, L23;
+    x3::split_pair(x[t][0], x[t][1], H01, L01);
+    if constexpr (D == 3) x3::split_pair(x[t][2], tau, H23, L23);
+    else x3::split_pair(tau, 0.0f, H23, L23);
+    // slots of group 0: (hi0 lo0) (hi0 hi1) (lo1 hi1) (hi2 lo2); group 1: (hi2 hi3) (lo3 hi3) 0 0  [D = 3, "2" = x2,
+    // "3" = tau]; D = 2: group 0 (hi0 lo0) (hi0 hi1) (lo1 hi1) (hiT loT), group 1 (hiT 0) 0 0 0
+    const uint32_t g0[4] = {lo2(H01, L01), H01, hi2(L01, H01), lo2(H23, L23)};
+    uint32_t g1[4];
+    if constexpr (D == 3) g1[0] = H23, g1[1] = hi2(L23, H23), g1[2] = 0u, g1[3] = 0u;
+    else g1[0] = H23, g1[1] = 0u, g1[2] = 0u, g1[3] = 0u;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) b[t][d] = (g0[d] & m0) | (g1[d] & m1);
+  }
+}
+
+// layer 1's tile O: its A fragment (lanes 32-63 read lanes 0-31's, KLay::L1) and bias row (per-y c (b1 + W1_y y))
+template <int O>
+__device__ __forceinline__ void l1_read(x3::lds_cptr la, x3::lds_cptr lb, u32x4& a, u32x4& b) {
+  a = x3::lds_rd<O * 512>(la);
+  b = x3::lds_rd<O * 64>(lb);
+}
+
+// tile O of layer 1 for every chain tile (fragments of tiles O, O + 1 in flight on entry; O + 2's issued here)
+template <int O, int NT, int ST>
+__device__ __forceinline__ void l1_tile(x3::lds_cptr la, x3::lds_cptr lb, u32x4 (&fa)[3], u32x4 (&fb)[3],
+                                        const u32x4 (&b1)[NT], f32x4 (&P)[NT][ST]) {
+  if constexpr (O < ST) {
+    if constexpr (O + 2 < ST) l1_read<O + 2>(la, lb, fa[(O + 2) % 3], fb[(O + 2) % 3]);
+    // the pairs of tiles O + 1 and O + 2 are younger than O's
+    x3::lds_wait2<(O + 2 < ST) ? 4 : ((O + 1 < ST) ? 2 : 0)>(fa[O % 3], fb[O % 3]);
+    const f32x4 c = __builtin_bit_cast(f32x4, fb[O % 3]);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) P[t][O] = mfma16(fa[O % 3], b1[t], c);
+    l1_tile<O + 1>(la, lb, fa, fb, b1, P);
+  }
+}
+
 // ---------------------------------------------------------------------------- sampler kernel
 // The reverse-SDE loop (models/diffusion.py:27-46) for the CDE, a = net(x, y, tau) with y folded into the
 // per-y layer-1 bias; mu = g a + 0.5 beta x, x <- x + delta mu + sqrt(delta) g xi (dmip_device.h
@@ -456,7 +506,6 @@ __global__ void __launch_bounds__(KWaves<NT>::NWV * 64, KWaves<NT>::NWV / 4) x3k
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4, j = lane & 15;
   const int yi = blockIdx.y;
-  constexpr int NV = D + 1;  // layer-1 inputs: x, tau (y folded into the bias)
 
   KEngine<D, NT, NOISE, DIAG> eng;
   eng.lds = lds;
@@ -565,22 +614,17 @@ __global__ void __launch_bounds__(KWaves<NT>::NWV * 64, KWaves<NT>::NWV / 4) x3k
       // ---- layer 1 (resident image, one MFMA per tile and chain tile), pre-activations in P
       f32x4 P[NT][ST];
       {
-        u32x4 b1[NT][1];
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-          float v[NV];
-#pragma unroll
-          for (int k = 0; k < D; ++k) v[k] = x[t][k];
-          v[NV - 1] = cf.tau;
-          x3::l1_operand<NV, 1>(v, g, b1[t]);
-        }
-#pragma unroll
-        for (int o = 0; o < ST; ++o) {
-          const u32x4 a = *(const u32x4*)(l1_lane + o * 512);
-          const f32x4 b = eng.bias4(0, o);
-#pragma unroll
-          for (int t = 0; t < NT; ++t) P[t][o] = mfma16(a, b1[t][0], b);
-        }
+        u32x4 b1[NT];
+        l1_operands(x, cf.tau, g, b1);
+        // the A fragments and the per-y bias rows (the MFMAs' C input) by explicit reads two tiles ahead with
+        // counted waits: left to itself the compiler waited lgkmcnt(0) before every tile's MFMAs and routed the
+        // bias through AGPRs (then copied P back out of them, each copy behind the MFMA's full latency)
+        const x3::lds_cptr la = (x3::lds_cptr)l1_lane;
+        const x3::lds_cptr lb = (x3::lds_cptr)(lds + L::BIAS + 16 * g);
+        u32x4 fa[3], fb[3];
+        l1_read<0>(la, lb, fa[0], fb[0]);
+        l1_read<1>(la, lb, fa[1], fb[1]);
+        l1_tile<0>(la, lb, fa, fb, b1, P);
       }
       u32x4 Hh[NT], Hl[NT];
 #pragma unroll
