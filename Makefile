@@ -5,7 +5,8 @@ HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-parameter
 F32OBJS := $(CSRC)/dmip_f32.o $(CSRC)/dmip_f32_cde.o $(CSRC)/dmip_f32_post.o $(CSRC)/dmip_f32_cdiffe.o
-X3OBJS := $(CSRC)/dmip_x3.o $(CSRC)/dmip_x3_cde.o $(CSRC)/dmip_x3_post.o $(CSRC)/dmip_x3_cdiffe.o $(CSRC)/dmip_x3k.o
+X3OBJS := $(CSRC)/dmip_x3.o $(CSRC)/dmip_x3_cde.o $(CSRC)/dmip_x3_post.o $(CSRC)/dmip_x3_cdiffe.o $(CSRC)/dmip_x3k.o \
+          $(CSRC)/dmip_dps_x3.o
 OBJS := $(CSRC)/dmip_kernels.o $(CSRC)/dmip_train.o $(CSRC)/dmip_eval.o $(CSRC)/dmip_surrogate.o $(CSRC)/dmip_gemm.o $(CSRC)/dmip_jets.o $(CSRC)/dmip_step.o $(F32OBJS) $(X3OBJS) $(CSRC)/dmip_capi.o
 HDRS := $(CSRC)/dmip_device.h $(CSRC)/dmip_internal.h include/dmip.h
 
@@ -51,6 +52,10 @@ $(CSRC)/dmip_x3_%.o: $(CSRC)/dmip_x3_%.hip $(CSRC)/dmip_x3.h $(HDRS)
 
 # the k-major multi-tile fp32x3 CDE engine (width 256): its own header
 $(CSRC)/dmip_x3k.o: $(CSRC)/dmip_x3k.hip $(CSRC)/dmip_x3k.h $(CSRC)/dmip_x3.h $(HDRS)
+	$(HIPCC) $(HIPFLAGS) -fno-slp-vectorize -c $< -o $@
+
+# DPS (config 4) on the split-fp16 arithmetic
+$(CSRC)/dmip_dps_x3.o: $(CSRC)/dmip_dps_x3.hip $(CSRC)/dmip_x3.h $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -fno-slp-vectorize -c $< -o $@
 
 $(CSRC)/dmip_capi.o: $(CSRC)/dmip_capi.cpp $(HDRS)

@@ -326,8 +326,11 @@ class Workload:
                 self.weights = "fixture-trained prior (tests/golden/ckpt_prior_scat.npz)"
             self.model.prior_net.to(dev)
             self.flops_sample_step = 2 * F_PRIOR + 2 * F_SUR
-            self.peak = PEAK_F32_TFLOPS
-            self.kernel = "dps_kernel (exact f32)"
+            dprec = "fp32" if args.precision == "fp32" else "fp32x3"
+            self.kw = {"precision": dprec}
+            self.peak = PEAK_F32_TFLOPS if dprec == "fp32" else PEAK_BF16_TFLOPS
+            self.kernel = {"fp32": "dps_kernel (exact f32, forward tangents)",
+                           "fp32x3": "dps_x3_kernel (split-fp16, reverse-mode J^T)"}[dprec]
             self.workload = "scatterometry DPS, surrogate guidance (BASELINE configs[3])"
         self.par = par
 
@@ -415,13 +418,13 @@ def other_configs(args, pkg, lib, dev):
                 wl.weights = "random-init"
             if workload != "dps":
                 wl.kernel = f"{fam[precision]}<{mode},{W},...>"
-            wl.peak = PEAK_F32_TFLOPS if precision == "fp32" or workload == "dps" else PEAK_BF16_TFLOPS
+            wl.peak = PEAK_F32_TFLOPS if precision == "fp32" else PEAK_BF16_TFLOPS
             wl.step(3000)
             el, lm, x = timed(wl, reps, None, 1, dev, seed0=3100)
             lib.device_status(dev)
             ach = wl.flops_sample_step * a.num_steps * wl.n_local / (lm * 1e-3) / 1e12
             out[name] = {"workload": wl.workload, "chains": wl.n_local, "sde_steps": a.num_steps,
-                         "precision": precision if workload != "dps" else "fp32", "value": wl.n_local * reps / el,
+                         "precision": precision, "value": wl.n_local * reps / el,
                          "unit": "samples/s", "launch_ms": lm,
                          "roofline": {"achieved": ach, "peak": wl.peak, "unit": "TFLOP/s", "frac": ach / wl.peak},
                          "kernel": wl.kernel, "weights": wl.weights, "finite": bool(torch.isfinite(x).all())}
@@ -453,7 +456,8 @@ def other_configs(args, pkg, lib, dev):
         out["config1_linear"] = {"error": f"{type(e).__name__}: {e}"}
     sampler("config3_cdiffe_pc_per_gpu", "cdiffe-pc", 125000, 2, "fp32x3")
     sampler("config3_cdiffe_pc_per_gpu_fast", "cdiffe-pc", 125000, 2, "fp16")
-    sampler("config4_dps", "dps", 262144, 1, "fp32")
+    sampler("config4_dps", "dps", 262144, 1, "fp32x3")
+    sampler("config4_dps_exact_f32", "dps", 262144, 1, "fp32")
     sampler("cde_reference_width_512", "cde", 100000, 2, "fp32x3", width=512)
     sampler("posterior_reference_width_512", "cde", 100000, 1, "fp32x3", width=512, posterior=True)
     # CDiffE scatterometry at width 512: fp32x3 with its 96 KiB split layer 1 streamed through the ring (L1R)

@@ -24,7 +24,7 @@ DMIP_PREC_FP16, DMIP_PREC_F32, DMIP_PREC_F32X3 = 0, 1, 2
 DMIP_PREC_BF16 = DMIP_PREC_FP16
 PRECISIONS = {"fp16": DMIP_PREC_FP16, "bf16": DMIP_PREC_BF16, "fp32": DMIP_PREC_F32, "fp32x3": DMIP_PREC_F32X3}
 DMIP_SAMPLER_CDE, DMIP_SAMPLER_POSTERIOR, DMIP_SAMPLER_CDIFFE = 0, 1, 2
-ABI_VERSION = 6
+ABI_VERSION = 7
 DMIP_LOSS_DSM, DMIP_LOSS_DSM_PDE, DMIP_LOSS_PINN, DMIP_LOSS_PINN2 = 0, 1, 2, 3
 DMIP_PDE_NONE, DMIP_PDE_FPE, DMIP_PDE_CFPE = 0, 1, 2
 DMIP_METRIC_L1, DMIP_METRIC_L2 = 0, 1
@@ -39,6 +39,7 @@ EXPORTED = (
     "dmip_sampler_supported_f32", "dmip_posterior_loss_grad", "dmip_loss_grad_f32", "dmip_train_draws",
     "dmip_adam_step", "dmip_em_sample_snapshots", "dmip_train_plan_create", "dmip_train_plan_step",
     "dmip_train_plan_set_counters", "dmip_train_plan_destroy", "dmip_sampler_supported_precision",
+    "dmip_dps_sample_ex",
 )
 DMIP_DPS_NLL, DMIP_DPS_NORM = 0, 1
 
@@ -149,6 +150,10 @@ def _declare(lib):
     lib.dmip_dps_sample.argtypes = [_c_void_p, _c_void_p, ctypes.POINTER(DmipScatNoise), ctypes.POINTER(DmipVpsde),
                                     _c_void_p, _i32, _i64, _i64, _i32, _f32, _f32, _u64, _i32, _f32, _c_void_p,
                                     _c_void_p]
+    lib.dmip_dps_sample_ex.argtypes = [_c_void_p, _c_void_p, ctypes.POINTER(DmipScatNoise), ctypes.POINTER(DmipVpsde),
+                                       _c_void_p, _i32, _i64, _i64, _i32, _f32, _f32, _u64, _i32, _f32, _i32,
+                                       _c_void_p, _c_void_p]
+    lib.dmip_dps_sample_ex.restype = _i32
     for name in ("dmip_train_draws", "dmip_adam_step", "dmip_loss_grad_f32", "dmip_posterior_loss_grad", "dmip_device_status", "dmip_sampler_supported_f32", "dmip_dps_sample", "dmip_mlp_create", "dmip_mlp_destroy", "dmip_mlp_forward", "dmip_em_sample",
                  "dmip_rng_words", "dmip_rng_normals", "dmip_schedule", "dmip_sampler_supported",
                  "dmip_em_sample_stamps", "dmip_em_sample_posterior", "dmip_em_sample_cdiffe",
@@ -416,12 +421,14 @@ def mh_sample(handle, noise, y, n_chains, chain_offset, num_steps, noise_std, se
                                ptr(inj_unif), ptr(x_out), ptr(e_out), stream_of(y.device)))
 
 
-def dps_sample(prior, surrogate, noise, sde, y, n_chains, chain_offset, num_steps, mean, std, seed, mode, zeta, out):
+def dps_sample(prior, surrogate, noise, sde, y, n_chains, chain_offset, num_steps, mean, std, seed, mode, zeta, out,
+               precision="fp32"):
+    """dmip_dps_sample_ex: "fp32" the exact-f32 kernel, "fp32x3" the split-fp16 one (dmip_dps_x3.hip)."""
     calls["dps_sample"] = calls.get("dps_sample", 0) + 1
-    check(lib().dmip_dps_sample(prior.h, surrogate.h, ctypes.byref(noise), ctypes.byref(sde), ptr(y), int(y.shape[0]),
-                                int(n_chains), int(chain_offset), int(num_steps), float(mean), float(std),
-                                ctypes.c_uint64(int(seed) & 0xFFFFFFFFFFFFFFFF), int(mode), float(zeta), ptr(out),
-                                stream_of(y.device)))
+    check(lib().dmip_dps_sample_ex(prior.h, surrogate.h, ctypes.byref(noise), ctypes.byref(sde), ptr(y),
+                                   int(y.shape[0]), int(n_chains), int(chain_offset), int(num_steps), float(mean),
+                                   float(std), ctypes.c_uint64(int(seed) & 0xFFFFFFFFFFFFFFFF), int(mode), float(zeta),
+                                   precision_code(precision), ptr(out), stream_of(y.device)))
 
 
 def posterior_loss_grad(prior_layers, lik_layers, surrogate, noise, lam, sde, x, y, t, eps, grad_prior, grad_lik,

@@ -176,6 +176,12 @@ struct dmip_mlp {
   char* dps_w3 = nullptr;
   char* dps_w4 = nullptr;         // [1][16][64][4], rows >= 3 zero
   float* dps_bias = nullptr;      // b2 | b3 | b4[16]
+  // fp32x3 images of a DPS prior (dmip_dps_x3.hip): the chunk stream, layer 1, the biases; none when a weight is
+  // beyond fp16's range (dps_x3_range: that magnitude)
+  char* dps_x3_img = nullptr;     // [kDpsX3PriorChunks][32 KiB]
+  char* dps_x3_l1 = nullptr;      // [16 tiles][64][8] fp16, scaled by 2 log2 e
+  float* dps_x3_bias = nullptr;   // c b1 | init2 | init3 [256] | out init [16]
+  double dps_x3_range = 0.0;
   // exact-f32 images (DMIP_PREC_F32, dmip_f32.h): every input column + bias as layer 1
   float* f32_l1 = nullptr;        // [W/16][k1q][64]
   char* f32_stream = nullptr;     // [(L-1) W/16 + f32_ot chunks][W/16][64][4]
@@ -202,7 +208,8 @@ struct dmip_mlp {
                     (void*)dps_w3, (void*)dps_w4, (void*)dps_bias, (void*)f32_l1, (void*)f32_stream,
                     (void*)f32_bias, (void*)x3_l1, (void*)x3_l1_full, (void*)x3_stream, (void*)x3_stream_l1r,
                     (void*)x3_bias,
-                    (void*)x3k_stream, (void*)x3k_out, (void*)x3p_stream, (void*)x3p_l1, (void*)x3p_ow})
+                    (void*)x3k_stream, (void*)x3k_out, (void*)x3p_stream, (void*)x3p_l1, (void*)x3p_ow,
+                    (void*)dps_x3_img, (void*)dps_x3_l1, (void*)dps_x3_bias})
       if (p) (void)hipFree(p);
   }
 };
@@ -338,9 +345,37 @@ int pack_x3p(dmip_mlp* net, const float* const* weights, const float* const* bia
 
 #endif  // DMIP_WITH_X3P
 
+// [n_tiles][KQ][hi, lo][64][8] fp16 split of A[r][c] = get(r, c): lane i + 16 g of tile o holds A[16 o + i][kperm16(q,
+// g, m)], m = 0..7 -- pack_x3_layer's layout without its r-form fold (the DPS engine's plain and transposed layers).
+// *maxabs: the largest |A| (the split needs it inside fp16's range)
+template <typename Get>
+std::vector<uint16_t> pack_x3_plain(int n_tiles, int KQ, Get get, double* maxabs) {
+  std::vector<uint16_t> img((size_t)n_tiles * KQ * 2 * 512, 0);
+  for (int o = 0; o < n_tiles; ++o)
+    for (int q = 0; q < KQ; ++q)
+      for (int l = 0; l < 64; ++l)
+        for (int m = 0; m < 8; ++m) {
+          const double v = (double)get(16 * o + (l & 15), kperm16(q, l >> 4, m));
+          *maxabs = std::max(*maxabs, std::fabs(v));
+          uint16_t hi, lo;
+          split_h(v, hi, lo);
+          img[((((size_t)o * KQ + q) * 2 + 0) * 64 + l) * 8 + m] = hi;
+          img[((((size_t)o * KQ + q) * 2 + 1) * 64 + l) * 8 + m] = lo;
+        }
+  return img;
+}
+
+// append an image to a chunk stream, zero-padded to whole 32 KiB chunks
+void append_chunks(std::vector<char>& out, const std::vector<uint16_t>& img) {
+  const size_t bytes = img.size() * 2, padded = (bytes + dmip::kDpsX3Chunk - 1) / dmip::kDpsX3Chunk * dmip::kDpsX3Chunk;
+  const size_t at = out.size();
+  out.resize(at + padded, 0);
+  std::memcpy(out.data() + at, img.data(), bytes);
+}
+
 // layer-1 image over the input columns `cols` (scaled by c): input n at k-slots 3n, 3n+1, 3n+2 with
 // A = [W_hi, W_hi, W_lo] (the kernel's B = [v_hi, v_lo, v_hi])
-std::vector<uint16_t> pack_x3_l1(const float* W1, int W, int in_dim, const std::vector<int>& cols) {
+std::vector<uint16_t> pack_x3_l1(const float* W1, int W, int in_dim, const std::vector<int>& cols, double scale = kC) {
   const int NV = (int)cols.size(), K1Q = x3_k1q(NV), ST = W / 16;
   std::vector<uint16_t> img((size_t)ST * K1Q * 512, 0);
   for (int o = 0; o < ST; ++o)
@@ -350,7 +385,7 @@ std::vector<uint16_t> pack_x3_l1(const float* W1, int W, int in_dim, const std::
           const int i = l & 15, g = l >> 4, s = 32 * q + 8 * g + m, n = s / 3, p = s % 3;
           if (n >= NV) continue;
           uint16_t hi, lo;
-          split_h(kC * (double)W1[(size_t)(16 * o + i) * in_dim + cols[n]], hi, lo);
+          split_h(scale * (double)W1[(size_t)(16 * o + i) * in_dim + cols[n]], hi, lo);
           img[(((size_t)o * K1Q + q) * 64 + l) * 8 + m] = p < 2 ? hi : lo;
         }
   return img;
@@ -381,6 +416,45 @@ void pack_x3_layer(const float* Wl, const float* bl, int n_rows, int W, int n_ti
             const size_t src = (size_t)row * W + kperm16(q, l >> 4, m);
             img[((((size_t)o * KQ + q) * 2 + p) * 64 + l) * 8 + m] = p == 0 ? hi[src] : lo[src];
           }
+}
+
+// the fp32x3 DPS engine's prior images (dmip_dps_x3.hip): layer 1 over (x, t) scaled by 2 log2 e; the forward chunks
+// P2 | P3 (pack_x3_layer: r-form folds) | Pout (folded, scale 1); the reverse chunks P4^T (one k-step: the 3 output
+// rows) | P3^T | P2^T (plain transposes) | P1^T (W1's x columns); biases c b1 | init2 | init3 | out init
+int pack_dps_x3_prior(dmip_mlp* net, const float* const* weights, const float* const* biases) {
+  const int W = 256;
+  const float *W1 = weights[0], *W2 = weights[1], *W3 = weights[2], *W4 = weights[3];
+  double mx = 0.0;
+  std::vector<float> bias((size_t)3 * W + 16, 0.0f);
+  for (int u = 0; u < W; ++u) bias[u] = (float)(kC * (double)biases[0][u]);
+  std::vector<char> chunks;
+  std::vector<uint16_t> img;
+  pack_x3_layer(W2, biases[1], W, W, 16, kC, img, bias.data() + W);
+  for (uint16_t h : img) mx = std::max(mx, std::fabs((double)h2f(h)));
+  append_chunks(chunks, img);
+  pack_x3_layer(W3, biases[2], W, W, 16, kC, img, bias.data() + 2 * W);
+  for (uint16_t h : img) mx = std::max(mx, std::fabs((double)h2f(h)));
+  append_chunks(chunks, img);
+  pack_x3_layer(W4, biases[3], 3, W, 1, 1.0, img, bias.data() + 3 * W);
+  for (uint16_t h : img) mx = std::max(mx, std::fabs((double)h2f(h)));
+  append_chunks(chunks, img);
+  append_chunks(chunks, pack_x3_plain(16, 1, [&](int r, int c) { return c < 3 ? W4[(size_t)c * W + r] : 0.0f; }, &mx));
+  append_chunks(chunks, pack_x3_plain(16, 8, [&](int r, int c) { return W3[(size_t)c * W + r]; }, &mx));
+  append_chunks(chunks, pack_x3_plain(16, 8, [&](int r, int c) { return W2[(size_t)c * W + r]; }, &mx));
+  append_chunks(chunks, pack_x3_plain(1, 8, [&](int r, int c) { return r < 3 ? W1[(size_t)c * 4 + r] : 0.0f; }, &mx));
+  for (size_t i = 0; i < (size_t)W * 4; ++i) mx = std::max(mx, kC * std::fabs((double)W1[i]));
+  if (!(mx <= 65504.0) || chunks.size() != (size_t)dmip::kDpsX3PriorChunks * dmip::kDpsX3Chunk) {
+    net->dps_x3_range = std::isfinite(mx) ? mx : 1e300;
+    return DMIP_OK;  // no fp32x3 DPS for this prior (fp16 range)
+  }
+  const std::vector<uint16_t> l1 = pack_x3_l1(W1, W, 4, {0, 1, 2, 3});
+  std::vector<char> l1b(l1.size() * 2);
+  std::memcpy(l1b.data(), l1.data(), l1b.size());
+  int rc = DMIP_OK;
+  if ((rc = upload(&net->dps_x3_img, chunks)) || (rc = upload(&net->dps_x3_l1, l1b)) ||
+      (rc = upload(&net->dps_x3_bias, bias)))
+    return rc;
+  return DMIP_OK;
 }
 
 // largest magnitude the fp32x3 images would hold in fp16: layer 1 scaled by 2 log2(e), the hidden layers by
@@ -707,7 +781,8 @@ int dmip_mlp_create(int in_dim, int out_dim, int n_hidden, const int* widths, in
     if ((rc = upload(&net->dps_l1, l1)) || (rc = upload(&net->dps_bias, pb)) ||
         (rc = upload(&net->dps_w2, pack_f32_tiles(16, 16, sqm(P2)))) ||
         (rc = upload(&net->dps_w3, pack_f32_tiles(16, 16, sqm(P3)))) ||
-        (rc = upload(&net->dps_w4, pack_f32_tiles(1, 16, [&](int r, int c) { return r < 3 ? P4[(size_t)r * W + c] : 0.0f; })))) {
+        (rc = upload(&net->dps_w4, pack_f32_tiles(1, 16, [&](int r, int c) { return r < 3 ? P4[(size_t)r * W + c] : 0.0f; }))) ||
+        (rc = pack_dps_x3_prior(net, weights, biases))) {
       delete net;
       return rc;
     }
@@ -1198,7 +1273,7 @@ static int loss_grad_bf16_impl(int in_dim, int out_dim, int n_hidden, const int*
                                const float* const* weights_dev, const float* const* biases_dev, const dmip_vpsde* sde,
                                const dmip_loss_cfg* cfg, const float* x_dev, const float* y_dev, const float* t_dev,
                                const float* eps_dev, int64_t batch, float* grad_out_dev, float* loss_out_dev,
-                               void* stream, Workspace* ws) {
+                               void* stream, Workspace* ws, const dmip::TrainFuse* fuse = nullptr) {
   if (!weights_dev || !biases_dev || !sde || !cfg || !x_dev || !y_dev || !t_dev || !eps_dev || !grad_out_dev ||
       !loss_out_dev)
     return fail(DMIP_ERR_INVALID, "null argument");
@@ -1264,7 +1339,8 @@ static int loss_grad_bf16_impl(int in_dim, int out_dim, int n_hidden, const int*
   }
   p.packed = (char*)partials + part_pad;
   p.adj = dmip::train_adj_bytes(batch) ? (float*)((char*)partials + part_pad + packed_pad) : nullptr;
-  e = dmip::launch_loss_grad(p, n_hidden, grad_out_dev, loss_out_dev, partials, n_wg, st);
+  e = fuse ? dmip::launch_loss_grad_fused(p, n_hidden, grad_out_dev, loss_out_dev, partials, n_wg, *fuse, st)
+           : dmip::launch_loss_grad(p, n_hidden, grad_out_dev, loss_out_dev, partials, n_wg, st);
   if (!ws) (void)hipFreeAsync(partials, st);
   if (e != hipSuccess) return hip_fail(e, "loss_grad launch");
   return DMIP_OK;
@@ -1457,13 +1533,21 @@ static int adam_params(int n_tensors, float* const* params, const float* const* 
 // ----------------------------------------------------------------- captured training-step graph
 struct dmip_train_plan {
   hipGraphExec_t exec = nullptr;
+  hipGraph_t graph = nullptr;
   int64_t batch = 0;
   int xdim = 0, ydim = 0;
-  float *x = nullptr, *y = nullptr;          // staging: the batch is copied in before each replay
+  float *x = nullptr, *y = nullptr;          // staging: the batch is copied in at each replay
   float *t = nullptr, *eps = nullptr, *loss = nullptr;  // caller-owned
   char* ws = nullptr;
   dmip::StepCounters* ctr = nullptr;
   int device = 0;
+  // the draws launch stages the batch itself: each step points that kernel node's x_src / y_src at the caller's
+  // batch (hipGraphExecKernelNodeSetParams) instead of two copy nodes; `stage_node` null: copies (fallback)
+  hipGraphNode_t stage_node = nullptr;
+  hipKernelNodeParams stage_kp{};
+  int stage_nargs = 0;
+  alignas(16) char stage_args[3][1024];      // the node's argument values (TrainDrawsParams first)
+  void* stage_argv[3] = {};
 };
 
 // makes `dev` the current device for the guard's scope (and restores the caller's)
@@ -1493,6 +1577,7 @@ static int pointer_device(const void* p) {
 static void plan_free(dmip_train_plan* pl) {
   if (!pl) return;
   if (pl->exec) (void)hipGraphExecDestroy(pl->exec);
+  if (pl->graph) (void)hipGraphDestroy(pl->graph);
   for (void* q : {(void*)pl->x, (void*)pl->y, (void*)pl->ws, (void*)pl->ctr})
     if (q) (void)hipFree(q);
   delete pl;
@@ -1568,10 +1653,11 @@ int dmip_train_plan_create(const dmip_train_plan_desc* d, dmip_train_plan** out)
   // workspace of the loss sequence, sized by a query pass
   Workspace ws;
   ws.query = true;
+  const dmip::TrainFuse* fuse = nullptr;  // bf16: the fused prologue / reduction + Adam launches (set below)
   auto loss_seq = [&](hipStream_t st, Workspace* w) {
     return bf16 ? loss_grad_bf16_impl(d->in_dim, d->out_dim, d->n_hidden, d->widths, d->xdim, d->weights_dev,
                                       d->biases_dev, &d->sde, &d->cfg, pl->x, pl->y, pl->t, pl->eps, B,
-                                      d->grads[0], pl->loss, st, w)
+                                      d->grads[0], pl->loss, st, w, fuse)
                 : loss_grad_f32_impl(d->in_dim, d->out_dim, d->n_hidden, d->widths, d->xdim, d->weights_dev,
                                      d->biases_dev, &d->sde, &d->cfg, pl->x, pl->y, pl->t, pl->eps, nullptr, B,
                                      d->grads[0], pl->loss, st, w);
@@ -1594,7 +1680,12 @@ int dmip_train_plan_create(const dmip_train_plan_desc* d, dmip_train_plan** out)
   }
   dp.draw_ctr = &pl->ctr->draw;
   ap.step_ctr = &pl->ctr->step;
-  // capture: draws -> loss + gradients -> Adam -> advance the counters
+  // the draws launch stages the batch (x_src / y_src set per step in its kernel node)
+  dp.x_src = pl->x, dp.y_src = pl->y, dp.x_dst = pl->x, dp.y_dst = pl->y, dp.ydim = ydim;
+  // bf16 (the config-5 kernel): four launches -- the pack in the draws launch, Adam and the counters in the
+  // gradient reduction (dmip::TrainFuse); exact f32: draws -> loss + gradients -> Adam -> advance the counters
+  const dmip::TrainFuse fz{dp, ap, pl->ctr};
+  if (bf16 && dmip::train_split()) fuse = &fz;
   hipStream_t cs = nullptr;
   if ((e = hipStreamCreateWithFlags(&cs, hipStreamNonBlocking)) != hipSuccess) {
     plan_free(pl);
@@ -1603,19 +1694,52 @@ int dmip_train_plan_create(const dmip_train_plan_desc* d, dmip_train_plan** out)
   hipGraph_t g = nullptr;
   e = hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed);
   if (e == hipSuccess) {
-    hipError_t le = dmip::launch_train_draws(dp, cs);
-    int lrc = le == hipSuccess ? loss_seq(cs, &ws) : DMIP_ERR_HIP;
-    if (lrc == DMIP_OK && (le = dmip::launch_adam(ap, cs)) == hipSuccess) le = dmip::launch_counters_advance(pl->ctr, cs);
+    hipError_t le = hipSuccess;
+    int lrc = DMIP_OK;
+    if (fuse) {
+      lrc = loss_seq(cs, &ws);
+    } else {
+      le = dmip::launch_train_draws(dp, cs);
+      lrc = le == hipSuccess ? loss_seq(cs, &ws) : DMIP_ERR_HIP;
+      if (lrc == DMIP_OK && (le = dmip::launch_adam(ap, cs)) == hipSuccess) le = dmip::launch_counters_advance(pl->ctr, cs);
+    }
     e = hipStreamEndCapture(cs, &g);
     if (e == hipSuccess && (le != hipSuccess || lrc != DMIP_OK)) e = le != hipSuccess ? le : hipErrorUnknown;
   }
   if (e == hipSuccess) e = hipGraphInstantiate(&pl->exec, g, nullptr, nullptr, 0);
-  if (g) (void)hipGraphDestroy(g);
   (void)hipStreamDestroy(cs);
   if (e != hipSuccess) {
+    if (g) (void)hipGraphDestroy(g);
     plan_free(pl);
     return hip_fail(e, "training-step graph capture");
   }
+  pl->graph = g;
+  // the staging kernel node: its arguments are kept here and re-pointed at each step's batch
+  const void* stage_fn = fuse ? dmip::train_plan_prologue_func(d->n_hidden) : dmip::train_draws_func();
+  size_t nn = 0;
+  if (hipGraphGetNodes(g, nullptr, &nn) == hipSuccess && nn > 0) {
+    std::vector<hipGraphNode_t> nodes(nn);
+    if (hipGraphGetNodes(g, nodes.data(), &nn) == hipSuccess)
+      for (size_t i = 0; i < nn && !pl->stage_node; ++i) {
+        hipGraphNodeType ty;
+        hipKernelNodeParams kp{};
+        if (hipGraphNodeGetType(nodes[i], &ty) != hipSuccess || ty != hipGraphNodeTypeKernel) continue;
+        if (hipGraphKernelNodeGetParams(nodes[i], &kp) != hipSuccess || kp.func != stage_fn || !kp.kernelParams) continue;
+        // prologue (TrainDrawsParams, TrainParams, int) or draws (TrainDrawsParams)
+        const size_t sizes[3] = {sizeof(dmip::TrainDrawsParams), sizeof(dmip::TrainParams), sizeof(int)};
+        const int nargs = fuse ? 3 : 1;
+        for (int a = 0; a < nargs; ++a) {
+          std::memcpy(pl->stage_args[a], kp.kernelParams[a], sizes[a]);
+          pl->stage_argv[a] = pl->stage_args[a];
+        }
+        pl->stage_kp = kp;
+        pl->stage_kp.kernelParams = pl->stage_argv;
+        pl->stage_kp.extra = nullptr;
+        pl->stage_nargs = nargs;
+        pl->stage_node = nodes[i];
+      }
+  }
+  (void)hipGetLastError();
   *out = pl;
   return DMIP_OK;
 }
@@ -1624,9 +1748,17 @@ int dmip_train_plan_step(dmip_train_plan* pl, const float* x_dev, const float* y
   if (!pl || !x_dev || (pl->ydim > 0 && !y_dev)) return fail(DMIP_ERR_INVALID, "null argument");
   hipStream_t st = (hipStream_t)stream;
   const DeviceGuard guard(pl->device);
-  hipError_t e = hipMemcpyAsync(pl->x, x_dev, (size_t)pl->batch * pl->xdim * 4, hipMemcpyDeviceToDevice, st);
-  if (e == hipSuccess && pl->ydim > 0)
-    e = hipMemcpyAsync(pl->y, y_dev, (size_t)pl->batch * pl->ydim * 4, hipMemcpyDeviceToDevice, st);
+  hipError_t e = hipSuccess;
+  if (pl->stage_node) {  // the draws launch copies the batch in: point its node at this step's x / y
+    auto* dp = (dmip::TrainDrawsParams*)pl->stage_args[0];
+    dp->x_src = x_dev;
+    dp->y_src = pl->ydim > 0 ? y_dev : pl->y;
+    e = hipGraphExecKernelNodeSetParams(pl->exec, pl->stage_node, &pl->stage_kp);
+  } else {
+    e = hipMemcpyAsync(pl->x, x_dev, (size_t)pl->batch * pl->xdim * 4, hipMemcpyDeviceToDevice, st);
+    if (e == hipSuccess && pl->ydim > 0)
+      e = hipMemcpyAsync(pl->y, y_dev, (size_t)pl->batch * pl->ydim * 4, hipMemcpyDeviceToDevice, st);
+  }
   if (e == hipSuccess) e = hipGraphLaunch(pl->exec, st);
   return e == hipSuccess ? DMIP_OK : hip_fail(e, "training-step graph launch");
 }
@@ -1667,10 +1799,18 @@ struct dmip_surrogate {
   float* l1 = nullptr;
   float* bias = nullptr;
   char* img[7] = {};  // w2, w3, w4, w3t, w2t, w4t, w1t
+  // fp32x3 images (dmip_dps_x3.hip): chunks S2 | S3 | Sout | S4^T | S3^T | S2^T | S1^T, layer 1, biases; none when
+  // a weight is beyond fp16's range (x3_range)
+  char* x3_img = nullptr;
+  char* x3_l1 = nullptr;
+  float* x3_bias = nullptr;  // b1 | b2 | b3 [256] | b4 [32]
+  double x3_range = 0.0;
   ~dmip_surrogate() {
     if (l1) (void)hipFree(l1);
     if (bias) (void)hipFree(bias);
     for (char* p : img)
+      if (p) (void)hipFree(p);
+    for (void* p : {(void*)x3_img, (void*)x3_l1, (void*)x3_bias})
       if (p) (void)hipFree(p);
   }
 };
@@ -1767,6 +1907,29 @@ int dmip_surrogate_create(int in_dim, int out_dim, int n_hidden, const int* widt
       delete s;
       return rc;
     }
+  {  // the fp32x3 DPS engine's images (plain splits; the surrogate is ReLU, no folds)
+    double mx = 0.0;
+    std::vector<char> chunks;
+    append_chunks(chunks, pack_x3_plain(16, 8, [&](int r, int c) { return W2[(size_t)r * kSurW + c]; }, &mx));
+    append_chunks(chunks, pack_x3_plain(16, 8, [&](int r, int c) { return W3[(size_t)r * kSurW + c]; }, &mx));
+    append_chunks(chunks, pack_x3_plain(2, 8, [&](int r, int c) { return r < YD ? W4[(size_t)r * kSurW + c] : 0.0f; }, &mx));
+    append_chunks(chunks, pack_x3_plain(16, 1, [&](int r, int c) { return c < YD ? W4[(size_t)c * kSurW + r] : 0.0f; }, &mx));
+    append_chunks(chunks, pack_x3_plain(16, 8, [&](int r, int c) { return W3[(size_t)c * kSurW + r]; }, &mx));
+    append_chunks(chunks, pack_x3_plain(16, 8, [&](int r, int c) { return W2[(size_t)c * kSurW + r]; }, &mx));
+    append_chunks(chunks, pack_x3_plain(1, 8, [&](int r, int c) { return r < XD ? W1[(size_t)c * XD + r] : 0.0f; }, &mx));
+    for (size_t i = 0; i < (size_t)kSurW * XD; ++i) mx = std::max(mx, std::fabs((double)W1[i]));
+    if (!(mx <= 65504.0) || chunks.size() != (size_t)dmip::kDpsX3SurChunks * dmip::kDpsX3Chunk) {
+      s->x3_range = std::isfinite(mx) ? mx : 1e300;
+    } else {
+      const std::vector<uint16_t> l1x = pack_x3_l1(W1, kSurW, XD, {0, 1, 2}, 1.0);
+      std::vector<char> l1b(l1x.size() * 2);
+      std::memcpy(l1b.data(), l1x.data(), l1b.size());
+      if ((rc = upload(&s->x3_img, chunks)) || (rc = upload(&s->x3_l1, l1b)) || (rc = upload(&s->x3_bias, bias))) {
+        delete s;
+        return rc;
+      }
+    }
+  }
   *out = s;
   return DMIP_OK;
 }
@@ -1880,6 +2043,63 @@ int dmip_dps_sample(const dmip_mlp* prior, const dmip_surrogate* fwd, const dmip
   p.zeta = zeta;
   hipError_t e = dmip::launch_dps(p, n_y, (hipStream_t)stream);
   return e == hipSuccess ? DMIP_OK : hip_fail(e, "dps_sample launch");
+}
+
+int dmip_dps_sample_ex(const dmip_mlp* prior, const dmip_surrogate* fwd, const dmip_scat_noise* noise,
+                       const dmip_vpsde* sde, const float* y_dev, int n_y, int64_t n_chains, int64_t chain_offset,
+                       int num_steps, float mean, float stdv, uint64_t seed, int mode, float zeta, int precision,
+                       float* x_out_dev, void* stream) {
+  if (precision == DMIP_PREC_F32)
+    return dmip_dps_sample(prior, fwd, noise, sde, y_dev, n_y, n_chains, chain_offset, num_steps, mean, stdv, seed,
+                           mode, zeta, x_out_dev, stream);
+  if (precision != DMIP_PREC_F32X3) return fail(DMIP_ERR_INVALID, "DPS precision: DMIP_PREC_F32 or DMIP_PREC_F32X3");
+  if (!prior || !fwd || !sde || !y_dev || !x_out_dev) return fail(DMIP_ERR_INVALID, "null argument");
+  if (mode != DMIP_DPS_NLL && mode != DMIP_DPS_NORM) return fail(DMIP_ERR_INVALID, "unknown DPS guidance mode");
+  dmip::DpsX3Params p{};
+  if (mode == DMIP_DPS_NLL) {
+    dmip::SurrogateParams sp{};
+    if (int rc = noise_check(noise, sp)) return rc;
+    p.a = sp.a;
+    p.b2 = sp.b2;
+  }
+  if (!prior->dps_l1)
+    return fail(DMIP_ERR_UNSUPPORTED, "DPS prior must be an x,t network (MLP2) with xdim 3 and hidden layers [256]*3");
+  if (!prior->dps_x3_img || !fwd->x3_img)
+    return fail(DMIP_ERR_UNSUPPORTED, "fp32x3 DPS: a weight is outside the fp16 range of the split engine (largest |w| " +
+                                          std::to_string(std::max(prior->dps_x3_range, fwd->x3_range)) +
+                                          " > 65504); use DMIP_PREC_F32");
+  if (n_y < 1 || n_y > 65535) return fail(DMIP_ERR_INVALID, "n_y must be in [1, 65535]");
+  if (n_chains < 0 || chain_offset < 0) return fail(DMIP_ERR_INVALID, "negative chain count/offset");
+  if (num_steps < 1) return fail(DMIP_ERR_INVALID, "num_steps must be >= 1");
+  if (!(sde->T > 0.0)) return fail(DMIP_ERR_INVALID, "T must be > 0");
+  if (!(zeta >= 0.0f)) return fail(DMIP_ERR_INVALID, "zeta must be >= 0");
+  if (n_chains == 0) return DMIP_OK;
+  hipStream_t st = (hipStream_t)stream;
+  p.pimg = prior->dps_x3_img;
+  p.simg = fwd->x3_img;
+  p.pl1 = prior->dps_x3_l1;
+  p.sl1 = fwd->x3_l1;
+  p.pbias = prior->dps_x3_bias;
+  p.sbias = fwd->x3_bias;
+  p.y = y_dev;
+  p.n_chains = n_chains;
+  p.chain_offset = chain_offset;
+  p.num_steps = num_steps;
+  p.T = (float)sde->T;
+  p.bmin = (float)sde->beta_min;
+  p.bdiff = (float)(sde->beta_max - sde->beta_min);
+  p.delta = (float)(sde->T / (double)num_steps);
+  p.sqrt_delta = (float)std::sqrt(sde->T / (double)num_steps);
+  p.mean = mean;
+  p.stdv = stdv;
+  p.zeta = zeta;
+  p.mode = mode;
+  p.seed = seed;
+  p.x_out = x_out_dev;
+  p.err = status_word(dmip::stream_device(st));
+  if (!p.err) return fail(DMIP_ERR_ALLOC, "device status word");
+  hipError_t e = dmip::launch_dps_x3(p, n_y, st);
+  return e == hipSuccess ? DMIP_OK : hip_fail(e, "dps_sample (fp32x3) launch");
 }
 
 }  // extern "C"

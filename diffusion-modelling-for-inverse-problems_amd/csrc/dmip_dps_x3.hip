@@ -1,0 +1,533 @@
+// Diffusion posterior sampling (BASELINE config 4; dmip_surrogate.hip dps_kernel documents the method) at the
+// reference's fp32 accuracy on the fp16 matrix rate: every product as the three-term split of dmip_x3.h
+// (W_hi h_hi + W_hi h_lo + W_lo h_hi on v_mfma_f32_16x16x32_f16, fp32 accumulation).
+//
+// Per step and chain (tau = T - t_i):
+//   s = prior(x, tau)                                   MLP2 [256]^3, double tanh on layer 1 (nets.py:37-57)
+//   x0 = (x + var s) / mean_weight                      Tweedie
+//   f = F(x0); v = dL/df                                the scatterometry surrogate (utils_scatterometry.py:8-25)
+//   gx = J_F^T v                                        its reverse pass (ReLU masks)
+//   G = (gx + var J_s^T gx) / mean_weight               the prior's vector-Jacobian product (reverse pass)
+//   x <- EM(x, g s) - lambda G
+// The exact-f32 kernel forms J_s by forward tangents (four prior passes); here one reverse pass through the prior
+// replaces the three tangent passes: the forward keeps the hidden tanh layers' derivatives (4 r (1 - r) in r-form)
+// in registers, 128 per lane; layer 1's (16 r1 (1 - r1) r2 (1 - r2) of its double tanh) is recomputed in the
+// reverse pass from its pre-activation, one MFMA per tile on the resident image.
+//
+// Layout (one wave = 16 chains, four waves per workgroup, one per SIMD): a layer's output tile is 16 units x 16
+// chains (lane (g, j): units 16 o + 4 g + r of chain j), which is the next layer's B operand with no lane movement
+// (dmip_x3.h). Every 256-wide layer streams from L2 through a 4-slot LDS ring in 32 KiB chunks of two output tiles
+// (hi + lo fragments of all eight k-steps); the per-step chunk stream is the prior's forward (hidden 2, 3, output),
+// the surrogate's forward (hidden 2, 3, output), its reverse pass (W4^T, W3^T, W2^T, W1^T) and the prior's reverse
+// pass (W4^T, W3^T, W2^T, W1's x columns): 70 chunks. Both networks' layer 1 and all biases are LDS-resident.
+// The reverse passes carry a per-chain power-of-two scale (exact) so the split operands stay inside fp16's range;
+// a surrogate activation or an input beyond it is reported (kErrRange, dmip_device_status), as the fp32x3 samplers
+// do, and the Python default resamples in exact f32.
+#include "dmip_x3.h"
+
+namespace dmip {
+namespace dx3 {
+
+using x3::f32x4;
+using x3::lds_cptr;
+using x3::mfma16;
+
+constexpr int W = 256, ST = 16, KQ = 8, CT = 2, TILE = KQ * 2048, CHUNK = CT * TILE, NCH = ST / CT;
+constexpr int NW = 4, R = 4, PPW = CHUNK / 1024 / NW;
+static_assert(CHUNK == 32768 && PPW == 8, "ring geometry");
+// the per-step chunk stream: prior image chunks [0, 17) = P2 (8) | P3 (8) | Pout (1), then the surrogate's 35,
+// then prior chunks [17, 35) = P4^T (1) | P3^T (8) | P2^T (8) | P1^T (1)
+constexpr int NPF = 17, NS = 35, NPB = 18, NSTREAM = NPF + NS + NPB;
+
+// LDS
+constexpr int RING = 0;
+constexpr int PL1 = RING + R * CHUNK;        // prior layer 1: [16 tiles][32 lanes][16 B] (lanes 32-63 read 0-31)
+constexpr int SL1 = PL1 + ST * 512;          // surrogate layer 1, same layout
+constexpr int PB = SL1 + ST * 512;           // prior: c b1 | init2 | init3 [256] | out init [16]
+constexpr int SB = PB + (3 * W + 16) * 4;    // surrogate: b1 | b2 | b3 [256] | b4 [32]
+constexpr int YO = SB + (3 * W + 32) * 4;    // the workgroup's y [32]
+constexpr int TOTAL = YO + 32 * 4;
+static_assert(TOTAL <= 160 * 1024, "LDS budget");
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+struct Eng {
+  char* lds;
+  const char* pimg;
+  const char* simg;
+  int c_issue, s_issue, s_read;
+  int w, lane, g;
+
+  __device__ __forceinline__ void ring_issue() {
+    const int c = __builtin_amdgcn_readfirstlane(c_issue);
+    const char* src = c < NPF ? pimg + (size_t)c * CHUNK
+                              : (c < NPF + NS ? simg + (size_t)(c - NPF) * CHUNK : pimg + (size_t)(c - NS) * CHUNK);
+    const uint64_t addr = (uint64_t)src;
+    const char* base = (const char*)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(addr >> 32)) << 32) |
+                                     (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)addr));
+    asm volatile("" : "+s"(base));  // keep the per-chunk address out of the loop-invariant hoist
+    char* dst = lds + RING + __builtin_amdgcn_readfirstlane(s_issue) * CHUNK;
+#pragma unroll
+    for (int q = 0; q < PPW; ++q) {
+      const int piece = w * PPW + q;
+      glds16(base + piece * 1024, dst + piece * 1024, lane);
+    }
+    c_issue = c_issue + 1 == NSTREAM ? 0 : c_issue + 1;
+    s_issue = s_issue + 1 == R ? 0 : s_issue + 1;
+  }
+
+  // the next chunk of the stream, landed (own pieces counted, the others' by the barrier); the slot read one
+  // chunk ago is refilled R - 1 chunks ahead
+  __device__ __forceinline__ lds_cptr chunk_sync() {
+    wait_vmcnt<(R - 2) * PPW>();
+    lds_barrier();
+    ring_issue();
+    const char* slot = lds + RING + s_read * CHUNK;
+    s_read = s_read + 1 == R ? 0 : s_read + 1;
+    return (lds_cptr)(slot + lane * 16);
+  }
+
+  __device__ __forceinline__ f32x4 bias4(int off_bytes, int tile) const {
+    return *(const f32x4*)(lds + off_bytes + (16 * tile + 4 * g) * 4);
+  }
+};
+
+// (hi, lo) B operand of k-step q from two accumulator-form tiles' f32 values v[2 q], v[2 q + 1] (dmip_x3.h
+// act_store's dword order)
+__device__ __forceinline__ void store_pair(const float (&a)[4], int o, u32x4 (&Oh)[KQ], u32x4 (&Ol)[KQ]) {
+  uint32_t h0, l0, h1, l1;
+  x3::split_pair(a[0], a[1], h0, l0);
+  x3::split_pair(a[2], a[3], h1, l1);
+  const int q = o >> 1, d = (o & 1) * 2;
+  Oh[q][d] = h0, Oh[q][d + 1] = h1;
+  Ol[q][d] = l0, Ol[q][d + 1] = l1;
+}
+
+__device__ __forceinline__ bool beyond_fp16(float v) { return !(__builtin_fabsf(v) <= 65504.0f); }
+
+// The per-tile epilogues of a 256 -> 256 layer (tile o of the layer's output, f32 pre-activations z):
+//   PriorFwd:  r = 1 / (1 + 2^z) (z pre-scaled by 2 log2 e; the next layer is folded for r), D = 4 r (1 - r)
+//   SurFwd:    h = relu(z), mask bit, range flag
+//   Back:      g = z * D (prior, tanh') or z * mask (surrogate, relu') -- the reverse pass's next B operand
+struct EpiPriorFwd {
+  float (*D)[4];
+  __device__ __forceinline__ void operator()(const f32x4& z, int o, u32x4 (&Oh)[KQ], u32x4 (&Ol)[KQ]) const {
+    float r[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      r[k] = x3::x3_act_r(z[k]);
+      D[o][k] = 4.0f * r[k] * (1.0f - r[k]);
+    }
+    store_pair(r, o, Oh, Ol);
+  }
+};
+struct EpiSurFwd {
+  uint32_t* m;  // [2]: bit 4 (o & 7) + k of word o >> 3
+  bool* oor;
+  __device__ __forceinline__ void operator()(const f32x4& z, int o, u32x4 (&Oh)[KQ], u32x4 (&Ol)[KQ]) const {
+    float h[4];
+    bool bad = false;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const bool pos = z[k] > 0.0f;
+      h[k] = pos ? z[k] : 0.0f;
+      m[o >> 3] |= (pos ? 1u : 0u) << ((o & 7) * 4 + k);
+      bad |= beyond_fp16(h[k]);
+    }
+    *oor |= bad;
+    store_pair(h, o, Oh, Ol);
+  }
+};
+struct EpiBackD {
+  const float (*D)[4];
+  bool* oor;
+  __device__ __forceinline__ void operator()(const f32x4& z, int o, u32x4 (&Oh)[KQ], u32x4 (&Ol)[KQ]) const {
+    float v[4];
+    bool bad = false;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      v[k] = z[k] * D[o][k];
+      bad |= beyond_fp16(v[k]);
+    }
+    *oor |= bad;
+    store_pair(v, o, Oh, Ol);
+  }
+};
+// the reverse pass into layer 1: g = z * dh1/dz1 with layer 1's double-tanh derivative recomputed per tile from its
+// pre-activation (one MFMA on the resident image; 64 registers fewer than keeping it from the forward)
+struct EpiBackL1 {
+  const char* lds;
+  int lane, g;
+  u32x4 b1;
+  bool* oor;
+  __device__ __forceinline__ void operator()(const f32x4& z, int o, u32x4 (&Oh)[KQ], u32x4 (&Ol)[KQ]) const {
+    const u32x4 a = *(const u32x4*)(lds + PL1 + o * 512 + (lane & 31) * 16);
+    const f32x4 c = *(const f32x4*)(lds + PB + (16 * o + 4 * g) * 4);
+    const f32x4 z1 = mfma16(a, b1, c);
+    float v[4];
+    bool bad = false;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float r1 = x3::x3_act_r(z1[k]);
+      const float r2 = x3::x3_act_r(__builtin_fmaf(-2.0f * kTanhScale, r1, kTanhScale));
+      v[k] = z[k] * (16.0f * r1 * (1.0f - r1) * r2 * (1.0f - r2));
+      bad |= beyond_fp16(v[k]);
+    }
+    *oor |= bad;
+    store_pair(v, o, Oh, Ol);
+  }
+};
+struct EpiBackMask {
+  const uint32_t* m;
+  bool* oor;
+  __device__ __forceinline__ void operator()(const f32x4& z, int o, u32x4 (&Oh)[KQ], u32x4 (&Ol)[KQ]) const {
+    float v[4];
+    bool bad = false;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      v[k] = ((m[o >> 3] >> ((o & 7) * 4 + k)) & 1u) ? z[k] : 0.0f;
+      bad |= beyond_fp16(v[k]);
+    }
+    *oor |= bad;
+    store_pair(v, o, Oh, Ol);
+  }
+};
+
+// a streamed 256 -> 256 layer: NCH chunks of CT tiles; accumulators start at the bias (bias_off >= 0) or zero; each
+// chunk's tiles go to the epilogue while the next chunk's MFMAs run
+template <typename Epi>
+__device__ __forceinline__ void layer256(Eng& e, const u32x4 (&Hh)[KQ], const u32x4 (&Hl)[KQ], int bias_off,
+                                         const Epi& epi, u32x4 (&Oh)[KQ], u32x4 (&Ol)[KQ]) {
+  f32x4 pend[CT];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    f32x4 acc[CT];
+#pragma unroll
+    for (int t = 0; t < CT; ++t) acc[t] = bias_off >= 0 ? e.bias4(bias_off, c * CT + t) : f32x4{0.f, 0.f, 0.f, 0.f};
+    x3::lgkm_drain();
+    const lds_cptr ch = e.chunk_sync();
+    x3::split_product<KQ, CT * KQ, 2>(ch, Hh, Hl, acc);
+    if (c > 0) {
+#pragma unroll
+      for (int t = 0; t < CT; ++t) epi(pend[t], (c - 1) * CT + t, Oh, Ol);
+    }
+#pragma unroll
+    for (int t = 0; t < CT; ++t) pend[t] = acc[t];
+  }
+#pragma unroll
+  for (int t = 0; t < CT; ++t) epi(pend[t], (NCH - 1) * CT + t, Oh, Ol);
+}
+
+// one chunk of NTL tiles over all KQ k-steps of a 256-wide input (output layers, the layer-1 transposes)
+template <int NTL>
+__device__ __forceinline__ void small256(Eng& e, const u32x4 (&Hh)[KQ], const u32x4 (&Hl)[KQ], int bias_off,
+                                         f32x4 (&acc)[NTL]) {
+#pragma unroll
+  for (int t = 0; t < NTL; ++t) acc[t] = bias_off >= 0 ? e.bias4(bias_off, t) : f32x4{0.f, 0.f, 0.f, 0.f};
+  x3::lgkm_drain();
+  const lds_cptr ch = e.chunk_sync();
+  x3::split_product<KQ, NTL * KQ, 2>(ch, Hh, Hl, acc);
+}
+
+// the transposed output layers (16 tiles, one k-step: the output rows): B = the split of the reverse pass's input
+// vector; in two halves of 8 tiles, the first half's epilogue beside the second half's MFMAs (32 accumulator
+// registers live instead of 64)
+template <typename Epi>
+__device__ __forceinline__ void wide1(Eng& e, const u32x4& Bh, const u32x4& Bl, const Epi& epi, u32x4 (&Oh)[KQ],
+                                      u32x4 (&Ol)[KQ]) {
+  const u32x4 bh[1] = {Bh}, bl[1] = {Bl};
+  const lds_cptr ch = e.chunk_sync();
+  f32x4 a0[ST / 2], a1[ST / 2];
+#pragma unroll
+  for (int t = 0; t < ST / 2; ++t) a0[t] = a1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  x3::split_product<1, ST / 2, 2>(ch, bh, bl, a0);
+  x3::split_product<1, ST / 2, 2>(ch + ST * 1024, bh, bl, a1);
+#pragma unroll
+  for (int t = 0; t < ST / 2; ++t) epi(a0[t], t, Oh, Ol);
+#pragma unroll
+  for (int t = 0; t < ST / 2; ++t) epi(a1[t], ST / 2 + t, Oh, Ol);
+}
+
+template <int O, typename Act>
+__device__ __forceinline__ void l1_step(lds_cptr la, lds_cptr lb, u32x4 (&fa)[3], u32x4 (&fb)[3], const u32x4& b,
+                                        const Act& act) {
+  if constexpr (O < ST) {
+    if constexpr (O + 2 < ST) fa[(O + 2) % 3] = x3::lds_rd<(O + 2) * 512>(la), fb[(O + 2) % 3] = x3::lds_rd<(O + 2) * 64>(lb);
+    x3::lds_wait2<(O + 2 < ST) ? 4 : ((O + 1 < ST) ? 2 : 0)>(fa[O % 3], fb[O % 3]);
+    act(mfma16(fa[O % 3], b, __builtin_bit_cast(f32x4, fb[O % 3])), O);
+    l1_step<O + 1>(la, lb, fa, fb, b, act);
+  }
+}
+
+// a resident layer 1 ([16 tiles][32 lanes] image, one MFMA per tile) from the B operand b, then each tile to `act`
+template <typename Act>
+__device__ __forceinline__ void layer1(const Eng& e, int l1_off, int bias_off, const u32x4& b, const Act& act) {
+  const lds_cptr la = (lds_cptr)(e.lds + l1_off + (e.lane & 31) * 16);
+  const lds_cptr lb = (lds_cptr)(e.lds + bias_off + 16 * e.g);
+  u32x4 fa[3], fb[3];
+  fa[0] = x3::lds_rd<0>(la), fb[0] = x3::lds_rd<0>(lb);
+  fa[1] = x3::lds_rd<512>(la), fb[1] = x3::lds_rd<64>(lb);
+  l1_step<0>(la, lb, fa, fb, b, act);
+}
+// layer-1 B operand over NV <= 5 inputs: input n in k-slots 3n, 3n + 1, 3n + 2 as [hi, lo, hi] (x3::l1_operand's
+// layout), lane group 0 slots 0-7, group 1 slots 8-15, groups 2-3 zero
+template <int NV>
+__device__ __forceinline__ u32x4 l1_b(const float (&v)[NV], int g) {
+  u32x4 b[1];
+  x3::l1_operand<NV, 1>(v, g, b);
+  return b[0];
+}
+
+// a per-chain vector of up to 4 components (all lanes of the chain hold it) as the B operand of a one-k-step
+// transposed layer: rows 0..3 of the k-step are lane group 0's m = 0..3 (kperm16(0, 0, m) = m)
+__device__ __forceinline__ void vec_b(const float (&v)[4], int g, u32x4& bh, u32x4& bl) {
+  uint32_t h0, l0, h1, l1;
+  x3::split_pair(v[0], v[1], h0, l0);
+  x3::split_pair(v[2], v[3], h1, l1);
+  const bool z = g != 0;
+  bh = u32x4{z ? 0u : h0, z ? 0u : h1, 0u, 0u};
+  bl = u32x4{z ? 0u : l0, z ? 0u : l1, 0u, 0u};
+}
+
+// rows 0..3 of an accumulator tile live in lane group 0 (registers 0..3): every lane of chain j gets them
+__device__ __forceinline__ float bcast_g0(float v) {
+  const auto s1 = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(__builtin_amdgcn_permlane32_swap(s1[0], s1[0], false, false)[0]);
+}
+
+// 2^e with e = the exponent of max |v| (exact scaling: the reverse passes are linear per chain)
+__device__ __forceinline__ float pow2_of(float m) {
+  if (!(m > 0.0f) || !(m < 3.0e38f)) return 1.0f;
+  int e;
+  (void)frexpf(m, &e);
+  return ldexpf(1.0f, e);
+}
+
+__global__ void __launch_bounds__(NW * 64, 1) dps_x3_kernel(DpsX3Params p) {
+  __shared__ __attribute__((aligned(16))) char lds[TOTAL];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, j = lane & 15;
+  const int yi = blockIdx.y;
+  const long long c_local = (long long)blockIdx.x * (NW * 16) + w * 16 + j;
+  const bool valid = c_local < p.n_chains;
+  Eng e{lds, p.pimg, p.simg, 0, 0, 0, w, lane, g};
+  {
+    // resident parts: the two layer-1 images (lanes 0-31 of each tile), the biases, y
+    const uint4* s1 = (const uint4*)p.pl1;
+    const uint4* s2 = (const uint4*)p.sl1;
+    uint4* d1 = (uint4*)(lds + PL1);
+    uint4* d2 = (uint4*)(lds + SL1);
+    for (int i = threadIdx.x; i < ST * 32; i += NW * 64) {
+      d1[i] = s1[(i >> 5) * 64 + (i & 31)];
+      d2[i] = s2[(i >> 5) * 64 + (i & 31)];
+    }
+    float* pb = (float*)(lds + PB);
+    for (int i = threadIdx.x; i < 3 * W + 16; i += NW * 64) pb[i] = p.pbias[i];
+    float* sb = (float*)(lds + SB);
+    for (int i = threadIdx.x; i < 3 * W + 32; i += NW * 64) sb[i] = p.sbias[i];
+    float* yo = (float*)(lds + YO);
+    for (int i = threadIdx.x; i < 32; i += NW * 64) yo[i] = i < kSurYdim ? p.y[(size_t)yi * kSurYdim + i] : 0.0f;
+    __syncthreads();
+    for (int q = 0; q < R - 1; ++q) e.ring_issue();
+  }
+  const float* ylds = (const float*)(lds + YO);
+
+  Rng rng = rng_init(p.seed, (uint64_t)(p.chain_offset + c_local), (uint64_t)yi);
+  float x[3];
+  {
+    float n0[3];
+    rng_normals<3>(rng, n0);
+#pragma unroll
+    for (int d = 0; d < 3; ++d) x[d] = __fadd_rn(__fmul_rn(n0[d], p.stdv), p.mean);
+  }
+  bool oor = false;
+  const int S = p.num_steps;
+  for (int i = 0; i < S; ++i) {
+    const float4 c4 = ((const float4*)p.coef)[2 * i];      // tau, beta, g (dmip_device.h step_coef)
+    const float4 c5 = ((const float4*)p.coef)[2 * i + 1];  // mean_weight, var (vp_mean_weight, vp_std^2)
+    const StepCoef cf{c4.x, c4.y, c4.z};
+    const float mw = c5.x, var = c5.y;
+    for (int d = 0; d < 3; ++d) oor |= beyond_fp16(x[d]);
+
+    // ---- prior forward: layer 1 (double tanh), hidden 2, hidden 3 (derivatives kept), output rows 0..2
+    float D2[ST][4], D3[ST][4];
+    u32x4 Ah[KQ], Al[KQ], Bh[KQ], Bl[KQ];
+    const float vin[4] = {x[0], x[1], x[2], cf.tau};
+    const u32x4 b1p = l1_b<4>(vin, g);
+    layer1(e, PL1, PB, b1p, [&](const f32x4& z, int o) {
+      float r2[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) r2[k] = x3::x3_act_r2(z[k]);
+      store_pair(r2, o, Ah, Al);
+    });
+    layer256(e, Ah, Al, PB + W * 4, EpiPriorFwd{D2}, Bh, Bl);
+    layer256(e, Bh, Bl, PB + 2 * W * 4, EpiPriorFwd{D3}, Ah, Al);
+    float sc[3];
+    {
+      f32x4 acc[1];
+      small256<1>(e, Ah, Al, PB + 3 * W * 4, acc);
+#pragma unroll
+      for (int d = 0; d < 3; ++d) sc[d] = bcast_g0(acc[0][d]);
+    }
+
+    // ---- Tweedie estimate, surrogate forward (masks kept)
+    float x0h[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      x0h[d] = (x[d] + var * sc[d]) / mw;
+      oor |= beyond_fp16(x0h[d]);
+    }
+    uint32_t m1[2] = {0u, 0u}, m2[2] = {0u, 0u}, m3[2] = {0u, 0u};
+    layer1(e, SL1, SB, l1_b<3>(x0h, g), [&](const f32x4& z, int o) {
+      float h[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const bool pos = z[k] > 0.0f;
+        h[k] = pos ? z[k] : 0.0f;
+        m1[o >> 3] |= (pos ? 1u : 0u) << ((o & 7) * 4 + k);
+        oor |= beyond_fp16(h[k]);
+      }
+      store_pair(h, o, Ah, Al);
+    });
+    layer256(e, Ah, Al, SB + W * 4, EpiSurFwd{m2, &oor}, Bh, Bl);
+    layer256(e, Bh, Bl, SB + 2 * W * 4, EpiSurFwd{m3, &oor}, Ah, Al);
+    f32x4 f[2];
+    small256<2>(e, Ah, Al, SB + 3 * W * 4, f);
+
+    // ---- the guidance's output-space vector v = dL/df and its step size (dps_kernel's two modes)
+    f32x4 v[2];
+    float scale;
+    if (p.mode == 0) {  // NLL: the likelihood terms of get_log_posterior (no boundary prior)
+      const float a2 = p.a * p.a;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = 16 * t + 4 * g + r;
+          float vk = 0.0f;
+          if (row < kSurYdim) {
+            const float fk = f[t][r];
+            const float af = p.a * fk;
+            const float pref = af * af + p.b2;
+            const float res = ylds[row] - fk;
+            const float q = res * res / pref;
+            vk = (a2 * fk * (1.0f - q) - res) / pref;
+          }
+          v[t][r] = vk;
+        }
+      scale = p.zeta * p.delta * cf.beta;  // zeta delta g^2
+    } else {  // NORM: v = d||r||^2/df = -2 r, step zeta / ||r||
+      float rr = 0.0f;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = 16 * t + 4 * g + r;
+          const float res = row < kSurYdim ? ylds[row] - f[t][r] : 0.0f;
+          rr += res * res;
+          v[t][r] = -2.0f * res;
+        }
+      rr += __shfl_xor(rr, 16, 64);
+      rr += __shfl_xor(rr, 32, 64);
+      scale = p.zeta * __frsqrt_rn(fmaxf(rr, 1e-30f));
+    }
+
+    // ---- surrogate reverse pass gx = J_F^T v, scaled per chain by a power of two (exact)
+    float gx[3];
+    {
+      float mx = 0.0f;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, __builtin_fabsf(v[t][r]));
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float s2 = pow2_of(mx), is2 = 1.0f / s2;
+      float vs[2][4];
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) vs[t][r] = v[t][r] * is2;
+      // B of the one-k-step W4^T: rows 0..31 = output rows (tiles 0, 1 in m = 0..3, 4..7)
+      uint32_t h0, l0, h1, l1, h2, l2, h3, l3;
+      x3::split_pair(vs[0][0], vs[0][1], h0, l0);
+      x3::split_pair(vs[0][2], vs[0][3], h1, l1);
+      x3::split_pair(vs[1][0], vs[1][1], h2, l2);
+      x3::split_pair(vs[1][2], vs[1][3], h3, l3);
+      wide1(e, u32x4{h0, h1, h2, h3}, u32x4{l0, l1, l2, l3}, EpiBackMask{m3, &oor}, Ah, Al);
+      layer256(e, Ah, Al, -1, EpiBackMask{m2, &oor}, Bh, Bl);
+      layer256(e, Bh, Bl, -1, EpiBackMask{m1, &oor}, Ah, Al);
+      f32x4 acc[1];
+      small256<1>(e, Ah, Al, -1, acc);
+#pragma unroll
+      for (int d = 0; d < 3; ++d) gx[d] = bcast_g0(acc[0][d]) * s2;
+    }
+
+    // ---- prior reverse pass: J_s^T gx, same scaling
+    float jt[3];
+    {
+      const float mx = fmaxf(fmaxf(__builtin_fabsf(gx[0]), __builtin_fabsf(gx[1])), __builtin_fabsf(gx[2]));
+      const float s2 = pow2_of(mx), is2 = 1.0f / s2;
+      const float u[4] = {gx[0] * is2, gx[1] * is2, gx[2] * is2, 0.0f};
+      u32x4 bh, bl;
+      vec_b(u, g, bh, bl);
+      wide1(e, bh, bl, EpiBackD{D3, &oor}, Ah, Al);
+      layer256(e, Ah, Al, -1, EpiBackD{D2, &oor}, Bh, Bl);
+      layer256(e, Bh, Bl, -1, EpiBackL1{lds, lane, g, b1p, &oor}, Ah, Al);
+      f32x4 acc[1];
+      small256<1>(e, Ah, Al, -1, acc);
+#pragma unroll
+      for (int d = 0; d < 3; ++d) jt[d] = bcast_g0(acc[0][d]) * s2;
+    }
+
+    // ---- EM predictor with the guidance step (dps_kernel's update)
+    float xi[3];
+    rng_normals<3>(rng, xi);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const float gt = (gx[k] + var * jt[k]) / mw;
+      const float xe = em_update(x[k], __fmul_rn(cf.g, sc[k]), xi[k], cf, p.delta, p.sqrt_delta);
+      x[k] = xe - scale * gt;
+    }
+  }
+  wait_vmcnt<0>();  // the prefetched chunks of a step that never ran land before the workgroup exits
+  x3::report_range(oor && valid, p.err, lane);
+  if (valid && g == 0) {
+    float* dst = p.x_out + ((size_t)yi * p.n_chains + c_local) * 3;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) dst[d] = x[d];
+  }
+}
+
+// the per-step coefficients: (tau, beta, g, 0), (mean_weight, var, 0, 0) -- the device functions every sampler uses
+__global__ void dps_x3_coef_kernel(float4* coef, int S, float T, float bmin, float bdiff) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < S) {
+    const StepCoef c = step_coef(i, S, T, bmin, bdiff);
+    const float sd = vp_std(c.tau, bmin, bdiff);
+    coef[2 * i] = make_float4(c.tau, c.beta, c.g, 0.0f);
+    coef[2 * i + 1] = make_float4(vp_mean_weight(c.tau, bmin, bdiff), sd * sd, 0.0f, 0.0f);
+  }
+}
+
+}  // namespace dx3
+
+hipError_t launch_dps_x3(const DpsX3Params& p, int n_y, hipStream_t st) {
+  const long long per_wg = dx3::NW * 16;
+  const int S = p.num_steps > 0 ? p.num_steps : 1;
+  float4* coef = nullptr;
+  hipError_t e = hipMallocAsync((void**)&coef, (size_t)2 * S * sizeof(float4), st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(dx3::dps_x3_coef_kernel, dim3((unsigned)((S + 255) / 256)), dim3(256), 0, st, coef, S, p.T, p.bmin,
+                     p.bdiff);
+  DpsX3Params q = p;
+  q.coef = (const float*)coef;
+  const dim3 grid((unsigned)((p.n_chains + per_wg - 1) / per_wg), (unsigned)n_y), block(dx3::NW * 64);
+  hipLaunchKernelGGL(dx3::dps_x3_kernel, grid, block, 0, st, q);
+  e = hipGetLastError();
+  (void)hipFreeAsync(coef, st);
+  return e;
+}
+
+}  // namespace dmip

@@ -187,6 +187,31 @@ struct DpsParams {
 
 hipError_t launch_dps(const DpsParams& p, int n_y, hipStream_t st);
 
+// DPS at fp32 accuracy on the fp16 matrix rate (dmip_dps_x3.hip): x3-split images of the prior (MLP2 [256]^3, x 3)
+// and of the surrogate, packed by dmip_capi.cpp (pack_dps_x3_prior / pack_dps_x3_surrogate)
+constexpr int kDpsX3Chunk = 32768;
+constexpr int kDpsX3PriorChunks = 35;  // P2 (8) | P3 (8) | Pout (1) | P4^T (1) | P3^T (8) | P2^T (8) | P1^T (1)
+constexpr int kDpsX3SurChunks = 35;    // S2 (8) | S3 (8) | Sout (1) | S4^T (1) | S3^T (8) | S2^T (8) | S1^T (1)
+struct DpsX3Params {
+  const char* pimg;     // the prior's chunks [35][32 KiB]
+  const char* simg;     // the surrogate's chunks [35][32 KiB]
+  const char* pl1;      // prior layer 1 over (x, t), split, scaled by 2 log2 e: [16 tiles][64][8] fp16
+  const char* sl1;      // surrogate layer 1 over x, split: [16][64][8] fp16
+  const float* pbias;   // prior: c b1 | folded init2 | folded init3 [256] | folded output init [16]
+  const float* sbias;   // surrogate: b1 | b2 | b3 [256] | b4 [32]
+  const float* y;       // [n_y][23]
+  long long n_chains, chain_offset;
+  int num_steps;
+  float T, bmin, bdiff, delta, sqrt_delta, mean, stdv, zeta;
+  int mode;             // 0: NLL guidance, 1: residual-norm step (DpsParams)
+  float a, b2;          // the noise model (NLL mode)
+  unsigned long long seed;
+  float* x_out;         // [n_y][n_chains][3]
+  unsigned int* err;    // device status word (kErrRange)
+  const float* coef;    // per-step (tau, beta, g, 0), (mean_weight, var, 0, 0): filled by launch_dps_x3
+};
+hipError_t launch_dps_x3(const DpsX3Params& p, int n_y, hipStream_t st);
+
 hipError_t launch_surrogate_eval(const SurrogateParams& p, int mode, int n_wg, hipStream_t st);
 int surrogate_rows_per_wg();
 hipError_t launch_mh(const SurrogateParams& p, int n_y, hipStream_t st);
@@ -415,6 +440,13 @@ struct TrainDrawsParams {
   // captured step graphs (dmip_train_plan): the step's draw stream is stream_id + *draw_ctr, read on
   // the device, so one graph replays every step (null: stream_id alone)
   const unsigned long long* draw_ctr;
+  // captured step graphs: the batch is copied from the caller's x / y into the graph's staging buffers by
+  // the draws launch itself (the step updates x_src / y_src in the graph's kernel node; null: no copy)
+  const float* x_src;
+  const float* y_src;
+  float* x_dst;
+  float* y_dst;
+  int ydim;
 };
 
 constexpr int kAdamMaxTensors = 16;
@@ -439,8 +471,24 @@ struct AdamParams {
 struct StepCounters {
   unsigned long long draw;  // draws' stream offset
   long long step;           // optimizer steps taken
+  unsigned int done;        // fused reduction + Adam: workgroups finished this step (the last advances the counters)
+  unsigned int pad;
 };
 hipError_t launch_counters_advance(StepCounters* c, hipStream_t st);
+
+// The captured bf16 training step's fused launches (dmip_train_plan; dmip_train.hip): the weight image's pack runs
+// in the draws launch (plan_prologue_kernel: pack workgroups + draw workgroups), and the gradient reduction applies
+// torch's Adam to each parameter it has just summed and, in its last workgroup, advances the step counters -- four
+// launches per step (prologue, forward half, reverse half, reduction) instead of seven plus two batch copies.
+struct TrainFuse {
+  TrainDrawsParams draws;
+  AdamParams adam;
+  StepCounters* ctr;
+};
+hipError_t launch_loss_grad_fused(const TrainParams& p, int n_hidden, float* grads, float* loss_out, float* partials,
+                                  int n_wg, const TrainFuse& f, hipStream_t st);
+const void* train_plan_prologue_func(int n_hidden);  // the kernel node a plan step updates (bf16)
+const void* train_draws_func();                      // the same for the exact-f32 plan
 
 hipError_t launch_train_draws(const TrainDrawsParams& p, hipStream_t st);
 hipError_t launch_adam(const AdamParams& p, hipStream_t st);

@@ -32,6 +32,7 @@
 
 #include "dmip_device.h"
 #include "dmip_internal.h"
+#include "dmip_stepdev.h"
 
 namespace dmip {
 namespace train {
@@ -67,17 +68,22 @@ static_assert(3 * IN + 2 <= 32, "layer-1 split operand fits one k-step");
 
 // PH: 0 = the fused kernel (forward jets, loss terms and reverse pass in one wave, one wave per SIMD);
 // 1 = the forward half (jets + per-sample loss terms and adjoints into p.adj; two waves per SIMD);
-// 2 = the reverse half (adjoints from p.adj, recompute + weight gradients; its layer loop unrolled, 357
-// registers, one wave per SIMD -- an 8-wave two-per-SIMD build spilled and measured slower, DESIGN.md
-// §4a). The reverse half accumulates the workgroup's gradient in
-// ONE LDS partial, its waves taking turns: at turn k wave w adds sub-block (w + k) % 4 of a layer's
-// gradient, a workgroup barrier between turns, so every address is summed in a fixed wave order
-// (deterministic) with no global atomics (~160 per tile in the fused kernel: its L2 atomic rate alone,
-// ~50 ns per 256-byte wave-instruction per CU, was ~130 us of the 0.3 ms)
+// 2 = the reverse half (adjoints from p.adj, recompute + weight gradients; its layer loop unrolled, one wave per
+// SIMD -- an 8-wave two-per-SIMD build spilled and measured slower). Round 5: each wave OWNS fixed
+// 32 x 32 blocks of the workgroup's weight gradient and keeps them in registers for the whole launch -- block
+// (T, U) = (w >> 1, w & 1) of every W x W layer, and the output layer's block U = w - 2 (waves 2-3) or layer 1's
+// block T = w (waves 0-1). At each layer the waves write their tile's transposed adjoints and activations (double-
+// buffered scratch), one workgroup barrier, then every wave contracts ITS blocks over the samples of all four waves'
+// tiles (wave order 0..3, stream order within: a fixed summation order, deterministic). Round 3's turns (one LDS
+// partial, four barrier-separated turns of read-add-write per layer: 16 barriers and 256 LDS read-modify-writes per
+// tile) become one barrier per layer and no adds; the biases and loss sums meet once, at the end, in wave order.
+// (~160 global atomics per tile in the fused kernel: its L2 atomic rate alone, ~50 ns per 256-byte wave-instruction
+// per CU, was ~130 us of the 0.3 ms)
 template <int NL, int PH = 0>
 struct TL {
   static constexpr int NW = PH == 0 ? NWV : 4;               // waves per workgroup
-  static constexpr bool TURN = PH == 2;                      // one LDS partial per workgroup, waves take turns
+  static constexpr bool OWN = PH == 2;                       // each wave owns fixed gradient blocks in registers
+  static constexpr int NBUF = OWN ? 2 : 1;                   // transposed scratch sets per wave (layer-parity buffered)
   static constexpr bool GG = PH == 0 ? GACC_GLOBAL : false;  // gradient partial rows in global memory
   static constexpr int RSV = PH == 2 ? 16 : RS;              // scratch row stride (reverse half: unpadded, to fit)
   static constexpr int p_w(int l) { return l == 0 ? 0 : W * IN + W + (l - 1) * (W * W + W); }
@@ -96,12 +102,14 @@ struct TL {
   static constexpr int COL = AOL + 2048;                 // fp32 [D][64]: layer-1 weight columns of x (forward)
   static constexpr int WAVE = COL + D * W * 4;
   static constexpr int IMG = PH == 2 ? AO : WAVE;        // image bytes this kernel copies (reverse: no forward-only parts)
-  static constexpr int GP_BYTES = TURN ? ((PART * 4 + 15) / 16) * 16 : 0;  // the workgroup's LDS partial (TURN)
   static constexpr int GACC = 0;                         // per wave: fp32 gradient partial (param order, LDS mode)
-  static constexpr int SCR = (GG || TURN) ? 0 : ((PART * 4 + 15) / 16) * 16;  // per wave: 6 transposed [64][16] bf16
-  static constexpr int WAVE_BYTES = PH == 1 ? 0 : SCR + 6 * W * RSV * 2;
-  static constexpr int TOTAL = IMG + GP_BYTES + NW * WAVE_BYTES;
+  static constexpr int SCR = (GG || OWN) ? 0 : ((PART * 4 + 15) / 16) * 16;  // per wave: 6 transposed [64][16] bf16
+  static constexpr int SET = 6 * W * RSV * 2;            // one transposed scratch set (bytes)
+  static constexpr int WAVE_BYTES = PH == 1 ? 0 : SCR + NBUF * SET;
+  static constexpr int TOTAL = IMG + NW * WAVE_BYTES;
   static_assert(TOTAL <= 160 * 1024, "LDS budget");
+  // OWN: the flush's bias / loss partial reuses the scratch (after the last tile)
+  static_assert(!OWN || PART * 4 <= NW * WAVE_BYTES, "flush partial fits the scratch");
 };
 
 __device__ __forceinline__ int kp(int s, int g, int j) { return 32 * s + 16 * (j >> 2) + 4 * g + (j & 3); }
@@ -281,14 +289,13 @@ __global__ void __launch_bounds__(256) train_pack_kernel(TrainParams p) {
 // wait for a load of its own row before every update: those read-modify-write round trips sat on the
 // tile's dependency chain); the row is the wave's own, and its updates to one address are issued in
 // program order, so the sums keep a fixed order. In LDS a plain add.
-// TURN: one wave's add into the workgroup's LDS partial: a plain read-modify-write (within a turn every
-// address has one writer). ds_add_f32 measured 2x slower for the whole reverse half (144 -> 294 us).
-__device__ __forceinline__ void lds_add(float* a, float v) { *a += v; }
-
-// TURN: a workgroup barrier after this wave's LDS adds have completed (the next turn's adds may touch them)
+// OWN: a workgroup barrier after this wave's LDS operations have completed (the reverse half's layer barrier, and
+// the flush's wave-ordered turns)
 __device__ __forceinline__ void turn_barrier() {
   __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+#ifndef DMIP_TRAIN_TIMING_NO_TURN_BARRIER  // timing ablation only (scripts/gpu_c5_ablate.sh): wrong gradients
   __builtin_amdgcn_s_barrier();
+#endif
 }
 
 template <bool GG>
@@ -317,10 +324,7 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
     uint4* dst = (uint4*)lds;
 #pragma unroll 4
     for (int e = tid; e < L::IMG / 16; e += NWV * 64) dst[e] = src[e];
-    if constexpr (PH == 1) {
-    } else if constexpr (L::TURN) {
-      float* gp = (float*)(lds + L::IMG);
-      for (int e = tid; e < L::PART; e += NWV * 64) gp[e] = 0.0f;
+    if constexpr (PH == 1 || L::OWN) {
     } else if constexpr (!GACC_GLOBAL) {
       float* gacc = (float*)(lds + L::WAVE + w * L::WAVE_BYTES + L::GACC);
       for (int e = lane; e < L::PART; e += 64) gacc[e] = 0.0f;
@@ -339,11 +343,23 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
   const char* aotr = lds + L::AOT;
   const float* bias = (const float*)(lds + L::BIAS);
   const float* col = (const float*)(lds + L::COL);
-  char* wave_base = lds + L::IMG + L::GP_BYTES + w * L::WAVE_BYTES;
-  float* gacc = L::TURN ? (float*)(lds + L::IMG)
-                        : (GACC_GLOBAL ? p.partials + ((size_t)blockIdx.x * NWV + w) * L::PART : (float*)(wave_base + L::GACC));
+  char* wave_base = lds + L::IMG + w * L::WAVE_BYTES;
+  // OWN: the flush's bias / loss partial (in the scratch, after the last tile)
+  float* gacc = L::OWN ? (float*)(lds + L::IMG)
+                       : (GACC_GLOBAL ? p.partials + ((size_t)blockIdx.x * NWV + w) * L::PART : (float*)(wave_base + L::GACC));
   __bf16* scr = (__bf16*)(wave_base + L::SCR);
-  auto S_ = [&](int k) { return scr + k * W * RS; };
+  int sbuf = 0;  // OWN: this layer's scratch set (alternates with every layer processed)
+  auto S_ = [&](int k) { return scr + (sbuf * 6 + k) * W * RS; };
+  // OWN: scratch k of wave v's current set
+  auto SV = [&](int v, int k) {
+    return (const __bf16*)(lds + L::IMG + v * L::WAVE_BYTES + L::SCR) + (sbuf * 6 + k) * W * RS;
+  };
+  // OWN: this wave's gradient blocks, accumulated over every tile of the workgroup
+  f32x16 gW[NL > 1 ? NL - 1 : 1];  // block (w >> 1, w & 1) of W x W layer l at gW[l - 1]
+  f32x16 gX;                       // waves 0-1: layer 1's block T = w; waves 2-3: the output layer's block U = w - 2
+#pragma unroll
+  for (int l = 0; l < (NL > 1 ? NL - 1 : 1); ++l) gW[l] = f32x16{};
+  gX = f32x16{};
 
   f32x4 bbar[NL > 1 ? NL - 1 : 1][4];  // per-lane bias-gradient partials of the hidden W x W layers
 #pragma unroll
@@ -354,11 +370,11 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
   float lsum[3] = {0.0f, 0.0f, 0.0f};  // DSM, IC, PDE row sums (lane group 0 only)
 
   const long long n_tiles = (p.n + NS - 1) / NS;
-  // TURN: every wave of the workgroup runs the same rounds (a wave past the end runs an all-invalid tile),
-  // so the turn barriers match
-  for (long long tile0 = (long long)blockIdx.x * NWV + (L::TURN ? 0 : w); tile0 < n_tiles;
+  // OWN: every wave of the workgroup runs the same rounds (a wave past the end runs an all-invalid tile),
+  // so the layer barriers match
+  for (long long tile0 = (long long)blockIdx.x * NWV + (L::OWN ? 0 : w); tile0 < n_tiles;
        tile0 += (long long)gridDim.x * NWV) {
-    const long long tile = tile0 + (L::TURN ? w : 0);
+    const long long tile = tile0 + (L::OWN ? w : 0);
     const long long si = tile * NS + c16;
     const bool valid = si < p.n;
     // ---------------------------------------------------------------- per-sample inputs
@@ -599,6 +615,7 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
     constexpr int kLiUnroll = PH == 2 ? NL + 1 : 1;
 #pragma unroll kLiUnroll
     for (int li = NL; li >= 0; --li) {
+      if constexpr (L::OWN) sbuf ^= 1;
       // ---- recompute P, V, C forward: h_{li-1} (B form + transposed into scratch 3..5) and z_li
       bf16x8 H[3][2], HL[3][2];
       f32x4 Z[3][4];
@@ -667,36 +684,34 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
 #pragma unroll
           for (int o = 0; o < OUT; ++o) bobar[o] += abP[o] + abC[o];
         }
-        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's scratch writes landed
-        __builtin_amdgcn_wave_barrier();
-        float go[2][OUT];  // TURN: this tile's output-layer gradient, added in turns
+        if constexpr (L::OWN) {
+          turn_barrier();  // every wave's scratch of this layer has landed
+          if (w >= 2) {    // the output layer's block U = w - 2, over the four waves' tiles
+            const int U = w - 2;
 #pragma unroll
-        for (int U = 0; U < 2; ++U) {
-          f32x16 acc{};
+            for (int v = 0; v < 4; ++v)
 #pragma unroll
-          for (int S = 0; S < 3; ++S) {
-            const bf16x8 A = tread<RS>(S_(S), i32, i32 < OUT, hh);
-            const bf16x8 Bm = tread<RS>(S_(3 + S), 32 * U + i32, true, hh);
-            acc = mfma32(A, Bm, acc);
+              for (int S = 0; S < 3; ++S) {
+                const bf16x8 A = tread<RS>(SV(v, S), i32, i32 < OUT, hh);
+                const bf16x8 Bm = tread<RS>(SV(v, 3 + S), 32 * U + i32, true, hh);
+                gX = mfma32(A, Bm, gX);
+              }
           }
-          if constexpr (L::TURN) {
+        } else {
+          __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's scratch writes landed
+          __builtin_amdgcn_wave_barrier();
 #pragma unroll
-            for (int o = 0; o < OUT; ++o) go[U][o] = acc[o];
-          } else if (hh == 0) {
+          for (int U = 0; U < 2; ++U) {
+            f32x16 acc{};
 #pragma unroll
-            for (int o = 0; o < OUT; ++o) gadd<GACC_GLOBAL>(&gacc[L::p_w(NL) + o * W + 32 * U + i32], acc[o]);
-          }
-        }
-        if constexpr (L::TURN) {  // sub-block (U, o) = ((w + k) % 4) / 2, ((w + k) % 4) % 2 at turn k
-          static_assert(OUT == 2, "four (U, o) sub-blocks, one per wave and turn");
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const int sb = (w + k) & 3;
-            turn_barrier();
+            for (int S = 0; S < 3; ++S) {
+              const bf16x8 A = tread<RS>(S_(S), i32, i32 < OUT, hh);
+              const bf16x8 Bm = tread<RS>(S_(3 + S), 32 * U + i32, true, hh);
+              acc = mfma32(A, Bm, acc);
+            }
             if (hh == 0) {
 #pragma unroll
-              for (int q = 0; q < 4; ++q)
-                if (sb == q) lds_add(&gacc[L::p_w(NL) + (q & 1) * W + 32 * (q >> 1) + i32], go[q >> 1][q & 1]);
+              for (int o = 0; o < OUT; ++o) gadd<GACC_GLOBAL>(&gacc[L::p_w(NL) + o * W + 32 * U + i32], acc[o]);
             }
           }
         }
@@ -754,22 +769,45 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
 #pragma unroll
         for (int R = 0; R < 4; ++R) bbar[(li - 1) > 0 ? li - 1 : 0][R] += zb[0][R] + zb[2][R];
       }
-      __builtin_amdgcn_s_waitcnt(0xc07f);
-      __builtin_amdgcn_wave_barrier();
-      if (li == 0) {
-        f32x16 a0[2];
+      if constexpr (L::OWN) {
+        turn_barrier();  // every wave's scratch of this layer has landed
+        if (li == 0) {
+          if (w < 2) {  // layer 1's block T = w (weight columns i32 < IN, the bias at i32 == IN)
 #pragma unroll
-        for (int T = 0; T < 2; ++T) {
-          f32x16 acc{};
+            for (int v = 0; v < 4; ++v)
 #pragma unroll
-          for (int S = 0; S < 3; ++S) {
-            const bf16x8 A = tread<RS>(S_(S), 32 * T + i32, true, hh);
-            const bf16x8 Bm = tread<RS>(S_(3 + S), i32, i32 <= IN, hh);
-            acc = mfma32(A, Bm, acc);
+              for (int S = 0; S < 3; ++S) {
+                const bf16x8 A = tread<RS>(SV(v, S), 32 * w + i32, true, hh);
+                const bf16x8 Bm = tread<RS>(SV(v, 3 + S), i32, i32 <= IN, hh);
+                gX = mfma32(A, Bm, gX);
+              }
           }
-          if constexpr (L::TURN) {
-            a0[T] = acc;
-          } else {
+        } else {  // W x W layer li: block (T, U) = (w >> 1, w & 1)
+          const int T = w >> 1, U = w & 1;
+#pragma unroll
+          for (int v = 0; v < 4; ++v)
+#pragma unroll
+            for (int S = 0; S < 3; ++S) {
+              const bf16x8 A = tread<RS>(SV(v, S), 32 * T + i32, true, hh);
+              const bf16x8 Bm = tread<RS>(SV(v, 3 + S), 32 * U + i32, true, hh);
+              gW[(li - 1) > 0 ? li - 1 : 0] = mfma32(A, Bm, gW[(li - 1) > 0 ? li - 1 : 0]);
+            }
+        }
+      } else {
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+      }
+      if (li == 0) {
+        if constexpr (!L::OWN) {
+#pragma unroll
+          for (int T = 0; T < 2; ++T) {
+            f32x16 acc{};
+#pragma unroll
+            for (int S = 0; S < 3; ++S) {
+              const bf16x8 A = tread<RS>(S_(S), 32 * T + i32, true, hh);
+              const bf16x8 Bm = tread<RS>(S_(3 + S), i32, i32 <= IN, hh);
+              acc = mfma32(A, Bm, acc);
+            }
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
               const int row = 32 * T + (r & 3) + 8 * (r >> 2) + 4 * hh;
@@ -778,44 +816,10 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
             }
           }
         }
-        if constexpr (L::TURN) {  // sub-block (T, half) = ((w + k) % 4) / 2, % 2: accumulator registers 8 half .. + 7
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const int sb = (w + k) & 3;
-            turn_barrier();
-            // weight column i32 < IN (stride IN) or the bias (i32 == IN, stride 1): one lane-divergent region
-            const int b0 = i32 < IN ? L::p_w(0) + i32 : L::p_b(0), s0 = i32 < IN ? IN : 1;
-            if (i32 <= IN) {
-#pragma unroll
-              for (int q = 0; q < 4; ++q) {
-                if (sb != q) continue;
-#pragma unroll
-                for (int r = 8 * (q & 1); r < 8 * (q & 1) + 8; ++r)
-                  lds_add(&gacc[b0 + (32 * (q >> 1) + (r & 3) + 8 * (r >> 2) + 4 * hh) * s0], a0[q >> 1][r]);
-              }
-            }
-          }
-        }
       } else {
         const int pw = L::p_w(li);
-        if constexpr (L::TURN) {  // block (T, U) = ((w + k) % 4) / 2, % 2 at turn k: its MFMAs, then its adds
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const int sb = (w + k) & 3, T = sb >> 1, U = sb & 1;
-            f32x16 acc{};
-#pragma unroll
-            for (int S = 0; S < 3; ++S) {
-              const bf16x8 A = tread<RS>(S_(S), 32 * T + i32, true, hh);
-              const bf16x8 Bm = tread<RS>(S_(3 + S), 32 * U + i32, true, hh);
-              acc = mfma32(A, Bm, acc);
-            }
-            turn_barrier();
-#pragma unroll
-            for (int r = 0; r < 16; ++r) lds_add(&gacc[pw + (32 * T + (r & 3) + 8 * (r >> 2) + 4 * hh) * W + 32 * U + i32], acc[r]);
-          }
-        }
-#pragma unroll
-        for (int T = 0; T < 2 && !L::TURN; ++T)
+        for (int T = 0; T < 2 && !L::OWN; ++T)
 #pragma unroll
           for (int U = 0; U < 2; ++U) {
             f32x16 acc{};
@@ -850,10 +854,35 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
   }
 
   if constexpr (PH == 1) return;  // the forward half: its adjoints and loss terms are in p.adj
-  // ---- flush: bias partials (reduce the 16 sample lanes of each lane group) and loss sums; TURN: one wave
-  // at a time into the workgroup's LDS partial (wave order), then the partial to its row in global memory
-  for (int turn = 0; turn < (L::TURN ? NWV : 1); ++turn) {
-    if constexpr (L::TURN) {
+  // ---- flush: bias partials (reduce the 16 sample lanes of each lane group) and loss sums; OWN: the weight
+  // blocks straight from registers to the workgroup's row, the bias / loss partials one wave at a time (wave order)
+  // into an LDS partial in the (now free) scratch, then that partial to the row
+  if constexpr (L::OWN) {
+    float* row = p.partials + (size_t)blockIdx.x * L::PART;
+    {
+      const int T = w >> 1, U = w & 1;
+#pragma unroll
+      for (int l = 1; l < NL; ++l)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          row[L::p_w(l) + (32 * T + (r & 3) + 8 * (r >> 2) + 4 * hh) * W + 32 * U + i32] = gW[l - 1][r];
+    }
+    if (w < 2) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int rr = 32 * w + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        if (i32 < IN) row[L::p_w(0) + rr * IN + i32] = gX[r];
+        else if (i32 == IN) row[L::p_b(0) + rr] = gX[r];
+      }
+    } else if (hh == 0) {  // output rows o < OUT sit in registers o of lane half 0
+#pragma unroll
+      for (int o = 0; o < OUT; ++o) row[L::p_w(NL) + o * W + 32 * (w - 2) + i32] = gX[o];
+    }
+    turn_barrier();  // the last tile's scratch reads are done: the bias / loss partial may take the scratch
+    for (int e = tid; e < L::PART; e += NWV * 64) gacc[e] = 0.0f;
+  }
+  for (int turn = 0; turn < (L::OWN ? NWV : 1); ++turn) {
+    if constexpr (L::OWN) {
       turn_barrier();
       if (w != turn) continue;
     }
@@ -881,15 +910,21 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
 #pragma unroll
     for (int m = 1; m < 64; m <<= 1) v += __shfl_xor(v, m, 64);
     if (lane == 0) {
-      if constexpr (L::TURN) gacc[L::NPARAM + k] += v;
+      if constexpr (L::OWN) gacc[L::NPARAM + k] += v;
       else gacc[L::NPARAM + k] = v;
     }
   }
   }  // turns
-  if constexpr (L::TURN) {
+  if constexpr (L::OWN) {
     turn_barrier();
     float* row = p.partials + (size_t)blockIdx.x * L::PART;
-    for (int e = tid; e < L::PART; e += NWV * 64) row[e] = gacc[e];
+    // the hidden and output biases and the loss sums (the weight blocks and layer 1's bias are in the row already)
+    for (int e = tid; e < L::PART; e += NWV * 64) {
+      bool mine = e >= L::NPARAM || (e >= L::p_b(NL) && e < L::p_b(NL) + OUT);
+#pragma unroll
+      for (int l = 1; l < NL; ++l) mine |= e >= L::p_b(l) && e < L::p_b(l) + W;
+      if (mine) row[e] = gacc[e];
+    }
     return;
   }
   if constexpr (GACC_GLOBAL) {
@@ -922,27 +957,40 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
 
 // grads[k] = sum over the per-workgroup partials in a fixed order (deterministic); slots nparam..+2
 // are the DSM / IC / PDE row sums -> loss_out = {loss, PDE, IC, DSM} means. 64 slots per block, the
-// partials split over 4 thread groups, combined in LDS in group order.
+// partials split over kRedGroups thread groups (rows g, g + 16, ...), combined in LDS in group order (f64).
 // total_flags (bit 0 DSM, 1 IC, 2 PDE, bit 3 = set): the block holding the three loss slots also writes
-// loss_out[0] (their sum, as loss_total_kernel), saving that launch
-__global__ void __launch_bounds__(256) loss_grad_reduce_kernel(const float* partials, int n_parts, int stride,
-                                                               int nparam, float* grads, float* loss_out, float inv_n,
-                                                               int total_flags) {
-  __shared__ double red[4][64];
+// loss_out[0] (their sum, as loss_total_kernel), saving that launch.
+// ADAM (the captured bf16 step's last launch, TrainFuse): then torch's Adam on each parameter its thread has just
+// summed (the same float the separate adam_kernel would read back from .grad), and in the last workgroup to finish
+// (a counter of finished workgroups) the step counters' advance. Every workgroup reads the step counter before it
+// counts itself finished, so the advance follows all of this step's reads.
+constexpr int kRedGroups = 16;  // 1024 threads: 16 rows in flight per slot (4 groups left the reduction latency-bound)
+template <bool ADAM>
+__global__ void __launch_bounds__(64 * kRedGroups) loss_grad_reduce_kernel(const float* partials, int n_parts,
+                                                                          int stride, int nparam, float* grads,
+                                                                          float* loss_out, float inv_n, int total_flags,
+                                                                          AdamParams ap, StepCounters* ctr) {
+  __shared__ double red[kRedGroups][64];
   __shared__ float lm[3];
+  __shared__ stepdev::AdamScalars sc;  // ADAM: the step's scalars once per workgroup (double pow)
   const int pi = threadIdx.x & 63, pg = threadIdx.x >> 6;
   const int k = blockIdx.x * 64 + pi;
+  if (ADAM && threadIdx.x == 64) sc = stepdev::adam_scalars(ap);
   double s = 0.0;
   if (k < nparam + 3) {
-#pragma unroll 8
-    for (int i = pg; i < n_parts; i += 4) s += (double)partials[(size_t)i * stride + k];
+#pragma unroll 4
+    for (int i = pg; i < n_parts; i += kRedGroups) s += (double)partials[(size_t)i * stride + k];
   }
   red[pg][pi] = s;
   __syncthreads();
   if (pg == 0 && k < nparam + 3) {
-    s = red[0][pi] + red[1][pi] + red[2][pi] + red[3][pi];
+    s = red[0][pi];
+#pragma unroll
+    for (int q = 1; q < kRedGroups; ++q) s += red[q][pi];
     if (k < nparam) {
-      grads[k] = (float)s;
+      const float gk = (float)s;
+      grads[k] = gk;
+      if constexpr (ADAM) stepdev::adam_one(ap, sc, k, gk);
     } else {
       const float mean = (float)(s * inv_n);
       const int c = k - nparam;  // 0 DSM, 1 IC, 2 PDE
@@ -950,17 +998,43 @@ __global__ void __launch_bounds__(256) loss_grad_reduce_kernel(const float* part
       lm[c] = mean;
     }
   }
-  if (!(total_flags & 8) || blockIdx.x != (unsigned)(nparam / 64)) return;
-  __syncthreads();
-  if (threadIdx.x == 0)
-    loss_out[0] = ((total_flags & 1) ? lm[0] : 0.0f) + ((total_flags & 2) ? lm[1] : 0.0f) + ((total_flags & 4) ? lm[2] : 0.0f);
+  if ((total_flags & 8) && blockIdx.x == (unsigned)(nparam / 64)) {
+    __syncthreads();
+    if (threadIdx.x == 0)
+      loss_out[0] = ((total_flags & 1) ? lm[0] : 0.0f) + ((total_flags & 2) ? lm[1] : 0.0f) + ((total_flags & 4) ? lm[2] : 0.0f);
+  }
+  if constexpr (ADAM) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __threadfence();
+      if (atomicAdd(&ctr->done, 1u) == gridDim.x - 1) {  // the last workgroup: every read of the counters is done
+        ctr->done = 0u;
+        ctr->draw += 1;
+        ctr->step += 1;
+      }
+    }
+  }
 }
 
 __global__ void loss_total_kernel(float* loss_out, int has_dsm, int has_ic, int has_pde) {
   loss_out[0] = (has_dsm ? loss_out[3] : 0.0f) + (has_ic ? loss_out[2] : 0.0f) + (has_pde ? loss_out[1] : 0.0f);
 }
 
+// The captured bf16 step's first launch (TrainFuse): workgroups [0, n_pack) pack the weight image
+// (train_pack_kernel's work), the rest draw t and eps (and stage the batch) as train_draws_kernel
+template <int NL>
+__global__ void __launch_bounds__(256) plan_prologue_kernel(TrainDrawsParams dp, TrainParams tp, int n_pack) {
+  if ((int)blockIdx.x < n_pack) {
+    pack_weights<NL>(tp, tp.packed, blockIdx.x * blockDim.x + threadIdx.x, n_pack * blockDim.x);
+    return;
+  }
+  stepdev::draw_one(dp, (long long)(blockIdx.x - n_pack) * blockDim.x + threadIdx.x);
+}
+
+
 }  // namespace train
+
+constexpr int kPackBlocks = 32;  // train_pack_kernel's grid (and the pack part of plan_prologue_kernel's)
 
 // the forward / reverse split (two kernels at two waves per SIMD) or the fused one-wave-per-SIMD kernel;
 // DMIP_TRAIN_SPLIT=0 selects the fused kernel (A/B knob, read once per process)
@@ -984,9 +1058,9 @@ hipError_t launch_loss_grad(const TrainParams& p, int n_hidden, float* grads, fl
   TrainParams q = p;
   q.partials = partials;
   if (n_hidden == 3)
-    hipLaunchKernelGGL(train_pack_kernel<3>, dim3(32), dim3(256), 0, st, q);
+    hipLaunchKernelGGL(train_pack_kernel<3>, dim3(kPackBlocks), dim3(256), 0, st, q);
   else
-    hipLaunchKernelGGL(train_pack_kernel<2>, dim3(32), dim3(256), 0, st, q);
+    hipLaunchKernelGGL(train_pack_kernel<2>, dim3(kPackBlocks), dim3(256), 0, st, q);
   hipError_t e0 = hipGetLastError();
   if (e0 != hipSuccess) return e0;
   if (train_split()) {
@@ -1011,11 +1085,52 @@ hipError_t launch_loss_grad(const TrainParams& p, int n_hidden, float* grads, fl
   // the loss total rides on the reduction when the three loss slots share one 64-slot block
   const bool fused_total = nparam / 64 == (nparam + 2) / 64;
   const int flags = fused_total ? 8 | (p.has_dsm ? 1 : 0) | (p.has_ic ? 2 : 0) | (p.pde != 0 ? 4 : 0) : 0;
-  hipLaunchKernelGGL(loss_grad_reduce_kernel, dim3((nparam + 3 + 63) / 64), dim3(256), 0, st, partials, n_wg,
-                     part * train_partials_per_wg(),
-                     nparam, grads, loss_out, p.inv_n, flags);
+  hipLaunchKernelGGL(loss_grad_reduce_kernel<false>, dim3((nparam + 3 + 63) / 64), dim3(64 * kRedGroups), 0, st,
+                     partials, n_wg, part * train_partials_per_wg(), nparam, grads, loss_out, p.inv_n, flags,
+                     AdamParams{}, (StepCounters*)nullptr);
   e = hipGetLastError();
   if (e != hipSuccess || fused_total) return e;
+  hipLaunchKernelGGL(loss_total_kernel, dim3(1), dim3(1), 0, st, loss_out, p.has_dsm, p.has_ic, p.pde != 0);
+  return hipGetLastError();
+}
+
+const void* train_plan_prologue_func(int n_hidden) {
+  return n_hidden == 3 ? (const void*)train::plan_prologue_kernel<3> : (const void*)train::plan_prologue_kernel<2>;
+}
+
+hipError_t launch_loss_grad_fused(const TrainParams& p, int n_hidden, float* grads, float* loss_out, float* partials,
+                                  int n_wg, const TrainFuse& f, hipStream_t st) {
+  using namespace train;
+  if (!train_split() || !p.adj || (n_hidden != 2 && n_hidden != 3)) return hipErrorInvalidValue;
+  const int part = n_hidden == 3 ? TL<3>::PART : TL<2>::PART;
+  const int nparam = train_nparam(n_hidden);
+  if (f.adam.off[f.adam.n] != nparam) return hipErrorInvalidValue;  // Adam's flat order is the gradient's
+  TrainParams q = p;
+  q.partials = partials;
+  const unsigned draw_blocks = (unsigned)((f.draws.batch + 255) / 256);
+  const dim3 pg(kPackBlocks + draw_blocks), pb(256);
+  if (n_hidden == 3)
+    hipLaunchKernelGGL(plan_prologue_kernel<3>, pg, pb, 0, st, f.draws, q, kPackBlocks);
+  else
+    hipLaunchKernelGGL(plan_prologue_kernel<2>, pg, pb, 0, st, f.draws, q, kPackBlocks);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const long long tiles = (p.n + NS - 1) / NS;
+  const long long g1 = std::min<long long>(2LL * n_wg, (tiles + 3) / 4);
+  if (n_hidden == 3) {
+    hipLaunchKernelGGL((loss_grad_kernel<3, 1>), dim3((unsigned)g1), dim3(TL<3, 1>::NW * 64), 0, st, q);
+    hipLaunchKernelGGL((loss_grad_kernel<3, 2>), dim3(n_wg), dim3(TL<3, 2>::NW * 64), 0, st, q);
+  } else {
+    hipLaunchKernelGGL((loss_grad_kernel<2, 1>), dim3((unsigned)g1), dim3(TL<2, 1>::NW * 64), 0, st, q);
+    hipLaunchKernelGGL((loss_grad_kernel<2, 2>), dim3(n_wg), dim3(TL<2, 2>::NW * 64), 0, st, q);
+  }
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  const bool fused_total = nparam / 64 == (nparam + 2) / 64;
+  const int flags = fused_total ? 8 | (p.has_dsm ? 1 : 0) | (p.has_ic ? 2 : 0) | (p.pde != 0 ? 4 : 0) : 0;
+  hipLaunchKernelGGL(loss_grad_reduce_kernel<true>, dim3((nparam + 3 + 63) / 64), dim3(64 * kRedGroups), 0, st,
+                     partials, n_wg, part * train_partials_per_wg(), nparam, grads, loss_out, p.inv_n, flags, f.adam,
+                     f.ctr);
+  if ((e = hipGetLastError()) != hipSuccess || fused_total) return e;
   hipLaunchKernelGGL(loss_total_kernel, dim3(1), dim3(1), 0, st, loss_out, p.has_dsm, p.has_ic, p.pde != 0);
   return hipGetLastError();
 }

@@ -464,7 +464,8 @@ class DPS(BaseClassDiffusionModel):
     measurement likelihood through the surrogate forward model at the Tweedie estimate
     x0_hat = (x + var s) / mean_weight -- the quantity PosteriorLoss.likelihood_target (losses.py:349-371)
     trains the reference's likelihood network towards, here computed exactly on the fly.
-    Fused kernel: dmip_dps_sample (include/dmip.h), one launch for all steps, exact f32.
+    Fused kernel: dmip_dps_sample_ex (include/dmip.h), one launch for all steps: fp32x3 by default (the split-fp16
+    engine, J^T by a reverse pass through the prior), exact f32 with precision="fp32".
 
     forward_model: the surrogate nn.Sequential (load_forward_model); params: {'a', 'b', 'lambd_bd'};
     guidance: 'norm' (default; Chung et al.'s zeta / ||y - F(x0_hat)|| step on ||y - F(x0_hat)||^2) or 'nll'
@@ -499,7 +500,10 @@ class DPS(BaseClassDiffusionModel):
 
     def sample_device(self, y, num_samples, num_steps=200, mean=0, std=1, seed=None, chain_offset=0, noise=None,
                       precision=None):
-        """Exact f32 always (dmip_dps_sample); `precision` is accepted for API symmetry."""
+        """dmip_dps_sample_ex at `precision` (default self.precision): "fp32x3" (the reference's fp32 accuracy at
+        the fp16 matrix rate, dmip_dps_x3.hip; also what "fp16" runs: there is no 16-bit DPS) or "fp32" (exact f32,
+        forward tangents). At the default precision a chain outside fp16's range resamples in exact f32
+        (parallel.sample_checked)."""
         if noise is not None:
             raise ValueError("noise injection is only implemented for the fused CDE sampler")
         from .problems import surrogate_handle
@@ -513,9 +517,11 @@ class DPS(BaseClassDiffusionModel):
         seed = _draw_seed() if seed is None else seed
         prior = pn.dmip_handle(dev, self.xdim)
         p = self.params
+        prec = canonical_precision(precision or self.precision)
         _lib.dps_sample(prior, sur, _lib.scat_noise(p['a'], p['b'], p['lambd_bd']), sde, ys, num_samples,
                         chain_offset, num_steps, mean, std, seed,
-                        _lib.DMIP_DPS_NLL if self.guidance == 'nll' else _lib.DMIP_DPS_NORM, self.zeta, out)
+                        _lib.DMIP_DPS_NLL if self.guidance == 'nll' else _lib.DMIP_DPS_NORM, self.zeta, out,
+                        precision="fp32" if prec == "fp32" else "fp32x3")
         return out
 
     def train_epoch(self, optimizer, loss_fn, epoch_data_loader):

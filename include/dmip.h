@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define DMIP_ABI_VERSION 6
+#define DMIP_ABI_VERSION 7
 
 typedef enum {
   DMIP_OK = 0,
@@ -354,6 +354,17 @@ int dmip_dps_sample(const dmip_mlp* prior, const dmip_surrogate* fwd, const dmip
                     const dmip_vpsde* sde, const float* y_dev, int n_y, int64_t n_chains, int64_t chain_offset,
                     int num_steps, float mean, float stdv, uint64_t seed, int mode, float zeta, float* x_out_dev,
                     void* stream);
+
+/* dmip_dps_sample with a precision (ABI 7): DMIP_PREC_F32 = dmip_dps_sample (exact f32 MFMA, J by three forward
+ * tangents); DMIP_PREC_F32X3 = the same method at the reference's fp32 accuracy on the fp16 matrix rate (every
+ * product as the three-term fp16 split of the fp32x3 samplers; J^T by one reverse pass through the prior). fp32x3
+ * range: a weight beyond fp16's range is refused (DMIP_ERR_UNSUPPORTED, "fp16 range"); a chain whose input,
+ * surrogate activation or reverse-pass value leaves it is reported by dmip_device_status ("fp16 range"), and the
+ * Python estimators then resample with DMIP_PREC_F32. Same RNG stream per chain as dmip_dps_sample. */
+int dmip_dps_sample_ex(const dmip_mlp* prior, const dmip_surrogate* fwd, const dmip_scat_noise* noise,
+                       const dmip_vpsde* sde, const float* y_dev, int n_y, int64_t n_chains, int64_t chain_offset,
+                       int num_steps, float mean, float stdv, uint64_t seed, int mode, float zeta, int precision,
+                       float* x_out_dev, void* stream);
 
 /* ---- PosteriorLoss training step ------------------------------------------ */
 /* Loss value, components and the parameter gradients of PosteriorLoss(forward_model, a, b, lam)(sde, x,

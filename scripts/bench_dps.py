@@ -8,7 +8,7 @@ Weights: the fixture-trained prior (tests/golden/ckpt_prior_scat.npz, DSM on inv
 samples) or random init. Algorithmic flops per chain-step: prior forward + input VJP (2 F_prior,
 F_prior = 2 (4*256 + 2*256^2 + 256*3)) + surrogate forward + VJP (2 F_sur, F_sur = 275,456); the kernel
 executes 4 F_prior for the prior (primal + 3 forward tangents).
-    python scripts/bench_dps.py [--samples 262144] [--steps 1000] [--zeta 0.005] [--guidance norm]
+    python scripts/bench_dps.py [--samples 262144] [--steps 1000] [--zeta 0.005] [--guidance norm] [--precision fp32x3]
     torchrun --nproc-per-node 4 scripts/bench_dps.py"""
 import argparse
 import importlib
@@ -26,6 +26,7 @@ sys.path.insert(0, ROOT)
 F_PRIOR = 2 * (4 * 256 + 2 * 256 * 256 + 256 * 3)
 F_SUR = 2 * (3 * 256 + 2 * 256 * 256 + 256 * 23)
 PEAK_F32_MFMA = 157.3
+PEAK_F16_MFMA = 2500.0
 
 
 def main():
@@ -37,6 +38,7 @@ def main():
     ap.add_argument("--y-index", type=int, default=0)
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--gt-chains", type=int, default=30000)
+    ap.add_argument("--precision", default="fp32x3", choices=["fp32x3", "fp32"])
     ap.add_argument("--compare-cde", action="store_true", help="also score the fixture-trained CDE on the same y")
     a = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -64,7 +66,8 @@ def main():
     y = torch.from_numpy(np.load(os.path.join(gold, "data_scat.npz"))["y_test"][a.y_index]).to(dev)
 
     lo, hi = par.shard_range(a.samples, rank, world)
-    run = lambda s: par.gather_shards(m.sample_device(y, hi - lo, a.steps, seed=s, chain_offset=lo), a.samples, dev)
+    run = lambda s: par.gather_shards(m.sample_device(y, hi - lo, a.steps, seed=s, chain_offset=lo,
+                                                     precision=a.precision), a.samples, dev)
     x = run(1)
     torch.cuda.synchronize()
     st = torch.cuda.current_stream(dev)
@@ -86,16 +89,20 @@ def main():
         el = float(t.item())
     launch_ms = e0.elapsed_time(e1) / a.reps
     alg = (2 * F_PRIOR + 2 * F_SUR) * a.steps * (hi - lo)
-    exe = (4 * F_PRIOR + 2 * F_SUR) * a.steps * (hi - lo)
+    # fp32 engine: primal + 3 forward tangents through the prior; fp32x3: every product as three fp16 MFMAs
+    exe_cs = 4 * F_PRIOR + 2 * F_SUR if a.precision == "fp32" else 3 * (2 * F_PRIOR + 2 * F_SUR)
+    exe = exe_cs * a.steps * (hi - lo)
+    peak = PEAK_F32_MFMA if a.precision == "fp32" else PEAK_F16_MFMA
     out = {"metric": "DPS posterior samples/s (1000-step reverse SDE + surrogate guidance)",
            "value": a.samples * a.reps / el, "unit": "samples/s", "n_gpus": world, "samples": a.samples,
-           "sde_steps": a.steps, "zeta": a.zeta, "guidance": a.guidance, "weights": weights,
+           "sde_steps": a.steps, "zeta": a.zeta, "guidance": a.guidance, "weights": weights, "precision": a.precision,
            "ms_per_call": el / a.reps * 1e3, "rank0_launch_ms": launch_ms,
-           "roofline": {"bound": "mfma", "achieved": alg / (launch_ms * 1e-3) / 1e12, "peak": PEAK_F32_MFMA,
-                        "unit": "TFLOP/s", "frac": alg / (launch_ms * 1e-3) / 1e12 / PEAK_F32_MFMA,
+           "roofline": {"bound": "mfma", "achieved": alg / (launch_ms * 1e-3) / 1e12, "peak": peak,
+                        "unit": "TFLOP/s", "frac": alg / (launch_ms * 1e-3) / 1e12 / peak,
                         "executed_tflops": exe / (launch_ms * 1e-3) / 1e12,
+                        "executed_frac": exe / (launch_ms * 1e-3) / 1e12 / peak,
                         "flops_per_chain_step_alg": 2 * F_PRIOR + 2 * F_SUR,
-                        "flops_per_chain_step_executed": 4 * F_PRIOR + 2 * F_SUR}}
+                        "flops_per_chain_step_executed": exe_cs}}
     if rank == 0:
         gt = pkg.mh_sample(fm, prm, y[None], a.gt_chains, 1000, 0.5, seed=99)[0]
         xs = x[:a.gt_chains] if x.ndim == 2 else x[0, :a.gt_chains]

@@ -201,16 +201,18 @@ def _dps_model(dmip, fm, seed, zeta, guidance):
     return m, prior, sur_params
 
 
+@pytest.mark.parametrize("precision", ["fp32x3", "fp32"])
 @pytest.mark.parametrize("guidance,zeta", [("nll", 1.0), ("nll", 0.0), ("norm", 0.05)])
-def test_dps_vs_oracle_product_rng(dmip, golden, fm, guidance, zeta):
-    """Fused DPS kernel (prior score + forward-mode Jacobian, Tweedie estimate, surrogate residual
-    gradient, EM) against oracle.dps_sample with the same chain-keyed RNG; 5 steps, 300 chains.
-    Both compute in f32 / f64 respectively: |x - ref| <= 1e-3 max(1, |ref|)."""
+def test_dps_vs_oracle_product_rng(dmip, golden, fm, guidance, zeta, precision):
+    """Fused DPS kernels against oracle.dps_sample with the same chain-keyed RNG; 5 steps, 300 chains:
+    "fp32" = exact f32 (prior score + forward-mode Jacobian, Tweedie estimate, surrogate residual gradient, EM);
+    "fp32x3" = the split-fp16 engine (the prior's J^T by a reverse pass; dmip_dps_x3.hip). The oracle computes in
+    f64: |x - ref| <= 1e-3 max(1, |ref|)."""
     m, prior, sur = _dps_model(dmip, fm, 3, zeta, guidance)
     y = golden("data_scat.npz")["y_test"][2]
     n, S, seed = 300, 5, 21
     before = dmip._lib.calls.get("dps_sample", 0)
-    x = m.sample_device(torch.from_numpy(y).to(DEV), n, S, seed=seed)[0].cpu().numpy()
+    x = m.sample_device(torch.from_numpy(y).to(DEV), n, S, seed=seed, precision=precision)[0].cpu().numpy()
     assert dmip._lib.calls["dps_sample"] == before + 1
     ref = O.dps_sample(prior, sur, y, n, S, seed, zeta=zeta, mode=guidance)
     assert np.all(np.isfinite(x))
@@ -221,13 +223,46 @@ def test_dps_vs_oracle_product_rng(dmip, golden, fm, guidance, zeta):
         assert np.abs(plain - ref).max() > 100 * err.max()
 
 
-def test_dps_shards_bit_identical(dmip, golden, fm):
+@pytest.mark.parametrize("precision", ["fp32x3", "fp32"])
+def test_dps_shards_bit_identical(dmip, golden, fm, precision):
     m, _, _ = _dps_model(dmip, fm, 4, 1.0, "nll")
     ys = torch.from_numpy(golden("data_scat.npz")["y_test"][:2]).to(DEV)
-    full = m.sample_device(ys, 700, 6, seed=5)
-    shard = m.sample_device(ys, 200, 6, seed=5, chain_offset=300)
+    full = m.sample_device(ys, 700, 6, seed=5, precision=precision)
+    shard = m.sample_device(ys, 200, 6, seed=5, chain_offset=300, precision=precision)
     assert torch.equal(full[:, 300:500], shard)
     assert not torch.equal(full[0], full[1])
+
+
+@pytest.mark.parametrize("guidance,zeta", [("norm", 0.005), ("nll", 0.002)])
+def test_dps_fp32x3_matches_exact_f32_over_many_steps(dmip, golden, fm, guidance, zeta):
+    """The two DPS engines chain by chain (same RNG) over 200 steps with the seeded smooth prior: the split-fp16
+    products and the reverse-mode J^T against exact f32 with forward tangents, within 1e-3 of max |x|."""
+    m, _, _ = _dps_model(dmip, fm, 5, zeta, guidance)
+    y = torch.from_numpy(golden("data_scat.npz")["y_test"][0]).to(DEV)
+    n, S, seed = 2000, 200, 77
+    a = m.sample_device(y, n, S, seed=seed, precision="fp32x3")[0].cpu().numpy()
+    b = m.sample_device(y, n, S, seed=seed, precision="fp32")[0].cpu().numpy()
+    assert np.all(np.isfinite(a)) and np.all(np.isfinite(b))
+    e = float(np.abs(a - b).max() / max(1.0, np.abs(b).max()))
+    print(f"\n[dps] fp32x3 vs exact f32, {guidance}, {S} steps: {e:.2e}")
+    assert e < 1e-3, e
+    assert not np.array_equal(a, b)  # two engines ran
+
+
+def test_dps_fp32x3_out_of_range_weight_falls_back(dmip, golden, fm):
+    """A prior weight beyond fp16's range in the split image: an explicit fp32x3 request is refused ("fp16 range"),
+    the default precision resamples with the exact-f32 engine (parallel.sample_checked), chain for chain."""
+    m, _, _ = _dps_model(dmip, fm, 6, 0.05, "norm")
+    with torch.no_grad():
+        [l for l in m.prior_net if isinstance(l, torch.nn.Linear)][1].weight[3, 4] = 7.0e4
+    y = torch.from_numpy(golden("data_scat.npz")["y_test"][1]).to(DEV)
+    with pytest.raises(ValueError, match="fp16 range"):
+        m.sample_device(y, 100, 3, seed=2, precision="fp32x3")
+    torch.manual_seed(8)
+    with pytest.warns(RuntimeWarning, match="fp16 range"):
+        x = m(y, num_samples=100, num_steps=3)
+    torch.manual_seed(8)
+    assert np.array_equal(x, m(y, num_samples=100, num_steps=3, precision="fp32"))
 
 
 def test_evaluate_scatterometry_driver(dmip, golden, fm, tmp_path):
