@@ -162,6 +162,28 @@ def _declare(lib):
         getattr(lib, name).restype = _i32
 
 
+class _OlderBuild:
+    """An older build of the library loaded for a same-box timing A/B (DMIP_LIB=<path> DMIP_LIB_AB=1, scripts/): the
+    entry points it lacks take their ctypes declarations and fail when called. Never the product path."""
+
+    def __init__(self, handle):
+        self._handle, self._absent = handle, {}
+
+    def __getattr__(self, name):
+        try:
+            return getattr(self._handle, name)
+        except AttributeError:
+            return self._absent.setdefault(name, _Absent(name))
+
+
+class _Absent:
+    def __init__(self, name):
+        self.name = name
+
+    def __call__(self, *args):
+        raise RuntimeError(f"dmip: {LIB_PATH} (A/B build) has no {self.name}")
+
+
 def lib():
     """The loaded library; raises RuntimeError if it has not been built."""
     global _lib
@@ -174,7 +196,9 @@ def lib():
                         "`python -c 'import __graft_entry__ as g; g.build()'` or `make` at the repo root")
                 handle = ctypes.CDLL(LIB_PATH)
                 missing = [n for n in EXPORTED if not hasattr(handle, n)]
-                if missing:
+                if missing and os.environ.get("DMIP_LIB_AB") == "1":
+                    handle = _OlderBuild(handle)
+                elif missing:
                     raise RuntimeError(f"dmip: {LIB_PATH} is not ABI {ABI_VERSION}: missing {', '.join(missing)} "
                                        "(rebuild with `make` at the repo root)")
                 _declare(handle)

@@ -10,7 +10,7 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_x3k.py tests/test_gpu_x3.py
 rc=$?; echo "pytest rc=$rc"; grep -E "FAILED|passed|failed" "$OUT/pytest.log" | tail -12
 case $rc in 0|1) ;; *) exit 3 ;; esac
 for r in 1 2 3; do
-  DMIP_LIB=abv/r5_base/libdmip.so timeout -k 10 200 python -u scripts/sweep.py --chains 100000 --rounds 2 > "$OUT/x3k_base_$r.json" 2>/dev/null || exit 3
+  DMIP_LIB=abv/r5_base/libdmip.so DMIP_LIB_AB=1 timeout -k 10 200 python -u scripts/sweep.py --chains 100000 --rounds 2 > "$OUT/x3k_base_$r.json" 2>/dev/null || exit 3
   timeout -k 10 200 python -u scripts/sweep.py --chains 100000 --rounds 2 > "$OUT/x3k_new_$r.json" 2>/dev/null || exit 3
   python -c "import json;b=json.load(open('$OUT/x3k_base_$r.json'));n=json.load(open('$OUT/x3k_new_$r.json'));print('x3k base',b['v0_n100000']['ms_median'],'new',n['v0_n100000']['ms_median'])"
 done

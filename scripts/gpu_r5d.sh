@@ -12,7 +12,7 @@ rc=$?; echo "pytest rc=$rc"; grep -E "FAILED|passed|failed" "$OUT/pytest.log" | 
 case $rc in 0|1) ;; *) exit 3 ;; esac
 for r in 1 2 3; do
   timeout -k 10 120 python -u scripts/bench_config5.py --steps 50 > "$OUT/c5_new_$r.json" 2>/dev/null || exit 3
-  DMIP_LIB=$BASE timeout -k 10 120 python -u scripts/bench_config5.py --steps 50 > "$OUT/c5_base_$r.json" 2>/dev/null || exit 3
+  DMIP_LIB=$BASE DMIP_LIB_AB=1 timeout -k 10 120 python -u scripts/bench_config5.py --steps 50 > "$OUT/c5_base_$r.json" 2>/dev/null || exit 3
   echo "new  $(tail -1 $OUT/c5_new_$r.json | cut -c1-110)"; echo "base $(tail -1 $OUT/c5_base_$r.json | cut -c1-110)"
 done
 timeout -k 10 120 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
