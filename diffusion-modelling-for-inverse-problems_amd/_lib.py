@@ -17,14 +17,14 @@ LIB_PATH = os.environ.get("DMIP_LIB", os.path.join(_HERE, "libdmip.so"))
 
 DMIP_OK, DMIP_ERR_INVALID, DMIP_ERR_UNSUPPORTED, DMIP_ERR_HIP, DMIP_ERR_ALLOC = range(5)
 DMIP_INPUT_X_Y_T, DMIP_INPUT_X_T = 0, 1
-DMIP_ACT_TANH_TWICE_FIRST, DMIP_ACT_TANH = 0, 1
+DMIP_ACT_TANH_TWICE_FIRST, DMIP_ACT_TANH, DMIP_ACT_SILU_TWICE_FIRST = 0, 1, 2
 DMIP_PREC_FP16, DMIP_PREC_F32, DMIP_PREC_F32X3 = 0, 1, 2
 # DMIP_PREC_BF16 (include/dmip.h): the same value -- the config-5 training kernel's split-bf16 arithmetic, and the
 # samplers' deprecated name of DMIP_PREC_FP16 (their 16-bit engine computes its hidden and output layers in fp16)
 DMIP_PREC_BF16 = DMIP_PREC_FP16
 PRECISIONS = {"fp16": DMIP_PREC_FP16, "bf16": DMIP_PREC_BF16, "fp32": DMIP_PREC_F32, "fp32x3": DMIP_PREC_F32X3}
 DMIP_SAMPLER_CDE, DMIP_SAMPLER_POSTERIOR, DMIP_SAMPLER_CDIFFE = 0, 1, 2
-ABI_VERSION = 7
+ABI_VERSION = 8
 DMIP_LOSS_DSM, DMIP_LOSS_DSM_PDE, DMIP_LOSS_PINN, DMIP_LOSS_PINN2 = 0, 1, 2, 3
 DMIP_PDE_NONE, DMIP_PDE_FPE, DMIP_PDE_CFPE = 0, 1, 2
 DMIP_METRIC_L1, DMIP_METRIC_L2 = 0, 1
@@ -196,11 +196,15 @@ def lib():
                         "`python -c 'import __graft_entry__ as g; g.build()'` or `make` at the repo root")
                 handle = ctypes.CDLL(LIB_PATH)
                 missing = [n for n in EXPORTED if not hasattr(handle, n)]
-                if missing and os.environ.get("DMIP_LIB_AB") == "1":
+                ab = os.environ.get("DMIP_LIB_AB") == "1"
+                if missing and ab:
                     handle = _OlderBuild(handle)
                 elif missing:
                     raise RuntimeError(f"dmip: {LIB_PATH} is not ABI {ABI_VERSION}: missing {', '.join(missing)} "
                                        "(rebuild with `make` at the repo root)")
+                elif not ab and handle.dmip_abi_version() != ABI_VERSION:
+                    raise RuntimeError(f"dmip: {LIB_PATH} is ABI {handle.dmip_abi_version()}, this package needs "
+                                       f"{ABI_VERSION} (rebuild with `make` at the repo root)")
                 _declare(handle)
                 _lib = handle
     return _lib
@@ -236,7 +240,7 @@ def vpsde(beta_min, beta_max, T):
 class MlpHandle:
     """Owns a dmip_mlp* (packed device weights) for one snapshot of a network's parameters."""
 
-    def __init__(self, layers, in_dim, out_dim, xdim, input_layout, device):
+    def __init__(self, layers, in_dim, out_dim, xdim, input_layout, device, act=DMIP_ACT_TANH_TWICE_FIRST):
         L = len(layers) - 1
         widths = (_i32 * L)(*[int(layers[i][0].shape[0]) for i in range(L)])
         with torch.cuda.device(device):
@@ -245,13 +249,14 @@ class MlpHandle:
             wp = (_c_void_p * (L + 1))(*[w.data_ptr() for w in ws])
             bp = (_c_void_p * (L + 1))(*[b.data_ptr() for b in bs])
             out = _c_void_p()
-            check(lib().dmip_mlp_create(in_dim, out_dim, L, widths, DMIP_ACT_TANH_TWICE_FIRST,
-                                        input_layout, xdim, wp, bp, ctypes.byref(out)))
+            check(lib().dmip_mlp_create(in_dim, out_dim, L, widths, act, input_layout, xdim, wp, bp,
+                                        ctypes.byref(out)))
         self.h = out
         self.device = device
         self.width = int(layers[0][0].shape[0])
         self.n_hidden = L
         self.in_dim, self.out_dim, self.xdim = in_dim, out_dim, xdim
+        self.act = act
 
     def __del__(self):
         h = getattr(self, "h", None)

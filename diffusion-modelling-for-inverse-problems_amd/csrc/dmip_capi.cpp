@@ -252,6 +252,16 @@ int pack_f32_net(dmip_mlp* net, const float* const* weights, const float* const*
 
 dmip::F32Net f32_net(const dmip_mlp* n) { return dmip::F32Net{n->f32_l1, n->f32_stream, n->f32_bias}; }
 
+// the activation chain's code in the exact-f32 kernels (dmip_f32.h act_f32): 0 tanh, 1 SiLU. Only the exact-f32
+// forward and the exact-f32 CDE sampler compile the SiLU chain; every other kernel computes tanh.
+int f32_act(const dmip_mlp* n) { return n->act_mode == DMIP_ACT_SILU_TWICE_FIRST ? 1 : 0; }
+
+int act_refused(const char* what) {
+  return fail(DMIP_ERR_UNSUPPORTED, std::string(what) +
+                                        ": the SiLU chain is compiled for the exact-f32 forward and the exact-f32 "
+                                        "CDE sampler only (DMIP_PREC_F32)");
+}
+
 // ---- fp32-accurate split-fp16 images (DMIP_PREC_F32X3, dmip_x3.h). A 16x16x32 f16 fragment block:
 // lane l = i + 16 g holds A[row i][k-slot 8 g + m], m = 0..7. Hidden-layer k-slots follow the previous
 // layer's accumulator tiles: slot (q, g, m) is unit kperm16(q, g, m).
@@ -639,8 +649,8 @@ int dmip_mlp_create(int in_dim, int out_dim, int n_hidden, const int* widths, in
     if (widths[i] != W) return fail(DMIP_ERR_UNSUPPORTED, "hidden widths must all be equal");
   if (W % 32 != 0 || W < 32) return fail(DMIP_ERR_UNSUPPORTED, "hidden width must be a multiple of 32");
   if (out_dim < 1 || out_dim > 32) return fail(DMIP_ERR_UNSUPPORTED, "out_dim must be in [1, 32]");
-  if (act_mode != DMIP_ACT_TANH_TWICE_FIRST)
-    return fail(DMIP_ERR_UNSUPPORTED, "only the reference activation chain (tanh twice on layer 1) is compiled");
+  if (act_mode != DMIP_ACT_TANH_TWICE_FIRST && act_mode != DMIP_ACT_SILU_TWICE_FIRST)
+    return fail(DMIP_ERR_UNSUPPORTED, "compiled activation chains: DMIP_ACT_TANH_TWICE_FIRST, DMIP_ACT_SILU_TWICE_FIRST");
   if (input_layout != DMIP_INPUT_X_Y_T && input_layout != DMIP_INPUT_X_T)
     return fail(DMIP_ERR_INVALID, "unknown input layout");
   if (xdim < 1 || xdim + 1 > in_dim) return fail(DMIP_ERR_INVALID, "xdim inconsistent with in_dim");
@@ -859,6 +869,7 @@ int dmip_mlp_forward(const dmip_mlp* net, const float* x_dev, const float* y_dev
     q.ydim = ydim;
     q.out_dim = net->out_dim;
     q.k1q = net->f32_k1q;
+    q.act = f32_act(net);
     bool ok = false;
     hipError_t e = dmip::launch_f32_forward(q, net->width, net->f32_ot, (hipStream_t)stream, &ok);
     if (!ok)
@@ -868,6 +879,7 @@ int dmip_mlp_forward(const dmip_mlp* net, const float* x_dev, const float* y_dev
     if (e != hipSuccess) return hip_fail(e, "mlp_forward (f32) launch");
     return DMIP_OK;
   }
+  if (f32_act(net)) return act_refused("mlp_forward at DMIP_PREC_FP16");
   dmip::ForwardParams p{};
   p.hidden = net->hidden;
   p.a1 = net->a1_full;
@@ -967,6 +979,7 @@ static int em_sample_f32(int mode, const dmip_mlp* net0, const dmip_mlp* net1, c
   }
   p.debug_flags = debug_no_handover();
   p.spin_limit = p.debug_flags ? (1u << 10) : (1u << 22);
+  p.act = f32_act(net0);
   bool ok = false;
   hipError_t e = dmip::launch_f32_sampler(p, mode, net0->width, net0->n_hidden, xdim, ydim, a.n_y, st, &ok);
   if (l1y) (void)hipFreeAsync(l1y, st);
@@ -1093,6 +1106,9 @@ static int em_sample_impl(int mode, const dmip_mlp* net0, const dmip_mlp* net1, 
   if (a.n_chains < 0 || a.chain_offset < 0) return fail(DMIP_ERR_INVALID, "negative chain count/offset");
   if (a.num_steps < 1) return fail(DMIP_ERR_INVALID, "num_steps must be >= 1");
   if (!(a.sde->T > 0.0)) return fail(DMIP_ERR_INVALID, "T must be > 0");
+  if (f32_act(net0) || (net1 && f32_act(net1))) {
+    if (a.precision != DMIP_PREC_F32 || mode != DMIP_SAMPLER_CDE) return act_refused("em_sample");
+  }
   if (a.n_chains == 0) return DMIP_OK;
   if (a.precision == DMIP_PREC_F32) return em_sample_f32(mode, net0, net1, a);
   if (a.precision == DMIP_PREC_F32X3) return em_sample_x3(mode, net0, net1, a);
@@ -2008,6 +2024,7 @@ int dmip_dps_sample(const dmip_mlp* prior, const dmip_surrogate* fwd, const dmip
                     void* stream) {
   if (!prior || !fwd || !sde || !y_dev || !x_out_dev) return fail(DMIP_ERR_INVALID, "null argument");
   if (mode != DMIP_DPS_NLL && mode != DMIP_DPS_NORM) return fail(DMIP_ERR_INVALID, "unknown DPS guidance mode");
+  if (f32_act(prior)) return act_refused("dps_sample");
   dmip::DpsParams p{};
   if (mode == DMIP_DPS_NLL) {
     if (int rc = noise_check(noise, p.s)) return rc;
@@ -2054,6 +2071,7 @@ int dmip_dps_sample_ex(const dmip_mlp* prior, const dmip_surrogate* fwd, const d
                            mode, zeta, x_out_dev, stream);
   if (precision != DMIP_PREC_F32X3) return fail(DMIP_ERR_INVALID, "DPS precision: DMIP_PREC_F32 or DMIP_PREC_F32X3");
   if (!prior || !fwd || !sde || !y_dev || !x_out_dev) return fail(DMIP_ERR_INVALID, "null argument");
+  if (f32_act(prior)) return act_refused("dps_sample_ex");
   if (mode != DMIP_DPS_NLL && mode != DMIP_DPS_NORM) return fail(DMIP_ERR_INVALID, "unknown DPS guidance mode");
   dmip::DpsX3Params p{};
   if (mode == DMIP_DPS_NLL) {

@@ -59,10 +59,19 @@ struct FLay {
   static_assert(R >= 2, "LDS budget: fewer than two ring slots");
 };
 
+// the hidden activation (include/dmip.h dmip_act): ACT 0 = tanh (the reference's nn.Tanh, libm tanhf), 1 = SiLU
+// (nn.SiLU: z sigmoid(z) = z / (1 + exp(-z)) with libm expf and an IEEE division). Layer 1 applies it twice
+// (nets.py:26: the activation module is registered a second time as `act`, whatever it is)
+template <int ACT>
+__device__ __forceinline__ float act_f32(float z) {
+  if constexpr (ACT == 0) return tanhf(z);
+  else return z / (1.0f + expf(-z));
+}
+
 // The network engine: NNET networks of nl layers (runtime) of width W share one weight ring; each
 // network evaluation streams (nl - 1) ST hidden tiles then OT output tiles, in the order of the host's
-// stream image. The ring position advances incrementally (no 64-bit modulo per chunk).
-template <int W, int NNET, int OT, int R, int RING_OFF>
+// stream image. The ring position advances incrementally (no 64-bit modulo per chunk). ACT: act_f32.
+template <int W, int NNET, int OT, int R, int RING_OFF, int ACT = 0>
 struct FEngine {
   using S = Shape<W>;
   static constexpr int ST = S::ST, NW = S::NW, PPW = S::PPW, CHUNK = S::CHUNK;
@@ -145,7 +154,7 @@ struct FEngine {
     return acc0 + acc1;
   }
 
-  // layer 1 (every input column + the bias column, image at l1_off) and its double tanh (nets.py:21-26)
+  // layer 1 (every input column + the bias column, image at l1_off) and its double activation (nets.py:21-26)
   //   K1Q: k-steps compiled (the operand array), k1q: k-steps of the image (<= K1Q, wave-uniform)
   template <int K1Q>
   __device__ __forceinline__ void layer1(int l1_off, int k1q, const float (&b)[K1Q], float (&H)[ST][4]) {
@@ -158,7 +167,7 @@ struct FEngine {
       for (int s = 0; s < K1Q; ++s)
         if (s < k1q) z = mfma4(l1[(o * k1q + s) * 64 + lane], b[s], z);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) H[o][r] = tanhf(tanhf(z[r]));
+      for (int r = 0; r < 4; ++r) H[o][r] = act_f32<ACT>(act_f32<ACT>(z[r]));
     }
   }
 
@@ -168,7 +177,7 @@ struct FEngine {
       const char* ch = chunk_sync();
       const f32x4 z = tile_product(ch, Hin, bias4(ni, li, o));
 #pragma unroll
-      for (int r = 0; r < 4; ++r) Hout[o][r] = tanhf(z[r]);
+      for (int r = 0; r < 4; ++r) Hout[o][r] = act_f32<ACT>(z[r]);
     }
   }
 
@@ -220,7 +229,7 @@ constexpr int kMaxHidden = 3;  // hidden layers compiled: 1..3 (bias staging bou
 // the balanced WaveSchedule of dmip_device.h (equal segments of C wave-steps, split tiles handed over
 // through global memory), so 100k chains cost 3.05 rounds of the GPU's capacity, not 4. Every lane
 // group of a chain holds the same state, so the hand-over stores all 64 lanes like the 16-bit kernel.
-template <int MODE, int W, int D, int M>
+template <int MODE, int W, int D, int M, int ACT = 0>
 struct SamplerCfg {
   static constexpr int NNET = MODE == SAMPLER_POSTERIOR ? 2 : 1;
   static constexpr int NV0 = MODE == SAMPLER_CDIFFE ? D + M + 1 : D + 1;  // net 0 inputs (y folded for CDE)
@@ -228,12 +237,12 @@ struct SamplerCfg {
   static constexpr int K1Q1 = k1q_of(D + 2);                              // prior (x, t) + bias
   static constexpr int BF_MAX = (kMaxHidden - 1) * W + 16;                // hidden biases + output tile 0
   using L = FLay<W, NNET, K1Q0, K1Q1, BF_MAX, M>;
-  using E = FEngine<W, NNET, 1, L::R, L::RING>;
+  using E = FEngine<W, NNET, 1, L::R, L::RING, ACT>;
 };
 
-template <int MODE, int W, int D, int M, bool NOISE>
+template <int MODE, int W, int D, int M, bool NOISE, int ACT = 0>
 __global__ void __launch_bounds__(Shape<W>::NW * 64, 1) f32_sampler_kernel(F32SamplerParams p) {
-  using C = SamplerCfg<MODE, W, D, M>;
+  using C = SamplerCfg<MODE, W, D, M, ACT>;
   using L = typename C::L;
   using E = typename C::E;
   constexpr int NW = Shape<W>::NW, ST = Shape<W>::ST;
@@ -410,16 +419,16 @@ __global__ void __launch_bounds__(Shape<W>::NW * 64, 1) f32_sampler_kernel(F32Sa
 //   K1Q: layer-1 k-steps compiled (any image with in_dim + 1 <= 4 K1Q; the image's own count is the
 //   runtime p.k1q);  OT: output tiles (out_dim <= 16 OT)
 constexpr int kForwardK1Q = 8;
-template <int W, int K1Q, int OT>
+template <int W, int K1Q, int OT, int ACT>
 struct ForwardCfg {
   static constexpr int BF_MAX = (kMaxHidden - 1) * W + 16 * OT;
   using L = FLay<W, 1, K1Q, 1, BF_MAX, 0>;
-  using E = FEngine<W, 1, OT, L::R, L::RING>;
+  using E = FEngine<W, 1, OT, L::R, L::RING, ACT>;
 };
 
-template <int W, int K1Q, int OT>
+template <int W, int K1Q, int OT, int ACT>
 __global__ void __launch_bounds__(Shape<W>::NW * 64, 1) f32_forward_kernel(F32ForwardParams p) {
-  using C = ForwardCfg<W, K1Q, OT>;
+  using C = ForwardCfg<W, K1Q, OT, ACT>;
   using L = typename C::L;
   constexpr int NW = Shape<W>::NW, ST = Shape<W>::ST;
   static_assert(L::TOTAL <= kLdsBudget, "LDS budget");
@@ -474,10 +483,10 @@ __global__ void __launch_bounds__(Shape<W>::NW * 64, 1) f32_forward_kernel(F32Fo
 }  // namespace f32
 
 // ----------------------------------------------------------------- launch helpers (per TU)
-template <int MODE, int W, int D, int M, bool NOISE>
+template <int MODE, int W, int D, int M, bool NOISE, int ACT = 0>
 inline hipError_t launch_f32_sampler_t(const F32SamplerParams& p, int n_y, hipStream_t st) {
   constexpr int NW = f32::Shape<W>::NW;
-  auto kern = f32::f32_sampler_kernel<MODE, W, D, M, NOISE>;
+  auto kern = f32::f32_sampler_kernel<MODE, W, D, M, NOISE, ACT>;
   const long long tiles = (p.n_chains + 15) / 16;
   long long g = resident_slots(kern, NW * 64, st) / (n_y > 0 ? n_y : 1);
   const long long cap = (tiles + NW - 1) / NW;
@@ -495,18 +504,24 @@ inline hipError_t launch_f32_sampler_t(const F32SamplerParams& p, int n_y, hipSt
   return e;
 }
 
+// the SiLU chain (p.act == DMIP_ACT_SILU_TWICE_FIRST) is compiled for the CDE sampler only; the caller
+// (dmip_em_sample) refuses it for the other modes
 template <int MODE, int W, int D, int M>
 inline hipError_t launch_f32_sampler_n(const F32SamplerParams& p, int n_y, hipStream_t st) {
   if constexpr (MODE == SAMPLER_CDE) {
+    if (p.act != 0) {
+      if (p.noise) return launch_f32_sampler_t<MODE, W, D, M, true, 1>(p, n_y, st);
+      return launch_f32_sampler_t<MODE, W, D, M, false, 1>(p, n_y, st);
+    }
     if (p.noise) return launch_f32_sampler_t<MODE, W, D, M, true>(p, n_y, st);
   }
   return launch_f32_sampler_t<MODE, W, D, M, false>(p, n_y, st);
 }
 
-template <int W, int K1Q, int OT>
+template <int W, int K1Q, int OT, int ACT>
 inline hipError_t launch_f32_forward_t(const F32ForwardParams& p, hipStream_t st) {
   constexpr int NW = f32::Shape<W>::NW;
-  auto kern = f32::f32_forward_kernel<W, K1Q, OT>;
+  auto kern = f32::f32_forward_kernel<W, K1Q, OT, ACT>;
   const long long tiles = (p.n + 15) / 16;
   long long g = resident_slots(kern, NW * 64, st);
   const long long cap = (tiles + NW - 1) / NW;

@@ -63,8 +63,9 @@ hipError_t launch_f32_forward(const F32ForwardParams& p, int width, int ot, hipS
     return hipSuccess;
   }
   constexpr int K = f32::kForwardK1Q;
-#define X(Wv, OTv) \
-  if (width == Wv && ot == OTv) return launch_f32_forward_t<Wv, K, OTv>(p, st);
+#define X(Wv, OTv)                                                                                    \
+  if (width == Wv && ot == OTv)                                                                       \
+    return p.act ? launch_f32_forward_t<Wv, K, OTv, 1>(p, st) : launch_f32_forward_t<Wv, K, OTv, 0>(p, st);
   X(64, 1) X(128, 1) X(256, 1) X(512, 1) X(64, 2) X(128, 2) X(256, 2) X(512, 2)
 #undef X
   *supported = false;

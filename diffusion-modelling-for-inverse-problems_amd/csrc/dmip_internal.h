@@ -245,6 +245,7 @@ struct F32SamplerParams {
   unsigned int* err;
   unsigned int spin_limit;
   int debug_flags;
+  int act;                    // 0 tanh, 1 SiLU (dmip_act: the activation chain; SiLU for SAMPLER_CDE only)
 };
 
 struct F32ForwardParams {
@@ -257,6 +258,7 @@ struct F32ForwardParams {
   long long n, y_stride;
   int t_stride, xdim, ydim, out_dim;
   int k1q;                    // layer-1 k-steps of the image: ceil((in_dim + 1) / 4)
+  int act;                    // 0 tanh, 1 SiLU (dmip_act)
 };
 
 struct F32L1PrepParams {

@@ -65,11 +65,15 @@ def default_precision():
 _MORE_ACCURATE = {"fp16": ("fp32x3", "fp32"), "fp32x3": ("fp32",), "fp32": ()}
 
 
-def _fused_precision(precision, mode, width, n_hidden, xdim, ydim):
+def _fused_precision(precision, mode, width, n_hidden, xdim, ydim, acts=(_lib.DMIP_ACT_TANH_TWICE_FIRST,)):
     """The precision a fused kernel runs this shape in: the requested one, else the next more accurate
-    one that is compiled (_MORE_ACCURATE); None when none is (per-step loop)."""
+    one that is compiled (_MORE_ACCURATE); None when none is (per-step loop). `acts`: the networks' activation
+    chains -- a SiLU network has the exact-f32 CDE sampler only (include/dmip.h dmip_act)."""
     _lib.precision_code(precision)
     precision = canonical_precision(precision)
+    if any(a != _lib.DMIP_ACT_TANH_TWICE_FIRST for a in acts):
+        ok = mode == _lib.DMIP_SAMPLER_CDE and _lib.sampler_supported(width, n_hidden, xdim, ydim, mode, "fp32")
+        return "fp32" if ok else None
     for prec in (precision,) + _MORE_ACCURATE[precision]:
         if _lib.sampler_supported(width, n_hidden, xdim, ydim, mode, prec):
             return prec
@@ -120,9 +124,10 @@ class BaseClassDiffusionModel:
         net, prior = handles[-1], (handles[0] if len(handles) > 1 else None)
         if prior is not None and (prior.width, prior.n_hidden) != (net.width, net.n_hidden):
             raise ValueError("prior and likelihood networks must have the same hidden layers")
-        prec = _fused_precision(precision or self.precision, mode, net.width, net.n_hidden, self.xdim, self.ydim)
+        prec = _fused_precision(precision or self.precision, mode, net.width, net.n_hidden, self.xdim, self.ydim,
+                                [h.act for h in handles])
         if prec is None:
-            raise ValueError("no fused sampler for this network shape")
+            raise ValueError("no fused sampler for this network shape / activation")
         snaps = torch.empty(int(num_steps) // int(snapshot_every), ys.shape[0], int(num_samples), self.xdim,
                             device=dev, dtype=torch.float32)
         seed = _draw_seed() if seed is None else seed
@@ -220,7 +225,7 @@ class CDE(BaseClassDiffusionModel):
         handle = net.dmip_handle(dev, self.xdim)
         seed = _draw_seed() if seed is None else seed
         prec = _fused_precision(precision or self.precision, _lib.DMIP_SAMPLER_CDE, handle.width, handle.n_hidden,
-                                self.xdim, self.ydim)
+                                self.xdim, self.ydim, [handle.act])
         if noise is not None:
             noise = noise.to(device=dev, dtype=torch.float32).contiguous()
             if tuple(noise.shape) != (int(num_steps) + 1, ys.shape[0], int(num_samples), self.xdim):
@@ -347,7 +352,7 @@ class CDiffE(BaseClassDiffusionModel):
         seed = _draw_seed() if seed is None else seed
         handle = net.dmip_handle(dev, self.xdim)
         prec = _fused_precision(precision or self.precision, _lib.DMIP_SAMPLER_CDIFFE, handle.width,
-                                handle.n_hidden, self.xdim, self.ydim)
+                                handle.n_hidden, self.xdim, self.ydim, [handle.act])
         if prec is not None:
             _lib.em_sample_cdiffe(handle, sde, ys, num_samples, chain_offset, num_steps, mean, std, seed, out,
                                   corrector_steps, snr, prec)
@@ -414,7 +419,7 @@ class PosteriorDiffusionEstimator(BaseClassDiffusionModel):
         prec = None
         if (prior.width, prior.n_hidden) == (lik.width, lik.n_hidden):
             prec = _fused_precision(precision or self.precision, _lib.DMIP_SAMPLER_POSTERIOR, lik.width,
-                                    lik.n_hidden, self.xdim, self.ydim)
+                                    lik.n_hidden, self.xdim, self.ydim, [prior.act, lik.act])
         if prec is not None:
             _lib.em_sample_posterior(prior, lik, sde, ys, num_samples, chain_offset, num_steps, mean, std, seed,
                                      out, prec)

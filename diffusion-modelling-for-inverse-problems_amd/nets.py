@@ -11,6 +11,8 @@ Evaluation on a HIP device with autograd off goes to the fused MFMA kernel
 arithmetic, e.g. for the evaluate drivers' score MSE), or with 16-bit operands (`"fp16"`: split-bf16 layer 1,
 fp16 hidden and output layers; `"bf16"` is its deprecated name); the weights
 are packed once per parameter snapshot. Autograd (the training losses) uses the eager module chain.
+The activation is the reference's constructor argument: nn.Tanh runs on every engine, nn.SiLU on the exact-f32
+forward and CDE sampler (`dmip_act`); any other activation has no HIP kernel and the HIP paths refuse it.
 """
 import collections
 
@@ -39,6 +41,24 @@ class _TanhChainMLP(nn.Sequential):
         self.dmip_precision = "fp32"  # arithmetic of the HIP forward (dmip_mlp_forward): "fp32" or "fp16"
 
     # -------------------------------------------------------------- packed HIP weights
+    @property
+    def dmip_act(self):
+        """The compiled activation chain of this network (include/dmip.h dmip_act): nn.Tanh -> the reference's
+        chain, nn.SiLU -> the SiLU chain (exact-f32 forward and CDE sampler only); None for any other activation,
+        which has no HIP kernel (the HIP paths raise NotImplementedError rather than compute another function)."""
+        if isinstance(self.act, nn.Tanh):
+            return _lib.DMIP_ACT_TANH_TWICE_FIRST
+        if isinstance(self.act, nn.SiLU):
+            return _lib.DMIP_ACT_SILU_TWICE_FIRST
+        return None
+
+    def require_dmip_act(self):
+        act = self.dmip_act
+        if act is None:
+            raise NotImplementedError(f"{type(self.act).__name__} has no HIP kernel: the compiled activation chains "
+                                      "are nn.Tanh (every engine) and nn.SiLU (exact f32)")
+        return act
+
     def linear_layers(self):
         return [(m.weight, m.bias) for m in self if isinstance(m, nn.Linear)]
 
@@ -46,10 +66,11 @@ class _TanhChainMLP(nn.Sequential):
         return (str(device),) + tuple((p.data_ptr(), p._version) for p in self.parameters())
 
     def dmip_handle(self, device, xdim):
-        key = self._snapshot_key(device) + (xdim,)
+        act = self.require_dmip_act()
+        key = self._snapshot_key(device) + (xdim, act)
         if self._dmip is None or self._dmip[0] != key:
             handle = _lib.MlpHandle(self.linear_layers(), self.input_dim, self.output_dim, xdim,
-                                    self.input_layout, device)
+                                    self.input_layout, device, act)
             self._dmip = (key, handle)
         return self._dmip[1]
 
@@ -75,7 +96,10 @@ class _TanhChainMLP(nn.Sequential):
             y_stride = yc.shape[1] if yc.shape[0] == n and n != 1 else 0
             yc = yc.contiguous()
         out = torch.empty(n, self.output_dim, device=dev, dtype=torch.float32)
-        _lib.mlp_forward(h, xc, yc, tt, out, y_stride, t_stride, getattr(self, "dmip_precision", "fp32"))
+        prec = getattr(self, "dmip_precision", "fp32")
+        if h.act != _lib.DMIP_ACT_TANH_TWICE_FIRST:
+            prec = "fp32"  # the SiLU chain's forward is compiled in exact f32 only
+        _lib.mlp_forward(h, xc, yc, tt, out, y_stride, t_stride, prec)
         return out
 
 

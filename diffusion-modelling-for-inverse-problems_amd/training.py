@@ -39,12 +39,18 @@ def _linear_ic(loss_fn):
     return None
 
 
+def _tanh_chain(net):
+    """The fused loss + gradient engines differentiate the reference's tanh chain only (their jets hold tanh
+    derivatives): a network with another activation (nets.MLP dmip_act) trains through autograd."""
+    return getattr(net, "dmip_act", None) == _lib.DMIP_ACT_TANH_TWICE_FIRST
+
+
 def fused_config(model, loss_fn):
     """dmip_loss_cfg for (model, loss_fn), or None when no fused path covers them."""
     if os.environ.get("DMIP_TRAIN_FUSED", "1") == "0":
         return None
     net = model.sde.a
-    if not hasattr(net, "linear_layers"):
+    if not hasattr(net, "linear_layers") or not _tanh_chain(net):
         return None
     layers = net.linear_layers()
     p0 = layers[0][0]
@@ -83,7 +89,7 @@ def joint_fused_config(model, loss_fn):
     if os.environ.get("DMIP_TRAIN_FUSED", "1") == "0" or type(loss_fn) is not DSMLoss:
         return None
     net = model.sde.a
-    if not hasattr(net, "linear_layers"):
+    if not hasattr(net, "linear_layers") or not _tanh_chain(net):
         return None
     layers = net.linear_layers()
     p0 = layers[0][0]
@@ -469,6 +475,8 @@ def posterior_fused_ok(model, loss_fn):
     if os.environ.get("DMIP_TRAIN_FUSED", "1") == "0" or not isinstance(loss_fn, PosteriorLoss):
         return False
     prior, lik = model.sde.a.prior_net, model.sde.a.likelihood_net
+    if not (_tanh_chain(prior) and _tanh_chain(lik)):
+        return False
     p0 = prior.linear_layers()[0][0]
     if not p0.is_cuda or p0.dtype != torch.float32 or (model.xdim, model.ydim) != (3, 23):
         return False

@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define DMIP_ABI_VERSION 7
+#define DMIP_ABI_VERSION 8
 
 typedef enum {
   DMIP_OK = 0,
@@ -34,8 +34,12 @@ typedef enum { DMIP_INPUT_X_Y_T = 0, DMIP_INPUT_X_T = 1 } dmip_input_layout;
 
 /* Activation chain (nets.py:17-30): Linear -> Tanh -> Tanh -> [Linear -> Tanh]*(L-1) -> Linear.
  * The first hidden layer applies tanh twice because MLP registers its activation module a second
- * time as `self.act` (nets.py:26). DMIP_ACT_TANH is the single-tanh chain. */
-typedef enum { DMIP_ACT_TANH_TWICE_FIRST = 0, DMIP_ACT_TANH = 1 } dmip_act;
+ * time as `self.act` (nets.py:26). DMIP_ACT_TANH is the single-tanh chain (not compiled).
+ * DMIP_ACT_SILU_TWICE_FIRST (ABI 8): the same chain for an MLP built with nn.SiLU() (nets.py:17's `activation`
+ * argument; SiLU(z) = z sigmoid(z)), twice on layer 1 by the same registration. It is compiled for the exact-f32
+ * network forward (dmip_mlp_forward at DMIP_PREC_F32 / F32X3) and the exact-f32 CDE sampler (dmip_em_sample at
+ * DMIP_PREC_F32); every other entry point refuses a SiLU network with DMIP_ERR_UNSUPPORTED. */
+typedef enum { DMIP_ACT_TANH_TWICE_FIRST = 0, DMIP_ACT_TANH = 1, DMIP_ACT_SILU_TWICE_FIRST = 2 } dmip_act;
 
 /* Arithmetic of the network GEMMs; the chain state, the schedule and the SDE update are fp32 in both.
  *   DMIP_PREC_FP16  16-bit MFMA operands, fp32 accumulation: layer 1 is a bf16 MFMA over split hi+lo

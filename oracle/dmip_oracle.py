@@ -94,39 +94,51 @@ def mlp_params_from_state(state, prefix=""):
             for i in idx]
 
 
-def mlp_forward(params, inp, tanh_twice_first=True):
-    """nets.py:17-35. Forward chain is Linear -> Tanh -> Tanh(act, the quirk of nets.py:26) ->
-    [Linear -> Tanh] * (L-1) -> Linear."""
+def activation(h, act="tanh"):
+    """The hidden activation of nets.py:17's `activation` argument: "tanh" (nn.Tanh, every diffusion net of the
+    reference, models/diffusion.py:69,118,190,195) or "silu" (nn.SiLU: z sigmoid(z), evaluated in f64 and
+    rounded once)."""
+    if act == "tanh":
+        return np.tanh(h).astype(F32)
+    if act == "silu":
+        z = np.asarray(h, np.float64)
+        return (z / (1.0 + np.exp(-z))).astype(F32)
+    raise ValueError(f"unknown activation {act!r}")
+
+
+def mlp_forward(params, inp, tanh_twice_first=True, act="tanh"):
+    """nets.py:17-35. Forward chain is Linear -> act -> act (the quirk of nets.py:26: the activation module is
+    registered a second time as `act`) -> [Linear -> act] * (L-1) -> Linear."""
     h = np.asarray(inp, F32)
     L = len(params)
     for li, (W, b) in enumerate(params):
         h = (h @ W.T + b).astype(F32)
         if li < L - 1:
-            h = np.tanh(h).astype(F32)
+            h = activation(h, act)
             if li == 0 and tanh_twice_first:
-                h = np.tanh(h).astype(F32)
+                h = activation(h, act)
     return h
 
 
-def cde_a(params, x, y, t):
+def cde_a(params, x, y, t, act="tanh"):
     """MLP.forward (nets.py:32-35): cat[x, y, t.view(N,1)]."""
     x = np.asarray(x, F32)
     n = x.shape[0]
     y = np.broadcast_to(np.asarray(y, F32), (n, np.asarray(y).shape[-1]))
     t = np.broadcast_to(np.asarray(t, F32).reshape(-1, 1), (n, 1))
-    return mlp_forward(params, np.concatenate([x, y, t], axis=1))
+    return mlp_forward(params, np.concatenate([x, y, t], axis=1), act=act)
 
 
-def mlp2_a(params, x, t):
+def mlp2_a(params, x, t, act="tanh"):
     """MLP2.forward (nets.py:52-57): cat[x, t]."""
     x = np.asarray(x, F32)
     t = np.broadcast_to(np.asarray(t, F32).reshape(-1, 1), (x.shape[0], 1))
-    return mlp_forward(params, np.concatenate([x, t], axis=1))
+    return mlp_forward(params, np.concatenate([x, t], axis=1), act=act)
 
 
-def posterior_a(prior_params, lik_params, x, y, t):
+def posterior_a(prior_params, lik_params, x, y, t, act="tanh"):
     """PosteriorScore.forward (nets.py:155-157): g(t) * (prior(x,t) + lik(x,y,t))."""
-    s = (mlp2_a(prior_params, x, t) + cde_a(lik_params, x, y, t)).astype(F32)
+    s = (mlp2_a(prior_params, x, t, act=act) + cde_a(lik_params, x, y, t, act=act)).astype(F32)
     tt = np.broadcast_to(np.asarray(t, F32).reshape(-1, 1), s.shape)
     return (vp_g(tt) * s).astype(F32)
 
@@ -300,25 +312,25 @@ def em_sample(a_fn, x0, num_steps, T=1.0, noise=None, rng_state=None, xdim=None,
 
 
 def cde_sample(params, y, num_samples, num_steps, seed, mean=0.0, std=1.0, chain_offset=0,
-               stream=0, T=1.0, snapshots=None):
+               stream=0, T=1.0, snapshots=None, act="tanh"):
     """Product-RNG CDE sampler: x0 = normals*std + mean (models/diffusion.py:32-33), then EM."""
     xdim = params[-1][0].shape[0]
     st = rng_init(seed, np.arange(chain_offset, chain_offset + num_samples), stream)
     x0 = (rng_normals(st, xdim) * F32(std) + F32(mean)).astype(F32)
     y = np.asarray(y, F32)
-    return em_sample(lambda x, tau: cde_a(params, x, y, tau), x0, num_steps, T=T,
+    return em_sample(lambda x, tau: cde_a(params, x, y, tau, act=act), x0, num_steps, T=T,
                      rng_state=st, xdim=xdim, snapshots=snapshots)
 
 
 def posterior_sample(prior_params, lik_params, y, num_samples, num_steps, seed, mean=0.0, std=1.0,
-                     chain_offset=0, stream=0, T=1.0):
+                     chain_offset=0, stream=0, T=1.0, act="tanh"):
     """Product-RNG PosteriorDiffusionEstimator sampler (models/diffusion.py:27-46 with the
     PosteriorScore drift a = g (prior + lik), nets.py:155-157): same RNG consumption as CDE."""
     xdim = lik_params[-1][0].shape[0]
     st = rng_init(seed, np.arange(chain_offset, chain_offset + num_samples), stream)
     x0 = (rng_normals(st, xdim) * F32(std) + F32(mean)).astype(F32)
     y = np.asarray(y, F32)
-    return em_sample(lambda x, tau: posterior_a(prior_params, lik_params, x, y, tau), x0, num_steps, T=T,
+    return em_sample(lambda x, tau: posterior_a(prior_params, lik_params, x, y, tau, act=act), x0, num_steps, T=T,
                      rng_state=st, xdim=xdim)
 
 

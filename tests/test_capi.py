@@ -32,7 +32,7 @@ def test_exports_every_declared_symbol(lib, dmip):
 
 
 def test_abi_version(lib, dmip):
-    assert lib.dmip_abi_version() == dmip._lib.ABI_VERSION == 7
+    assert lib.dmip_abi_version() == dmip._lib.ABI_VERSION == 8
 
 
 def test_supported_shapes(lib, dmip):
