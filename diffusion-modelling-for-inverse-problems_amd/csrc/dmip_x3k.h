@@ -47,7 +47,15 @@ constexpr int W = 256, ST = 16, KQ = 8, NH = 2;  // [256]*3: layer 1 + two W x W
 constexpr int CHUNK = 32768;                     // k-step q of a W x W layer: 16 tiles x (hi, lo) x 1 KiB
 constexpr int NCHUNK = NH * KQ;                  // ring chunks per step
 constexpr int R = 4;                             // ring slots
-constexpr int PF = 1;                            // ring fragment pairs read ahead (o-steps)
+#ifndef DMIP_X3K_PF
+#define DMIP_X3K_PF 1
+#endif
+#ifndef DMIP_X3K_SYNC_O
+#define DMIP_X3K_SYNC_O 8
+#endif
+constexpr int PF = DMIP_X3K_PF;                  // ring fragment pairs read ahead (o-steps)
+constexpr int SYNC_O = DMIP_X3K_SYNC_O;          // the o-step of a chunk that holds the next chunk's barrier
+static_assert(SYNC_O + PF < 16 && SYNC_O < 15, "the barrier precedes the next chunk's first reads, pieces follow it");
 // waves per workgroup: one per SIMD for 2-3 chain tiles per wave (up to 512 registers), two per SIMD for
 // one tile per wave (<= 256 registers: each wave's VALU chains issue between the other's MFMAs)
 template <int NT>
@@ -224,7 +232,7 @@ struct KEngine {
   // boundary at the last PF o-steps -- by explicit ds_read_b128 with counted lgkmcnt waits; left to itself the
   // compiler hoists all 32 reads to the chunk's top, 128 more registers), beside one slice of the work the
   // chunk carries: the activation of k-step Q + 1's operand pair (t, d) = (O / 4, O % 4) for O < 4 NT;
-  // B(K + 1) at O = 8; LDS-DMA pieces of chunk K + 3 at O = 9..15. (The asm reads and waits are scheduling
+  // B(K + 1) at O = SYNC_O; LDS-DMA pieces of chunk K + 3 after it. (The asm reads and waits are scheduling
   // boundaries: what is placed in an o-step stays beside its MFMAs.)
   template <int LI, bool IN_L1, int Q, int O>
   __device__ __forceinline__ void ostep(x3::lds_cptr base, x3::lds_cptr nbase, const f32x4 (&In)[NT][ST],
@@ -240,8 +248,8 @@ struct KEngine {
         Out[t][O] = mfma16(f[O % (PF + 1)][1], Hh[t], Out[t][O]);
         Out[t][O] = mfma16(f[O % (PF + 1)][0], Hh[t], Out[t][O]);
       }
-      if constexpr (Q + 1 < KQ && O < 4 * NT) {
-        constexpr int t = O / 4, d = O % 4;
+      if constexpr (Q + 1 < KQ && act_pair_at(O) >= 0) {
+        constexpr int P = act_pair_at(O), t = P / 4, d = P % 4;
         const f32x4& z = In[t][2 * Q + 2 + d / 2];
         const int e = 2 * (d % 2);
         const float r0 = IN_L1 ? x3::x3_act_r2(z[e]) : x3::x3_act_r(z[e]);
@@ -257,7 +265,7 @@ struct KEngine {
   }
 
   // the ring's part of o-step O: the fragment pair PF o-steps ahead (across the chunk boundary at the last PF o-steps:
-  // the next chunk's, whose barrier has passed at O = 8), then the wait for this o-step's pair
+  // the next chunk's, whose barrier has passed at O = SYNC_O), then the wait for this o-step's pair
   template <int O>
   __device__ __forceinline__ void ring_pre(x3::lds_cptr base, x3::lds_cptr nbase, u32x4 (&f)[PF + 1][2],
                                            u32x4 (&fpre)[PF][2]) const {
@@ -271,18 +279,34 @@ struct KEngine {
     // PF younger fragment pairs are in flight (an output-fragment read between them only makes it stricter)
     x3::lds_wait2<2 * PF>(f[O % (PF + 1)][0], f[O % (PF + 1)][1]);
   }
-  // B(K + 1) at O = 8; LDS-DMA pieces of chunk K + 3 at O = 9..15
+  // hidden layer 1: the o-step that activates operand pair P (< 4 NT) of the next k-step -- pair P at o-step P, or
+  // (DMIP_X3K_ACT_SPREAD) the 4 NT pairs spread evenly over the 16 o-steps
+  static constexpr int act_ostep(int P) {
+#ifdef DMIP_X3K_ACT_SPREAD
+    return (P * ST) / (4 * NT);
+#else
+    return P;
+#endif
+  }
+  static constexpr int act_pair_at(int O) {
+    for (int P = 0; P < 4 * NT; ++P)
+      if (act_ostep(P) == O) return P;
+    return -1;
+  }
+  // B(K + 1) at O = SYNC_O; the PPW LDS-DMA pieces of chunk K + 3 spread over o-steps SYNC_O + 1 .. 15 (SYNC_O = 8:
+  // two at O = 9, then one per o-step)
+  static constexpr int piece_ostep(int q) { return SYNC_O + 1 + (q * (15 - SYNC_O)) / PPW; }
+  template <int K, int O, int Q = 0>
+  __device__ __forceinline__ void ring_pieces() const {
+    if constexpr (Q < PPW) {
+      if constexpr (piece_ostep(Q) == O) issue_piece<(K + R - 1) % NCHUNK, (K + R - 1) % R, Q>();
+      ring_pieces<K, O, Q + 1>();
+    }
+  }
   template <int K, int O>
   __device__ __forceinline__ void ring_post() const {
-    if constexpr (O == 8) sync_mid<(K + 1) % NCHUNK>();
-    if constexpr (!(DIAG & 1) && PPW == 8 && O == 9) {
-      issue_piece<(K + R - 1) % NCHUNK, (K + R - 1) % R, 0>();
-      issue_piece<(K + R - 1) % NCHUNK, (K + R - 1) % R, 1>();
-    }
-    if constexpr (!(DIAG & 1) && PPW == 8 && O >= 10)
-      issue_piece<(K + R - 1) % NCHUNK, (K + R - 1) % R, O - 8>();
-    if constexpr (!(DIAG & 1) && PPW == 4 && O >= 9 && O < 13)
-      issue_piece<(K + R - 1) % NCHUNK, (K + R - 1) % R, O - 9>();
+    if constexpr (O == SYNC_O) sync_mid<(K + 1) % NCHUNK>();
+    if constexpr (!(DIAG & 1) && O > SYNC_O) ring_pieces<K, O>();
   }
 
   // ---- hidden layer 2 in two output halves (ring chunks 8..11: output tiles 0..7; 12..15: tiles 8..15), each
