@@ -201,6 +201,10 @@ struct XEngine {
 
   // chunks of layer 1 in the stream (L1R): k-step q of every output tile, ST KiB
   static constexpr int NL1C = L1R ? K1Q : 0;
+  // resident weights: at W = 64 one network's whole stream (at most kMaxHidden 16 KiB chunks: the W x W layers and
+  // the output tile) fits the ring, so it is loaded once per launch and every chunk_sync is a plain slot address --
+  // no barrier, no LDS-DMA, no vmcnt wait per chunk (the linear problem's networks, BASELINE configs[0])
+  static constexpr bool RES = W == 64 && NNET == 1 && !L1R && R >= kMaxHidden && (DIAG & 1) == 0;
   static_assert(!L1R || ST * 1024 == CHUNK, "a streamed layer-1 chunk is one k-step of all output tiles");
 
   __device__ __forceinline__ void init(int n_hidden) {
@@ -229,6 +233,11 @@ struct XEngine {
   // the next chunk of the stream, landed (own pieces counted, the others' by the barrier); the slot
   // read one chunk ago is refilled R - 1 chunks ahead
   __device__ __forceinline__ const char* chunk_sync() {
+    if constexpr (RES) {
+      const char* slot = lds + RING_OFF + s_read * CHUNK;
+      s_read = s_read + 1 == ncn ? 0 : s_read + 1;
+      return slot;
+    }
     if constexpr (DIAG & 1) {
       asm volatile("" ::: "memory");
       const char* slot = lds + RING_OFF + s_read * CHUNK;
@@ -248,6 +257,12 @@ struct XEngine {
   }
 
   __device__ __forceinline__ void start() {
+    if constexpr (RES) {  // the whole stream into slots 0 .. ncn - 1, landed and visible before the first step
+      for (int q = 0; q < ncn; ++q) ring_issue();
+      wait_vmcnt<0>();
+      __syncthreads();
+      return;
+    }
     wait_vmcnt<0>();
     __syncthreads();
     for (int q = 0; q < R - 1; ++q) ring_issue();
