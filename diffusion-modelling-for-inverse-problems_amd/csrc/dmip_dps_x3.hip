@@ -58,7 +58,11 @@ struct Eng {
   int c_issue, s_issue, s_read;
   int w, lane, g;
 
-  __device__ __forceinline__ void ring_issue() {
+  // the next refill: its source chunk and ring slot (the stream position advances); its PPW pieces per wave go out at
+  // once (ring_issue) or beside the consuming chunk's MFMAs (Spread, split_product_h)
+  const char* dma_src;
+  char* dma_dst;
+  __device__ __forceinline__ void ring_target() {
     const int c = __builtin_amdgcn_readfirstlane(c_issue);
     const char* src = c < NPF ? pimg + (size_t)c * CHUNK
                               : (c < NPF + NS ? simg + (size_t)(c - NPF) * CHUNK : pimg + (size_t)(c - NS) * CHUNK);
@@ -66,22 +70,52 @@ struct Eng {
     const char* base = (const char*)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(addr >> 32)) << 32) |
                                      (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)addr));
     asm volatile("" : "+s"(base));  // keep the per-chunk address out of the loop-invariant hoist
-    char* dst = lds + RING + __builtin_amdgcn_readfirstlane(s_issue) * CHUNK;
-#pragma unroll
-    for (int q = 0; q < PPW; ++q) {
-      const int piece = w * PPW + q;
-      glds16(base + piece * 1024, dst + piece * 1024, lane);
-    }
+    dma_src = base;
+    dma_dst = lds + RING + __builtin_amdgcn_readfirstlane(s_issue) * CHUNK;
     c_issue = c_issue + 1 == NSTREAM ? 0 : c_issue + 1;
     s_issue = s_issue + 1 == R ? 0 : s_issue + 1;
   }
+  template <int Q>
+  __device__ __forceinline__ void ring_piece() const {
+    const int piece = w * PPW + Q;
+    glds16(dma_src + piece * 1024, dma_dst + piece * 1024, lane);
+  }
+  __device__ __forceinline__ void ring_issue() {
+    ring_target();
+#pragma unroll
+    for (int q = 0; q < PPW; ++q) {
+      const int piece = w * PPW + q;
+      glds16(dma_src + piece * 1024, dma_dst + piece * 1024, lane);
+    }
+  }
+  // the hook of x3::split_product_h: piece Q of the pending refill beside k-step unit (Q NU) / PPW (round 5: a burst
+  // of PPW LDS-DMA instructions at the chunk start held the wave's issue ~100-185 cycles a piece)
+  struct Spread {
+    const Eng* e;
+    template <int U, int NU, int Q = 0>
+    __device__ __forceinline__ void at() const {
+      if constexpr (Q < PPW) {
+        if constexpr ((Q * NU) / PPW == U) e->template ring_piece<Q>();
+        at<U, NU, Q + 1>();
+      }
+    }
+  };
 
   // the next chunk of the stream, landed (own pieces counted, the others' by the barrier); the slot read one
-  // chunk ago is refilled R - 1 chunks ahead
+  // chunk ago is refilled R - 1 chunks ahead -- its pieces issued here (chunk_sync) or by the chunk's MFMAs
+  // (chunk_sync_deferred + Spread: every piece of a refill within the chunk that set it, so the vmcnt count holds)
   __device__ __forceinline__ lds_cptr chunk_sync() {
     wait_vmcnt<(R - 2) * PPW>();
     lds_barrier();
     ring_issue();
+    const char* slot = lds + RING + s_read * CHUNK;
+    s_read = s_read + 1 == R ? 0 : s_read + 1;
+    return (lds_cptr)(slot + lane * 16);
+  }
+  __device__ __forceinline__ lds_cptr chunk_sync_deferred() {
+    wait_vmcnt<(R - 2) * PPW>();
+    lds_barrier();
+    ring_target();
     const char* slot = lds + RING + s_read * CHUNK;
     s_read = s_read + 1 == R ? 0 : s_read + 1;
     return (lds_cptr)(slot + lane * 16);
@@ -205,8 +239,8 @@ __device__ __forceinline__ void layer256(Eng& e, const u32x4 (&Hh)[KQ], const u3
 #pragma unroll
     for (int t = 0; t < CT; ++t) acc[t] = bias_off >= 0 ? e.bias4(bias_off, c * CT + t) : f32x4{0.f, 0.f, 0.f, 0.f};
     x3::lgkm_drain();
-    const lds_cptr ch = e.chunk_sync();
-    x3::split_product<KQ, CT * KQ, 2>(ch, Hh, Hl, acc);
+    const lds_cptr ch = e.chunk_sync_deferred();
+    x3::split_product_h<KQ, CT * KQ, 2>(ch, Hh, Hl, acc, Eng::Spread{&e});
     if (c > 0) {
 #pragma unroll
       for (int t = 0; t < CT; ++t) epi(pend[t], (c - 1) * CT + t, Oh, Ol);
@@ -225,8 +259,8 @@ __device__ __forceinline__ void small256(Eng& e, const u32x4 (&Hh)[KQ], const u3
 #pragma unroll
   for (int t = 0; t < NTL; ++t) acc[t] = bias_off >= 0 ? e.bias4(bias_off, t) : f32x4{0.f, 0.f, 0.f, 0.f};
   x3::lgkm_drain();
-  const lds_cptr ch = e.chunk_sync();
-  x3::split_product<KQ, NTL * KQ, 2>(ch, Hh, Hl, acc);
+  const lds_cptr ch = e.chunk_sync_deferred();
+  x3::split_product_h<KQ, NTL * KQ, 2>(ch, Hh, Hl, acc, Eng::Spread{&e});
 }
 
 // the transposed output layers (16 tiles, one k-step: the output rows): B = the split of the reverse pass's input
@@ -236,11 +270,11 @@ template <typename Epi>
 __device__ __forceinline__ void wide1(Eng& e, const u32x4& Bh, const u32x4& Bl, const Epi& epi, u32x4 (&Oh)[KQ],
                                       u32x4 (&Ol)[KQ]) {
   const u32x4 bh[1] = {Bh}, bl[1] = {Bl};
-  const lds_cptr ch = e.chunk_sync();
+  const lds_cptr ch = e.chunk_sync_deferred();
   f32x4 a0[ST / 2], a1[ST / 2];
 #pragma unroll
   for (int t = 0; t < ST / 2; ++t) a0[t] = a1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  x3::split_product<1, ST / 2, 2>(ch, bh, bl, a0);
+  x3::split_product_h<1, ST / 2, 2>(ch, bh, bl, a0, Eng::Spread{&e});
   x3::split_product<1, ST / 2, 2>(ch + ST * 1024, bh, bl, a1);
 #pragma unroll
   for (int t = 0; t < ST / 2; ++t) epi(a0[t], t, Oh, Ol);

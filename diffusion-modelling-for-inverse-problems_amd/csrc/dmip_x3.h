@@ -65,10 +65,13 @@ constexpr int align16(int v) { return (v + 15) / 16 * 16; }
 // LDS: layer-1 images, biases (per network: layer 1 | hidden layers | output rows 0..15), the
 // observation (CDiffE), the ring. L1R: layer 1 is not resident but streams through the ring ahead of the
 // hidden chunks (CDiffE at width 512: its 27-input split image is 96 KiB).
-template <int W, int NNET, int K1Q, int M, bool L1R = false>
+// L1H: a one-k-step layer 1 over at most 5 inputs (15 k-slots) leaves lane groups 2-3 of its B operand zero, so its
+// resident image holds lanes 0-31 of each tile (512 B) and lanes 32-63 read those finite weights (dmip_x3k.h KLay):
+// half the LDS, which gives the Posterior at W = 512 (two layer-1 images) a third ring slot
+template <int W, int NNET, int K1Q, int M, bool L1R = false, bool L1H = false>
 struct XLay {
   using S = Shape<W>;
-  static constexpr int L1_BYTES = L1R ? 0 : S::ST * K1Q * 1024;
+  static constexpr int L1_BYTES = L1R ? 0 : (L1H ? S::ST * 512 : S::ST * K1Q * 1024);
   static constexpr int BF = kMaxHidden * W + 16;  // bias floats per network
   static constexpr int L1 = 0;
   static constexpr int BIAS = L1 + NNET * L1_BYTES;
@@ -138,6 +141,39 @@ __device__ __forceinline__ void split_chain(lds_cptr base, const u32x4 (&Hh)[KQ]
   }
 }
 
+// split_chain with a hook run beside k-step U's MFMAs (hook.template at<U>(): the ring's LDS-DMA pieces, spread)
+template <int KQ, int NU, int PF, typename Hook, int U = 0>
+__device__ __forceinline__ void split_chain_h(lds_cptr base, const u32x4 (&Hh)[KQ], const u32x4 (&Hl)[KQ],
+                                              f32x4 (&acc)[(NU + KQ - 1) / KQ], u32x4 (&fa)[PF + 1][2],
+                                              const Hook& hook) {
+  if constexpr (U < NU) {
+    if constexpr (U + PF < NU) {
+      fa[(U + PF) % (PF + 1)][0] = lds_rd<(2 * (U + PF)) * 1024>(base);
+      fa[(U + PF) % (PF + 1)][1] = lds_rd<(2 * (U + PF) + 1) * 1024>(base);
+    }
+    lds_wait2<2 * cmin(NU - 1 - U, PF)>(fa[U % (PF + 1)][0], fa[U % (PF + 1)][1]);
+    constexpr int t = U / KQ, q = U % KQ;
+    acc[t] = mfma16(fa[U % (PF + 1)][0], Hl[q], acc[t]);
+    acc[t] = mfma16(fa[U % (PF + 1)][1], Hh[q], acc[t]);
+    acc[t] = mfma16(fa[U % (PF + 1)][0], Hh[q], acc[t]);
+    hook.template at<U, NU>();
+    split_chain_h<KQ, NU, PF, Hook, U + 1>(base, Hh, Hl, acc, fa, hook);
+  }
+}
+
+template <int KQ, int NU, int PF, typename Hook>
+__device__ __forceinline__ void split_product_h(lds_cptr base, const u32x4 (&Hh)[KQ], const u32x4 (&Hl)[KQ],
+                                                f32x4 (&acc)[(NU + KQ - 1) / KQ], const Hook& hook) {
+  u32x4 fa[PF + 1][2];
+#pragma unroll
+  for (int u = 0; u < cmin(PF, NU); ++u) {
+    if (u == 0) fa[0][0] = lds_rd<0>(base), fa[0][1] = lds_rd<1024>(base);
+    if (u == 1) fa[1][0] = lds_rd<2048>(base), fa[1][1] = lds_rd<3072>(base);
+    if (u == 2) fa[2][0] = lds_rd<4096>(base), fa[2][1] = lds_rd<5120>(base);
+  }
+  split_chain_h<KQ, NU, PF, Hook>(base, Hh, Hl, acc, fa, hook);
+}
+
 template <int KQ, int NU, int PF>
 __device__ __forceinline__ void split_product(lds_cptr base, const u32x4 (&Hh)[KQ], const u32x4 (&Hl)[KQ],
                                               f32x4 (&acc)[(NU + KQ - 1) / KQ]) {
@@ -154,14 +190,15 @@ __device__ __forceinline__ void split_product(lds_cptr base, const u32x4 (&Hh)[K
 }
 
 // layer 1: one fragment per k-step (the split lives in the k-slots), NU = n_tiles K1Q k-steps in tile order
-template <int K1Q, int NU, int PF, int F = 0>
+// STR: bytes between consecutive fragments (1024; 512 for a half-size image holding lanes 0-31 only, XLay L1H)
+template <int K1Q, int NU, int PF, int F = 0, int STR = 1024>
 __device__ __forceinline__ void l1_chain(lds_cptr base, const u32x4 (&b1)[K1Q], f32x4 (&acc)[NU / K1Q],
                                          u32x4 (&fa)[PF + 1]) {
   if constexpr (F < NU) {
-    if constexpr (F + PF < NU) fa[(F + PF) % (PF + 1)] = lds_rd<(F + PF) * 1024>(base);
+    if constexpr (F + PF < NU) fa[(F + PF) % (PF + 1)] = lds_rd<(F + PF) * STR>(base);
     lds_wait1<cmin(NU - 1 - F, PF)>(fa[F % (PF + 1)]);
     acc[F / K1Q] = mfma16(fa[F % (PF + 1)], b1[F % K1Q], acc[F / K1Q]);
-    l1_chain<K1Q, NU, PF, F + 1>(base, b1, acc, fa);
+    l1_chain<K1Q, NU, PF, F + 1, STR>(base, b1, acc, fa);
   }
 }
 
@@ -182,7 +219,7 @@ __device__ __forceinline__ float x3_act_r2(float zs) {
 // DIAG (timing ablations only, never on the product path; DMIP_X3_DIAG): bit 0 = no ring (no DMA, no
 // barrier: stale weights), bit 1 = hidden activations replaced by the split alone, bit 2 = the same for
 // layer 1's double tanh
-template <int W, int NNET, int K1Q, int R, int RING_OFF, int DIAG = 0, bool L1R = false>
+template <int W, int NNET, int K1Q, int R, int RING_OFF, int DIAG = 0, bool L1R = false, bool L1H = false>
 struct XEngine {
   using S = Shape<W>;
   static constexpr int ST = S::ST, KQ = S::KQ, CT = S::CT, NCH = S::NCH, NW = S::NW, PPW = S::PPW;
@@ -213,22 +250,56 @@ struct XEngine {
     c_issue = s_issue = s_read = 0;
   }
 
-  __device__ __forceinline__ void ring_issue() {
+  // the refill of the next chunk to issue: its source and ring slot (then the stream position advances); its PPW
+  // pieces per wave go out at once (ring_issue) or spread beside the consuming chunk's MFMAs (SpreadPieces)
+  const char* dma_src;
+  char* dma_dst;
+  __device__ __forceinline__ void ring_target() {
     const int c = __builtin_amdgcn_readfirstlane(c_issue);
     const int n = __builtin_amdgcn_readfirstlane(ncn);
     const uint64_t addr = (uint64_t)((c < n ? img[0] : img[1]) + (size_t)(c < n ? c : c - n) * CHUNK);
     const char* base = (const char*)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(addr >> 32)) << 32) |
                                      (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)addr));
     asm volatile("" : "+s"(base));  // keep the per-chunk address out of the loop-invariant hoist
-    char* dst = lds + RING_OFF + __builtin_amdgcn_readfirstlane(s_issue) * CHUNK;
-#pragma unroll
-    for (int q = 0; q < PPW; ++q) {
-      const int piece = w * PPW + q;
-      glds16(base + piece * 1024, dst + piece * 1024, lane);
-    }
+    dma_src = base;
+    dma_dst = lds + RING_OFF + __builtin_amdgcn_readfirstlane(s_issue) * CHUNK;
     c_issue = c_issue + 1 == NNET * ncn ? 0 : c_issue + 1;
     s_issue = s_issue + 1 == R ? 0 : s_issue + 1;
   }
+  template <int Q>
+  __device__ __forceinline__ void ring_piece() const {
+    const int piece = w * PPW + Q;
+    glds16(dma_src + piece * 1024, dma_dst + piece * 1024, lane);
+  }
+  __device__ __forceinline__ void ring_issue() {
+    ring_target();
+#pragma unroll
+    for (int q = 0; q < PPW; ++q) {
+      const int piece = w * PPW + q;
+      glds16(dma_src + piece * 1024, dma_dst + piece * 1024, lane);
+    }
+  }
+  // the hook of split_product_h: piece Q of the pending refill beside k-step U = (Q NU) / PPW of the chunk
+  struct SpreadPieces {
+    const XEngine* e;
+    template <int U, int NU, int Q = 0>
+    __device__ __forceinline__ void at() const {
+      if constexpr (Q < PPW) {
+        if constexpr ((Q * NU) / PPW == U) e->template ring_piece<Q>();
+        at<U, NU, Q + 1>();
+      }
+    }
+  };
+  // Round 5: a hidden or output chunk's refill pieces are spread over its k-steps (one per NU / PPW MFMA groups)
+  // instead of a burst of PPW LDS-DMA instructions at the chunk start, which held the wave's issue for ~100-185
+  // cycles a piece (MI355X_MICROARCH.md) before the first MFMA. DMIP_X3_BURST_DMA (A/B builds) keeps the burst.
+#ifdef DMIP_X3_BURST_DMA
+  static constexpr bool SPREAD = false;
+#else
+  // (with R = 2 slots -- the Posterior's two layer-1 images at W = 512 -- a refill is consumed by the very next
+  // chunk, and pieces issued late in a chunk would land after it starts: those rings keep the burst)
+  static constexpr bool SPREAD = !RES && (DIAG & 1) == 0 && R >= 3;
+#endif
 
   // the next chunk of the stream, landed (own pieces counted, the others' by the barrier); the slot
   // read one chunk ago is refilled R - 1 chunks ahead
@@ -247,6 +318,17 @@ struct XEngine {
     wait_vmcnt<(R - 2) * PPW>();
     lds_barrier();
     ring_issue();
+    const char* slot = lds + RING_OFF + s_read * CHUNK;
+    s_read = s_read + 1 == R ? 0 : s_read + 1;
+    return slot;
+  }
+  // chunk_sync for a chunk whose MFMAs issue the refill's pieces themselves (split_product_h + SpreadPieces): the
+  // same waits and barrier, the refill's target set but nothing issued yet. The pieces of a refill are all issued
+  // within the chunk that set it, so the vmcnt accounting of chunk_sync holds.
+  __device__ __forceinline__ const char* chunk_sync_deferred() {
+    wait_vmcnt<(R - 2) * PPW>();
+    lds_barrier();
+    ring_target();
     const char* slot = lds + RING_OFF + s_read * CHUNK;
     s_read = s_read + 1 == R ? 0 : s_read + 1;
     return slot;
@@ -300,13 +382,14 @@ struct XEngine {
 #pragma unroll
     for (int o = 0; o < ST; ++o) acc[o] = bias4(ni, 0, o);
     lgkm_drain();
-    const lds_cptr base = (lds_cptr)(lds + l1_off[ni] + lane * 16);
+    constexpr int STR = L1H ? 512 : 1024;
+    const lds_cptr base = (lds_cptr)(lds + l1_off[ni] + (L1H ? (lane & 31) : lane) * 16);
     constexpr int NU = ST * K1Q;
     u32x4 fa[4];
     fa[0] = lds_rd<0>(base);
-    if constexpr (NU > 1) fa[1] = lds_rd<1024>(base);
-    if constexpr (NU > 2) fa[2] = lds_rd<2048>(base);
-    l1_chain<K1Q, NU, 3>(base, b1, acc, fa);
+    if constexpr (NU > 1) fa[1] = lds_rd<STR>(base);
+    if constexpr (NU > 2) fa[2] = lds_rd<2 * STR>(base);
+    l1_chain<K1Q, NU, 3, 0, STR>(base, b1, acc, fa);
 #pragma unroll
     for (int o = 0; o < ST; ++o) act_store<true>(acc[o], o, Oh, Ol);
   }
@@ -356,8 +439,13 @@ struct XEngine {
 #pragma unroll
       for (int t = 0; t < CT; ++t) acc[t] = bias4(ni, li, c * CT + t);
       lgkm_drain();
-      const char* ch = chunk_sync();
-      split_product<KQ, CT * KQ, 2>((lds_cptr)(ch + lane * 16), Hh, Hl, acc);
+      if constexpr (SPREAD) {
+        const char* ch = chunk_sync_deferred();
+        split_product_h<KQ, CT * KQ, 2>((lds_cptr)(ch + lane * 16), Hh, Hl, acc, SpreadPieces{this});
+      } else {
+        const char* ch = chunk_sync();
+        split_product<KQ, CT * KQ, 2>((lds_cptr)(ch + lane * 16), Hh, Hl, acc);
+      }
       // the previous chunk's tiles are activated beside this chunk's MFMAs
       if (c > 0) {
 #pragma unroll
@@ -374,8 +462,13 @@ struct XEngine {
   __device__ __forceinline__ f32x4 output(int ni, const u32x4 (&Hh)[KQ], const u32x4 (&Hl)[KQ]) {
     f32x4 acc[1] = {bias4(ni, nl, 0)};
     lgkm_drain();
-    const char* ch = chunk_sync();
-    split_product<KQ, KQ, 2>((lds_cptr)(ch + lane * 16), Hh, Hl, acc);
+    if constexpr (SPREAD) {
+      const char* ch = chunk_sync_deferred();
+      split_product_h<KQ, KQ, 2>((lds_cptr)(ch + lane * 16), Hh, Hl, acc, SpreadPieces{this});
+    } else {
+      const char* ch = chunk_sync();
+      split_product<KQ, KQ, 2>((lds_cptr)(ch + lane * 16), Hh, Hl, acc);
+    }
     return acc[0];
   }
 
@@ -456,8 +549,9 @@ struct SamplerCfg {
   static constexpr int K1Q = k1q_of(NV);
   // CDiffE's split layer 1 over all inputs streams through the ring when it would not fit resident
   static constexpr bool L1R = MODE == SAMPLER_CDIFFE && Shape<W>::ST * K1Q * 1024 > 48 * 1024;
-  using L = XLay<W, NNET, K1Q, M, L1R>;
-  using E = XEngine<W, NNET, K1Q, L::R, L::RING, DIAG, L1R>;
+  static constexpr bool L1H = !L1R && K1Q == 1 && 3 * NV <= 16;
+  using L = XLay<W, NNET, K1Q, M, L1R, L1H>;
+  using E = XEngine<W, NNET, K1Q, L::R, L::RING, DIAG, L1R, L1H>;
 };
 
 template <int MODE, int W, int D, int M, bool NOISE, int DIAG = 0>
@@ -480,7 +574,13 @@ __global__ void __launch_bounds__(Shape<W>::NW * 64, Shape<W>::NW / 4) x3_sample
   {
     const int bf = p.n_hidden * W + 16;
     for (int ni = 0; ni < C::NNET; ++ni) {
-      eng.stage(lds + L::L1 + ni * L::L1_BYTES, p.net[ni].l1, L::L1_BYTES);
+      if constexpr (C::L1H) {  // lanes 0-31 of each tile's 1 KiB ([tile][64 lanes][16 B] -> [tile][32][16 B])
+        const uint4* s1 = (const uint4*)p.net[ni].l1;
+        uint4* d1 = (uint4*)(lds + L::L1 + ni * L::L1_BYTES);
+        for (int e = threadIdx.x; e < L::L1_BYTES / 16; e += NW * 64) d1[e] = s1[(e >> 5) * 64 + (e & 31)];
+      } else {
+        eng.stage(lds + L::L1 + ni * L::L1_BYTES, p.net[ni].l1, L::L1_BYTES);
+      }
       float* bl = (float*)(lds + L::BIAS + ni * L::BIAS_BYTES);
       // CDE / likelihood: layer 1's bias is the per-y c (b1 + W1_y y) (x3_bias_prep_kernel)
       const bool per_y = ni == 0 && MODE != SAMPLER_CDIFFE;
