@@ -1,0 +1,17 @@
+#!/bin/bash
+# the one-tile fp32x3 engine's mid-chunk barrier (MID): its tests, then a same-box A/B of its bench rows against the
+# spread-only build (abv/spread_only)
+set -u
+OUT=gpurun_out/${1:-r5m}
+mkdir -p "$OUT"
+export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
+timeout -k 10 600 python -u -m pytest tests/test_gpu_x3.py tests/test_gpu_parity.py tests/test_gpu_drivers.py -m gpu -q --timeout 300 \
+  --timeout-method thread -p no:cacheprovider -rf > "$OUT/pytest.log" 2>&1
+rc=$?; echo "pytest rc=$rc"; grep -E "FAILED|passed|failed" "$OUT/pytest.log" | tail -6
+case $rc in 0|1) ;; *) exit 3 ;; esac
+for r in 1 2; do
+  timeout -k 10 300 python -u scripts/bench_x3_rows.py > "$OUT/new_$r.json" 2>/dev/null || exit 3
+  echo "new    $(cat $OUT/new_$r.json)"
+  DMIP_LIB=abv/spread_only/libdmip.so DMIP_LIB_AB=1 timeout -k 10 300 python -u scripts/bench_x3_rows.py > "$OUT/spread_$r.json" 2>/dev/null || exit 3
+  echo "spread $(cat $OUT/spread_$r.json)"
+done
