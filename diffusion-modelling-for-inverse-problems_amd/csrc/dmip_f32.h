@@ -92,8 +92,28 @@ struct FEngine {
     c_issue = s_issue = s_read = 0;
   }
 
-  __device__ __forceinline__ void ring_issue() {
+  // the next refill's source and ring slot (the stream position advances); its PPW pieces per wave go out at once
+  // (ring_issue) or beside the consuming tile's MFMAs (round 5, as the fp32x3 engine: SPREAD)
+  const char* dma_src;
+  char* dma_dst;
+  __device__ __forceinline__ void ring_target() {
     // wave-uniform by construction; say so (the divergence analysis cannot see it through the loops)
+    const int c = __builtin_amdgcn_readfirstlane(c_issue);
+    const int n = __builtin_amdgcn_readfirstlane(ncn);
+    const uint64_t addr = (uint64_t)((c < n ? img[0] : img[1]) + (size_t)(c < n ? c : c - n) * CHUNK);
+    const char* base = (const char*)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(addr >> 32)) << 32) |
+                                     (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)addr));
+    asm volatile("" : "+s"(base));  // keep the per-chunk address out of the loop-invariant hoist
+    dma_src = base;
+    dma_dst = lds + RING_OFF + __builtin_amdgcn_readfirstlane(s_issue) * CHUNK;
+    c_issue = c_issue + 1 == NNET * ncn ? 0 : c_issue + 1;
+    s_issue = s_issue + 1 == R ? 0 : s_issue + 1;
+  }
+  __device__ __forceinline__ void ring_piece(int q) const {
+    const int piece = w * PPW + q;
+    glds16(dma_src + piece * 1024, dma_dst + piece * 1024, lane);
+  }
+  __device__ __forceinline__ void ring_issue() {  // (locals, not the members: at W = 512 that spilled less)
     const int c = __builtin_amdgcn_readfirstlane(c_issue);
     const int n = __builtin_amdgcn_readfirstlane(ncn);
     const uint64_t addr = (uint64_t)((c < n ? img[0] : img[1]) + (size_t)(c < n ? c : c - n) * CHUNK);
@@ -109,13 +129,20 @@ struct FEngine {
     c_issue = c_issue + 1 == NNET * ncn ? 0 : c_issue + 1;
     s_issue = s_issue + 1 == R ? 0 : s_issue + 1;
   }
+#ifdef DMIP_X3_BURST_DMA
+  static constexpr bool SPREAD = false;
+#else
+  // (the refill 2 chunks ahead; at W = 512 the f32 kernels are register-bound and the live refill state spilled)
+  static constexpr bool SPREAD = R >= 3 && PPW <= ST && W <= 256;
+#endif
 
   // the next chunk of the stream, landed (own pieces counted, the others' by the barrier); the
   // slot read one chunk ago is refilled R - 1 chunks ahead
   __device__ __forceinline__ const char* chunk_sync() {
     wait_vmcnt<(R - 2) * PPW>();
     lds_barrier();
-    ring_issue();
+    if constexpr (SPREAD) ring_target();  // pieces issued by tile_product, all within this chunk
+    else ring_issue();
     const char* slot = lds + RING_OFF + s_read * CHUNK;
     s_read = s_read + 1 == R ? 0 : s_read + 1;
     return slot;
@@ -140,10 +167,16 @@ struct FEngine {
 
   // acc(tile) = sum over the W inputs of a streamed chunk: two accumulation chains (even / odd
   // k-groups), the MFMA's 40-cycle dependent latency against its 32-cycle issue
+  // (SPREAD: the pending refill's piece p issued beside k-group (p ST) / PPW)
   __device__ __forceinline__ f32x4 tile_product(const char* ch, const float (&H)[ST][4], f32x4 acc0) const {
     f32x4 acc1 = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
     for (int q = 0; q < ST; ++q) {
+      if constexpr (SPREAD) {
+#pragma unroll
+        for (int p = 0; p < PPW; ++p)
+          if ((p * ST) / PPW == q) ring_piece(p);
+      }
       const f32x4 a = *(const f32x4*)(ch + (q * 64 + lane) * 16);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {

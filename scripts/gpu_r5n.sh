@@ -1,0 +1,16 @@
+#!/bin/bash
+# spread LDS-DMA pieces in the exact-f32 engine (W <= 256): its tests, then a same-box A/B against abv/burst
+set -u
+OUT=gpurun_out/${1:-r5n}
+mkdir -p "$OUT"
+export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
+timeout -k 10 600 python -u -m pytest tests/test_gpu_f32.py tests/test_gpu_silu.py -m gpu -q --timeout 300 \
+  --timeout-method thread -p no:cacheprovider -rf > "$OUT/pytest.log" 2>&1
+rc=$?; echo "pytest rc=$rc"; grep -E "FAILED|passed|failed" "$OUT/pytest.log" | tail -6
+case $rc in 0|1) ;; *) exit 3 ;; esac
+for r in 1 2; do
+  timeout -k 10 300 python -u scripts/bench_f32_rows.py > "$OUT/new_$r.json" 2>/dev/null || exit 3
+  echo "new   $(cat $OUT/new_$r.json)"
+  DMIP_LIB=abv/burst/libdmip.so DMIP_LIB_AB=1 timeout -k 10 300 python -u scripts/bench_f32_rows.py > "$OUT/burst_$r.json" 2>/dev/null || exit 3
+  echo "burst $(cat $OUT/burst_$r.json)"
+done
