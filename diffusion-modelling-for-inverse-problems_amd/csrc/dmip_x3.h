@@ -611,6 +611,12 @@ __global__ void __launch_bounds__(Shape<W>::NW * 64, Shape<W>::NW / 4) x3_sample
     const bool valid = sg.job >= 0 && c_local < p.n_chains;
     const long long c_rd = valid ? c_local : 0;
     const bool live = sg.kind != 3 && valid;  // a chain whose result is kept (idle segments and padded lanes are not)
+    // the chain index again where it is needed after the step loop or per snapshot, from the wave-uniform job and the
+    // lane id (v_mbcnt), so that no per-lane index stays live across the loop (at W = 512 it was spilled to scratch)
+    auto chain_now = [&]() __attribute__((always_inline)) {
+      const int jl = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) & 15;
+      return (long long)(sg.job >= 0 ? sg.job : 0) * 16 + jl;
+    };
     Rng rng;
     float x[D];
     if (sg.kind == 2) {  // resume the tile the previous wave of the grid handed over
@@ -705,8 +711,11 @@ __global__ void __launch_bounds__(Shape<W>::NW * 64, Shape<W>::NW / 4) x3_sample
         const float ak = MODE == SAMPLER_POSTERIOR ? __fmul_rn(cf.g, a[k]) : a[k];
         x[k] = em_update(x[k], ak, xi[k], cf, p.delta, p.sqrt_delta);
       }
-      snap.at_step<D>(i0, p.snap_every, p.snap_out, gridDim.y, yi, p.n_chains, c_local,
-                      sg.kind != 3 && valid && g == 0, x);
+      {
+        const long long cn = chain_now();
+        snap.at_step<D>(i0, p.snap_every, p.snap_out, gridDim.y, yi, p.n_chains, cn,
+                        sg.kind != 3 && sg.job >= 0 && cn < p.n_chains && g == 0, x);
+      }
     }
     if (sg.kind == 1) {  // hand the tile over to the next wave of the grid
       const size_t slot = (size_t)yi * n_waves + gw;
@@ -718,8 +727,8 @@ __global__ void __launch_bounds__(Shape<W>::NW * 64, Shape<W>::NW / 4) x3_sample
       dst[(D + 2) * 64 + lane] = __uint_as_float(rng.s2);
       dst[(D + 3) * 64 + lane] = __uint_as_float(rng.s3);
       handover_publish(p.xflag + slot, lane, p.debug_flags);
-    } else if (sg.kind != 3 && valid && g == 0) {
-      float* dst = p.x_out + ((size_t)yi * p.n_chains + c_local) * D;
+    } else if (const long long cn = chain_now(); sg.kind != 3 && sg.job >= 0 && cn < p.n_chains && g == 0) {
+      float* dst = p.x_out + ((size_t)yi * p.n_chains + cn) * D;
 #pragma unroll
       for (int k = 0; k < D; ++k) dst[k] = x[k];
     }
