@@ -124,7 +124,81 @@ struct Eng {
   __device__ __forceinline__ f32x4 bias4(int off_bytes, int tile) const {
     return *(const f32x4*)(lds + off_bytes + (16 * tile + 4 * g) * 4);
   }
+
+  // MID (round 5; dmip_x3k.h's ring protocol): chunk c + 1's barrier B(c + 1) in the MIDDLE of chunk c (after unit
+  // NU / 2), then the refill of chunk c - 1's slot spread over the rest of chunk c, and chunk c + 1's first fragment
+  // pair read ahead at the last unit (nxt). At one wave per SIMD a wave reaching the barrier early waits while its
+  // MFMAs are still in the pipe, and no chunk starts with an LDS-latency bubble. R = 4: a refill issued in chunk c
+  // lands by B(c + 2)'s wait, one and a half chunks later.
+  u32x4 nxt0, nxt1;
+  __device__ __forceinline__ void start_mid() {
+    for (int q = 0; q < R - 1; ++q) ring_issue();
+    wait_vmcnt<(R - 2) * PPW>();
+    lds_barrier();
+    const lds_cptr b0 = (lds_cptr)(lds + RING + lane * 16);
+    nxt0 = x3::lds_rd<0>(b0);
+    nxt1 = x3::lds_rd<1024>(b0);
+    x3::lds_wait2<0>(nxt0, nxt1);
+  }
+  // the current chunk's lane base, the ring advanced: the next chunk's lane base in nb
+  __device__ __forceinline__ lds_cptr take(lds_cptr& nb) {
+    const lds_cptr b = (lds_cptr)(lds + RING + s_read * CHUNK + lane * 16);
+    s_read = s_read + 1 == R ? 0 : s_read + 1;
+    nb = (lds_cptr)(lds + RING + s_read * CHUNK + lane * 16);
+    return b;
+  }
 };
+static_assert(R == 4, "MID's vmcnt accounting: one younger refill in flight at B(c + 1)");
+template <int NU, int U, int Q = 0>
+__device__ __forceinline__ void mid_pieces(const Eng& e);
+
+// units U0 .. U1 - 1 of a chunk of NU k-step units (unit u: hi / lo fragments at 2u, 2u + 1 KiB), accumulator of unit
+// U = acc[(U - U0) / KQ_], B operand (Hh, Hl)[U % KQ_]; fa[U % 2] holds unit U's pair on entry (unit 0: nxt)
+template <int KQ_, int NU, int U0, int U1, int NA, int U = U0>
+__device__ __forceinline__ void mid_units(Eng& e, lds_cptr base, lds_cptr nbase, const u32x4 (&Hh)[KQ_],
+                                          const u32x4 (&Hl)[KQ_], f32x4 (&acc)[NA], u32x4 (&fa)[2][2]) {
+  if constexpr (U < U1) {
+    constexpr int MIDU = NU / 2;
+    static_assert(MIDU < NU - 1, "the barrier precedes the read-ahead");
+    if constexpr (U + 1 < NU) {
+      fa[(U + 1) % 2][0] = x3::lds_rd<(2 * (U + 1)) * 1024>(base);
+      fa[(U + 1) % 2][1] = x3::lds_rd<(2 * (U + 1) + 1) * 1024>(base);
+    } else {  // after B(c + 1): the next chunk has landed for every wave
+      e.nxt0 = x3::lds_rd<0>(nbase);
+      e.nxt1 = x3::lds_rd<1024>(nbase);
+    }
+    x3::lds_wait2<2>(fa[U % 2][0], fa[U % 2][1]);
+    constexpr int t = (U - U0) / KQ_, q = U % KQ_;
+    acc[t] = mfma16(fa[U % 2][0], Hl[q], acc[t]);
+    acc[t] = mfma16(fa[U % 2][1], Hh[q], acc[t]);
+    acc[t] = mfma16(fa[U % 2][0], Hh[q], acc[t]);
+    if constexpr (U == MIDU) {  // own pieces of chunk c + 1 landed (chunk c + 2's younger), then everyone's
+      wait_vmcnt<PPW>();
+      lds_barrier();
+      e.ring_target();  // chunk c - 1's slot: every wave has passed its last read
+    }
+    if constexpr (U > MIDU) mid_pieces<NU, U>(e);
+    mid_units<KQ_, NU, U0, U1, NA, U + 1>(e, base, nbase, Hh, Hl, acc, fa);
+  }
+}
+template <int NU, int U, int Q>
+__device__ __forceinline__ void mid_pieces(const Eng& e) {
+  if constexpr (Q < PPW) {
+    constexpr int MIDU = NU / 2;
+    if constexpr (MIDU + 1 + (Q * (NU - 1 - MIDU)) / PPW == U) e.template ring_piece<Q>();
+    mid_pieces<NU, U, Q + 1>(e);
+  }
+}
+// a whole chunk of NU units
+template <int KQ_, int NU, int NA>
+__device__ __forceinline__ void mid_chunk(Eng& e, const u32x4 (&Hh)[KQ_], const u32x4 (&Hl)[KQ_], f32x4 (&acc)[NA]) {
+  lds_cptr nb;
+  const lds_cptr b = e.take(nb);
+  u32x4 fa[2][2];
+  fa[0][0] = e.nxt0, fa[0][1] = e.nxt1;
+  mid_units<KQ_, NU, 0, NU, NA>(e, b, nb, Hh, Hl, acc, fa);
+  x3::lds_wait2<0>(e.nxt0, e.nxt1);  // an asm load's registers must not leave the chunk before its data lands
+}
 
 // (hi, lo) B operand of k-step q from two accumulator-form tiles' f32 values v[2 q], v[2 q + 1] (dmip_x3.h
 // act_store's dword order)
@@ -238,9 +312,7 @@ __device__ __forceinline__ void layer256(Eng& e, const u32x4 (&Hh)[KQ], const u3
     f32x4 acc[CT];
 #pragma unroll
     for (int t = 0; t < CT; ++t) acc[t] = bias_off >= 0 ? e.bias4(bias_off, c * CT + t) : f32x4{0.f, 0.f, 0.f, 0.f};
-    x3::lgkm_drain();
-    const lds_cptr ch = e.chunk_sync_deferred();
-    x3::split_product_h<KQ, CT * KQ, 2>(ch, Hh, Hl, acc, Eng::Spread{&e});
+    mid_chunk<KQ, CT * KQ>(e, Hh, Hl, acc);
     if (c > 0) {
 #pragma unroll
       for (int t = 0; t < CT; ++t) epi(pend[t], (c - 1) * CT + t, Oh, Ol);
@@ -258,9 +330,7 @@ __device__ __forceinline__ void small256(Eng& e, const u32x4 (&Hh)[KQ], const u3
                                          f32x4 (&acc)[NTL]) {
 #pragma unroll
   for (int t = 0; t < NTL; ++t) acc[t] = bias_off >= 0 ? e.bias4(bias_off, t) : f32x4{0.f, 0.f, 0.f, 0.f};
-  x3::lgkm_drain();
-  const lds_cptr ch = e.chunk_sync_deferred();
-  x3::split_product_h<KQ, NTL * KQ, 2>(ch, Hh, Hl, acc, Eng::Spread{&e});
+  mid_chunk<KQ, NTL * KQ>(e, Hh, Hl, acc);
 }
 
 // the transposed output layers (16 tiles, one k-step: the output rows): B = the split of the reverse pass's input
@@ -270,12 +340,18 @@ template <typename Epi>
 __device__ __forceinline__ void wide1(Eng& e, const u32x4& Bh, const u32x4& Bl, const Epi& epi, u32x4 (&Oh)[KQ],
                                       u32x4 (&Ol)[KQ]) {
   const u32x4 bh[1] = {Bh}, bl[1] = {Bl};
-  const lds_cptr ch = e.chunk_sync_deferred();
   f32x4 a0[ST / 2], a1[ST / 2];
 #pragma unroll
   for (int t = 0; t < ST / 2; ++t) a0[t] = a1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  x3::split_product_h<1, ST / 2, 2>(ch, bh, bl, a0, Eng::Spread{&e});
-  x3::split_product<1, ST / 2, 2>(ch + ST * 1024, bh, bl, a1);
+  {  // one chunk of ST units (one k-step per tile), in two halves of accumulators
+    lds_cptr nb;
+    const lds_cptr b = e.take(nb);
+    u32x4 fa[2][2];
+    fa[0][0] = e.nxt0, fa[0][1] = e.nxt1;
+    mid_units<1, ST, 0, ST / 2, ST / 2>(e, b, nb, bh, bl, a0, fa);
+    mid_units<1, ST, ST / 2, ST, ST / 2>(e, b, nb, bh, bl, a1, fa);
+    x3::lds_wait2<0>(e.nxt0, e.nxt1);
+  }
 #pragma unroll
   for (int t = 0; t < ST / 2; ++t) epi(a0[t], t, Oh, Ol);
 #pragma unroll
@@ -363,7 +439,7 @@ __global__ void __launch_bounds__(NW * 64, 1) dps_x3_kernel(DpsX3Params p) {
     float* yo = (float*)(lds + YO);
     for (int i = threadIdx.x; i < 32; i += NW * 64) yo[i] = i < kSurYdim ? p.y[(size_t)yi * kSurYdim + i] : 0.0f;
     __syncthreads();
-    for (int q = 0; q < R - 1; ++q) e.ring_issue();
+    e.start_mid();
   }
   const float* ylds = (const float*)(lds + YO);
 
