@@ -24,7 +24,7 @@ DMIP_PREC_FP16, DMIP_PREC_F32, DMIP_PREC_F32X3 = 0, 1, 2
 DMIP_PREC_BF16 = DMIP_PREC_FP16
 PRECISIONS = {"fp16": DMIP_PREC_FP16, "bf16": DMIP_PREC_BF16, "fp32": DMIP_PREC_F32, "fp32x3": DMIP_PREC_F32X3}
 DMIP_SAMPLER_CDE, DMIP_SAMPLER_POSTERIOR, DMIP_SAMPLER_CDIFFE = 0, 1, 2
-ABI_VERSION = 8
+ABI_VERSION = 9
 DMIP_LOSS_DSM, DMIP_LOSS_DSM_PDE, DMIP_LOSS_PINN, DMIP_LOSS_PINN2 = 0, 1, 2, 3
 DMIP_PDE_NONE, DMIP_PDE_FPE, DMIP_PDE_CFPE = 0, 1, 2
 DMIP_METRIC_L1, DMIP_METRIC_L2 = 0, 1
@@ -39,7 +39,7 @@ EXPORTED = (
     "dmip_sampler_supported_f32", "dmip_posterior_loss_grad", "dmip_loss_grad_f32", "dmip_train_draws",
     "dmip_adam_step", "dmip_em_sample_snapshots", "dmip_train_plan_create", "dmip_train_plan_step",
     "dmip_train_plan_set_counters", "dmip_train_plan_destroy", "dmip_sampler_supported_precision",
-    "dmip_dps_sample_ex",
+    "dmip_dps_sample_ex", "dmip_mh_sample_ex",
 )
 DMIP_DPS_NLL, DMIP_DPS_NORM = 0, 1
 
@@ -154,6 +154,11 @@ def _declare(lib):
                                        _c_void_p, _i32, _i64, _i64, _i32, _f32, _f32, _u64, _i32, _f32, _i32,
                                        _c_void_p, _c_void_p]
     lib.dmip_dps_sample_ex.restype = _i32
+    if hasattr(lib, "dmip_mh_sample_ex"):  # ABI >= 9
+        lib.dmip_mh_sample_ex.argtypes = [_c_void_p, ctypes.POINTER(DmipScatNoise), _c_void_p, _i32, _i64, _i64, _i32,
+                                          _f32, _u64, _c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p,
+                                          _c_void_p]
+        lib.dmip_mh_sample_ex.restype = _i32
     for name in ("dmip_train_draws", "dmip_adam_step", "dmip_loss_grad_f32", "dmip_posterior_loss_grad", "dmip_device_status", "dmip_sampler_supported_f32", "dmip_dps_sample", "dmip_mlp_create", "dmip_mlp_destroy", "dmip_mlp_forward", "dmip_em_sample",
                  "dmip_rng_words", "dmip_rng_normals", "dmip_schedule", "dmip_sampler_supported",
                  "dmip_em_sample_stamps", "dmip_em_sample_posterior", "dmip_em_sample_cdiffe",
@@ -442,12 +447,14 @@ def log_posterior(handle, noise, x, y, y_stride, e_out, grad_out=None):
 
 
 def mh_sample(handle, noise, y, n_chains, chain_offset, num_steps, noise_std, seed, x_out, x_init=None,
-              inj_noise=None, inj_unif=None, e_out=None):
+              inj_noise=None, inj_unif=None, e_out=None, precision="fp32"):
+    """dmip_mh_sample_ex: "fp32" the exact-f32 kernel, "fp32x3" the split-fp16 one (dmip_dps_x3.hip mh_x3_kernel)."""
     calls["mh_sample"] = calls.get("mh_sample", 0) + 1
-    check(lib().dmip_mh_sample(handle.h, ctypes.byref(noise), ptr(y), int(y.shape[0]), int(n_chains),
-                               int(chain_offset), int(num_steps), float(noise_std),
-                               ctypes.c_uint64(int(seed) & 0xFFFFFFFFFFFFFFFF), ptr(x_init), ptr(inj_noise),
-                               ptr(inj_unif), ptr(x_out), ptr(e_out), stream_of(y.device)))
+    check(lib().dmip_mh_sample_ex(handle.h, ctypes.byref(noise), ptr(y), int(y.shape[0]), int(n_chains),
+                                  int(chain_offset), int(num_steps), float(noise_std),
+                                  ctypes.c_uint64(int(seed) & 0xFFFFFFFFFFFFFFFF), ptr(x_init), ptr(inj_noise),
+                                  ptr(inj_unif), precision_code(precision), ptr(x_out), ptr(e_out),
+                                  stream_of(y.device)))
 
 
 def dps_sample(prior, surrogate, noise, sde, y, n_chains, chain_offset, num_steps, mean, std, seed, mode, zeta, out,

@@ -2018,6 +2018,50 @@ int dmip_mh_sample(const dmip_surrogate* s, const dmip_scat_noise* noise, const 
   return e == hipSuccess ? DMIP_OK : hip_fail(e, "mh_sample launch");
 }
 
+int dmip_mh_sample_ex(const dmip_surrogate* s, const dmip_scat_noise* noise, const float* y_dev, int n_y,
+                      int64_t n_chains, int64_t chain_offset, int num_steps, float noise_std, uint64_t seed,
+                      const float* x_init_dev, const float* noise_dev, const float* unif_dev, int precision,
+                      float* x_out_dev, float* e_out_dev, void* stream) {
+  if (precision == DMIP_PREC_F32)
+    return dmip_mh_sample(s, noise, y_dev, n_y, n_chains, chain_offset, num_steps, noise_std, seed, x_init_dev,
+                          noise_dev, unif_dev, x_out_dev, e_out_dev, stream);
+  if (precision != DMIP_PREC_F32X3) return fail(DMIP_ERR_INVALID, "MH precision: DMIP_PREC_F32 or DMIP_PREC_F32X3");
+  if (int rc = surrogate_check(s, n_chains)) return rc;
+  dmip::SurrogateParams sp{};
+  if (int rc = noise_check(noise, sp)) return rc;
+  if (!y_dev || !x_out_dev) return fail(DMIP_ERR_INVALID, "null argument");
+  if (n_y < 1 || n_y > 65535) return fail(DMIP_ERR_INVALID, "n_y must be in [1, 65535]");
+  if (chain_offset < 0) return fail(DMIP_ERR_INVALID, "negative chain offset");
+  if (num_steps < 0) return fail(DMIP_ERR_INVALID, "num_steps must be >= 0");
+  if (!(noise_std >= 0.0f)) return fail(DMIP_ERR_INVALID, "noise_std must be >= 0");
+  if (noise_dev || unif_dev) return fail(DMIP_ERR_UNSUPPORTED, "fp32x3 MH: injected draws need DMIP_PREC_F32");
+  if (!s->x3_img)
+    return fail(DMIP_ERR_UNSUPPORTED, "fp32x3 MH: a weight is outside the fp16 range of the split engine (largest |w| " +
+                                          std::to_string(s->x3_range) + " > 65504); use DMIP_PREC_F32");
+  if (n_chains == 0) return DMIP_OK;
+  hipStream_t st = (hipStream_t)stream;
+  dmip::MhX3Params p{};
+  p.simg = s->x3_img;
+  p.sl1 = s->x3_l1;
+  p.sbias = s->x3_bias;
+  p.y = y_dev;
+  p.n_chains = n_chains;
+  p.chain_offset = chain_offset;
+  p.num_steps = num_steps;
+  p.noise_std = noise_std;
+  p.a = sp.a;
+  p.b2 = sp.b2;
+  p.lam = sp.lam;
+  p.seed = seed;
+  p.x_init = x_init_dev;
+  p.x_out = x_out_dev;
+  p.e_out = e_out_dev;
+  p.err = status_word(dmip::stream_device(st));
+  if (!p.err) return fail(DMIP_ERR_ALLOC, "device status word");
+  hipError_t e = dmip::launch_mh_x3(p, n_y, st);
+  return e == hipSuccess ? DMIP_OK : hip_fail(e, "mh_sample (fp32x3) launch");
+}
+
 int dmip_dps_sample(const dmip_mlp* prior, const dmip_surrogate* fwd, const dmip_scat_noise* noise,
                     const dmip_vpsde* sde, const float* y_dev, int n_y, int64_t n_chains, int64_t chain_offset,
                     int num_steps, float mean, float stdv, uint64_t seed, int mode, float zeta, float* x_out_dev,

@@ -57,6 +57,10 @@ struct Eng {
   const char* simg;
   int c_issue, s_issue, s_read;
   int w, lane, g;
+  // the per-step chunk stream: chunks [0, na) of image a, then [0, nb) of image b, then image a's chunks [na, ...)
+  // up to nstream (DPS: a = the prior's 17 forward chunks, b = the surrogate's 35, then the prior's 18 reverse
+  // chunks; MH: the surrogate's 17 forward chunks alone, na = nstream = 17, nb = 0)
+  int na = NPF, nb = NS, nstream = NSTREAM;
 
   // the next refill: its source chunk and ring slot (the stream position advances); its PPW pieces per wave go out at
   // once (ring_issue) or beside the consuming chunk's MFMAs (Spread, split_product_h)
@@ -64,15 +68,16 @@ struct Eng {
   char* dma_dst;
   __device__ __forceinline__ void ring_target() {
     const int c = __builtin_amdgcn_readfirstlane(c_issue);
-    const char* src = c < NPF ? pimg + (size_t)c * CHUNK
-                              : (c < NPF + NS ? simg + (size_t)(c - NPF) * CHUNK : pimg + (size_t)(c - NS) * CHUNK);
+    const int a = __builtin_amdgcn_readfirstlane(na), b = __builtin_amdgcn_readfirstlane(nb);
+    const char* src = c < a ? pimg + (size_t)c * CHUNK
+                            : (c < a + b ? simg + (size_t)(c - a) * CHUNK : pimg + (size_t)(c - b) * CHUNK);
     const uint64_t addr = (uint64_t)src;
     const char* base = (const char*)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(addr >> 32)) << 32) |
                                      (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)addr));
     asm volatile("" : "+s"(base));  // keep the per-chunk address out of the loop-invariant hoist
     dma_src = base;
     dma_dst = lds + RING + __builtin_amdgcn_readfirstlane(s_issue) * CHUNK;
-    c_issue = c_issue + 1 == NSTREAM ? 0 : c_issue + 1;
+    c_issue = c_issue + 1 == nstream ? 0 : c_issue + 1;
     s_issue = s_issue + 1 == R ? 0 : s_issue + 1;
   }
   template <int Q>
@@ -610,6 +615,124 @@ __global__ void __launch_bounds__(NW * 64, 1) dps_x3_kernel(DpsX3Params p) {
   }
 }
 
+// ---------------------------------------------------------------------------- fp32x3 Metropolis-Hastings
+// The fused random-walk MH of dmip_surrogate.hip mh_kernel (generate_scatterometry_ground_truth.py:26-28, 59-62 with
+// anneal_to_energy, models/SNF.py:250-275) with the surrogate's three streamed layers as three-term fp16 splits: the
+// forward half of the DPS kernel's surrogate pass (layer 1 resident, S2 | S3 | Sout streamed, 17 chunks per step,
+// the mid-chunk ring protocol). Same RNG consumption per chain (x0 ~ U[-1, 1]^3 unless given, then per step 3
+// proposal normals and one acceptance uniform), same energy function and acceptance test; four waves of 16 chains.
+
+// get_log_posterior's energy of one chain (dmip_surrogate.hip energy, the same operations): 0.5 sum log pref +
+// 0.5 sum (y - f)^2 / pref + lam sum of the box violations, pref = (a f)^2 + b^2
+__device__ __forceinline__ float mh_energy(const f32x4 (&f)[2], const float* y, const float (&x)[3], float a,
+                                           float b2, float lam, int g) {
+  float slog = 0.0f, ssq = 0.0f;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 16 * t + 4 * g + r;
+      if (row < kSurYdim) {
+        const float fk = f[t][r];
+        const float af = a * fk;
+        const float pref = af * af + b2;
+        const float res = y[row] - fk;
+        slog += logf(pref);
+        ssq += res * res / pref;
+      }
+    }
+  slog += __shfl_xor(slog, 16, 64);
+  slog += __shfl_xor(slog, 32, 64);
+  ssq += __shfl_xor(ssq, 16, 64);
+  ssq += __shfl_xor(ssq, 32, 64);
+  float bd = 0.0f;
+#pragma unroll
+  for (int d = 0; d < 3; ++d) bd += fmaxf(x[d] - 1.0f, 0.0f) + fmaxf(-1.0f - x[d], 0.0f);
+  return 0.5f * slog + 0.5f * ssq + lam * bd;
+}
+
+// the surrogate's forward pass at x (every lane of the chain holds x): output rows f (tiles 0, 1), range flag
+__device__ __forceinline__ void sur_forward(Eng& e, const float (&x)[3], int g, bool& oor, f32x4 (&f)[2]) {
+  u32x4 Ah[KQ], Al[KQ], Bh[KQ], Bl[KQ];
+  uint32_t m2[2] = {0u, 0u}, m3[2] = {0u, 0u};
+  layer1(e, SL1, SB, l1_b<3>(x, g), [&](const f32x4& z, int o) {
+    float h[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      h[k] = z[k] > 0.0f ? z[k] : 0.0f;
+      oor |= beyond_fp16(h[k]);
+    }
+    store_pair(h, o, Ah, Al);
+  });
+  layer256(e, Ah, Al, SB + W * 4, EpiSurFwd{m2, &oor}, Bh, Bl);
+  layer256(e, Bh, Bl, SB + 2 * W * 4, EpiSurFwd{m3, &oor}, Ah, Al);
+  small256<2>(e, Ah, Al, SB + 3 * W * 4, f);
+}
+
+__global__ void __launch_bounds__(NW * 64, 1) mh_x3_kernel(MhX3Params p) {
+  __shared__ __attribute__((aligned(16))) char lds[TOTAL];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, j = lane & 15;
+  const int yi = blockIdx.y;
+  const long long c_local = (long long)blockIdx.x * (NW * 16) + w * 16 + j;
+  const bool valid = c_local < p.n_chains;
+  const long long cc = valid ? c_local : 0;
+  Eng e{lds, p.simg, p.simg, 0, 0, 0, w, lane, g};
+  e.na = kDpsX3SurFwdChunks, e.nb = 0, e.nstream = kDpsX3SurFwdChunks;
+  {
+    const uint4* s2 = (const uint4*)p.sl1;
+    uint4* d2 = (uint4*)(lds + SL1);
+    for (int i = threadIdx.x; i < ST * 32; i += NW * 64) d2[i] = s2[(i >> 5) * 64 + (i & 31)];
+    float* sb = (float*)(lds + SB);
+    for (int i = threadIdx.x; i < 3 * W + 32; i += NW * 64) sb[i] = p.sbias[i];
+    float* yo = (float*)(lds + YO);
+    for (int i = threadIdx.x; i < 32; i += NW * 64) yo[i] = i < kSurYdim ? p.y[(size_t)yi * kSurYdim + i] : 0.0f;
+    __syncthreads();
+    e.start_mid();
+  }
+  const float* ylds = (const float*)(lds + YO);
+  Rng rng = rng_init(p.seed, (uint64_t)(p.chain_offset + c_local), (uint64_t)yi);
+  float x[3];
+  if (p.x_init) {
+#pragma unroll
+    for (int d = 0; d < 3; ++d) x[d] = p.x_init[((size_t)yi * p.n_chains + cc) * 3 + d];
+  } else {  // torch.rand(n, 3) * 2 - 1 (generate_scatterometry_ground_truth.py:27)
+#pragma unroll
+    for (int d = 0; d < 3; ++d) x[d] = (float)(rng_next(rng) >> 8) * 0x1p-24f * 2.0f - 1.0f;
+  }
+  bool oor = false;
+  f32x4 f[2];
+  sur_forward(e, x, g, oor, f);
+  const float e0 = mh_energy(f, ylds, x, p.a, p.b2, p.lam, g);
+  float e_cur = e0;
+  for (int s = 0; s < p.num_steps; ++s) {
+    float xi[3];
+    rng_normals<3>(rng, xi);
+    const float u = (float)(rng_next(rng) >> 8) * 0x1p-24f;
+    float xp[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      xp[d] = x[d] + p.noise_std * xi[d];
+      oor |= beyond_fp16(xp[d]);
+    }
+    sur_forward(e, xp, g, oor, f);
+    const float e_prop = mh_energy(f, ylds, xp, p.a, p.b2, p.lam, g);
+    const bool acc = u < expf(-e_prop + e_cur);
+#pragma unroll
+    for (int d = 0; d < 3; ++d) x[d] = acc ? xp[d] : x[d];
+    e_cur = acc ? e_prop : e_cur;
+  }
+  wait_vmcnt<0>();  // the prefetched chunks of a step that never ran land before the workgroup exits
+  x3::report_range(oor && valid, p.err, lane);
+  if (valid && g == 0) {
+    float* dst = p.x_out + ((size_t)yi * p.n_chains + c_local) * 3;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) dst[d] = x[d];
+    if (p.e_out) p.e_out[(size_t)yi * p.n_chains + c_local] = e_cur - e0;
+  }
+}
+
 // the per-step coefficients: (tau, beta, g, 0), (mean_weight, var, 0, 0) -- the device functions every sampler uses
 __global__ void dps_x3_coef_kernel(float4* coef, int S, float T, float bmin, float bdiff) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -622,6 +745,13 @@ __global__ void dps_x3_coef_kernel(float4* coef, int S, float T, float bmin, flo
 }
 
 }  // namespace dx3
+
+hipError_t launch_mh_x3(const MhX3Params& p, int n_y, hipStream_t st) {
+  const long long per_wg = dx3::NW * 16;
+  const dim3 grid((unsigned)((p.n_chains + per_wg - 1) / per_wg), (unsigned)n_y), block(dx3::NW * 64);
+  hipLaunchKernelGGL(dx3::mh_x3_kernel, grid, block, 0, st, p);
+  return hipGetLastError();
+}
 
 hipError_t launch_dps_x3(const DpsX3Params& p, int n_y, hipStream_t st) {
   const long long per_wg = dx3::NW * 16;

@@ -212,6 +212,24 @@ struct DpsX3Params {
 };
 hipError_t launch_dps_x3(const DpsX3Params& p, int n_y, hipStream_t st);
 
+// fp32x3 random-walk MH (dmip_dps_x3.hip mh_x3_kernel): the surrogate's forward chunks S2 | S3 | Sout of the DPS image
+constexpr int kDpsX3SurFwdChunks = 17;
+struct MhX3Params {
+  const char* simg;     // the surrogate's fp32x3 chunks (DpsX3Params::simg; the first 17 used)
+  const char* sl1;      // its layer 1 over x, split: [16][64][8] fp16
+  const float* sbias;   // b1 | b2 | b3 [256] | b4 [32]
+  const float* y;       // [n_y][23]
+  long long n_chains, chain_offset;
+  int num_steps;
+  float noise_std, a, b2, lam;
+  unsigned long long seed;
+  const float* x_init;  // [n_y][n_chains][3] or null (x0 ~ U[-1, 1]^3 from the chain RNG)
+  float* x_out;         // [n_y][n_chains][3]
+  float* e_out;         // [n_y][n_chains] E(x_S) - E(x_0), or null
+  unsigned int* err;    // device status word (kErrRange)
+};
+hipError_t launch_mh_x3(const MhX3Params& p, int n_y, hipStream_t st);
+
 hipError_t launch_surrogate_eval(const SurrogateParams& p, int mode, int n_wg, hipStream_t st);
 int surrogate_rows_per_wg();
 hipError_t launch_mh(const SurrogateParams& p, int n_y, hipStream_t st);

@@ -9,6 +9,7 @@ exact-f32 MFMA kernels (libdmip dmip_log_posterior / dmip_mh_sample, csrc/dmip_s
 whenever the samples are on a HIP device and the forward model is the reference's surrogate shape.
 """
 import os
+import warnings
 
 import numpy as np
 import torch
@@ -201,10 +202,13 @@ class ScatterometryEnergy:
 
 
 def mh_sample(forward_model, params, ys, n_chains, num_steps, noise_std, seed=None, chain_offset=0, x_init=None,
-              noise=None, unif=None, return_ediff=False):
-    """Fused random-walk MH (dmip_mh_sample) for every row of ys (n_y, 23): device tensor
+              noise=None, unif=None, return_ediff=False, precision="fp32"):
+    """Fused random-walk MH (dmip_mh_sample_ex) for every row of ys (n_y, 23): device tensor
     (n_y, n_chains, 3). x_init (n_y, n_chains, 3) or None for x0 ~ U[-1, 1]^3 from the chain RNG;
-    noise (S, n_y, n_chains, 3) / unif (S, n_y, n_chains) replay captured draws."""
+    noise (S, n_y, n_chains, 3) / unif (S, n_y, n_chains) replay captured draws (exact f32 only).
+    precision "fp32": the exact-f32 kernel; "fp32x3": the surrogate's products as three-term fp16 splits (same
+    RNG stream and acceptance test per chain) -- a weight, proposal or activation beyond fp16's range resamples
+    every chain with "fp32" (RuntimeWarning)."""
     from . import _lib
     ys = torch.as_tensor(ys)
     if not torch.cuda.is_available():
@@ -219,8 +223,25 @@ def mh_sample(forward_model, params, ys, n_chains, num_steps, noise_std, seed=No
     out = torch.empty(ys.shape[0], int(n_chains), 3, device=dev, dtype=torch.float32)
     ed = torch.empty(ys.shape[0], int(n_chains), device=dev, dtype=torch.float32) if return_ediff else None
     prep = lambda t: None if t is None else t.to(device=dev, dtype=torch.float32).contiguous()
-    _lib.mh_sample(h, _lib.scat_noise(params['a'], params['b'], params['lambd_bd']), ys, n_chains, chain_offset,
-                   num_steps, noise_std, seed, out, prep(x_init), prep(noise), prep(unif), ed)
+    if precision not in ("fp32", "fp32x3"):
+        raise ValueError(f"mh_sample: precision {precision!r} (\"fp32\" or \"fp32x3\")")
+    if precision == "fp32x3" and (noise is not None or unif is not None):
+        raise ValueError("mh_sample: injected draws replay the exact-f32 kernel (precision=\"fp32\")")
+    nz = _lib.scat_noise(params['a'], params['b'], params['lambd_bd'])
+    x0 = prep(x_init)
+    if precision == "fp32x3":
+        try:
+            _lib.clear_range_status(dev)
+            _lib.mh_sample(h, nz, ys, n_chains, chain_offset, num_steps, noise_std, seed, out, x0, None, None, ed,
+                           precision="fp32x3")
+            _lib.device_status(dev)
+            return (out, ed) if return_ediff else out
+        except (ValueError, RuntimeError) as e:
+            if not _lib.is_range_error(e):
+                raise
+            warnings.warn(f"{e}; sampled with the exact-f32 engine instead", RuntimeWarning)
+    _lib.mh_sample(h, nz, ys, n_chains, chain_offset, num_steps, noise_std, seed, out, x0, prep(noise), prep(unif),
+                   ed)
     return (out, ed) if return_ediff else out
 
 
@@ -251,14 +272,14 @@ def anneal_to_energy(x_curr, energy, metr_steps_per_block, noise_std=0.1, langev
 
 
 def generate_gt_samples(forward_model, params, ys, out_dir=None, n_samples_x=30000, n_repeats=10, metr_steps=1000,
-                        noise_std=0.5, seed=None):
+                        noise_std=0.5, seed=None, precision="fp32"):
     """generate_scatterometry_ground_truth.py:26-63 on the device: for every y and repeat j,
     n_samples_x MH chains from U[-1, 1]^3 for metr_steps steps (NOISE_STD_MCMC, METR_STEPS of
-    config_scatterometry.yml), all in one launch; optionally written as out_dir/<i>/<j>.npy.
-    Returns a device tensor (n_y, n_repeats, n_samples_x, 3)."""
+    config_scatterometry.yml), all in one launch (precision as mh_sample); optionally written as
+    out_dir/<i>/<j>.npy. Returns a device tensor (n_y, n_repeats, n_samples_x, 3)."""
     ys = torch.as_tensor(ys, dtype=torch.float32).reshape(-1, 23)
     rows = ys.repeat_interleave(n_repeats, dim=0)
-    x = mh_sample(forward_model, params, rows, n_samples_x, metr_steps, noise_std, seed=seed)
+    x = mh_sample(forward_model, params, rows, n_samples_x, metr_steps, noise_std, seed=seed, precision=precision)
     x = x.reshape(ys.shape[0], n_repeats, n_samples_x, 3)
     if out_dir:
         xh = x.cpu().numpy()

@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define DMIP_ABI_VERSION 8
+#define DMIP_ABI_VERSION 9
 
 typedef enum {
   DMIP_OK = 0,
@@ -336,6 +336,17 @@ int dmip_mh_sample(const dmip_surrogate* s, const dmip_scat_noise* noise, const 
                    int64_t n_chains, int64_t chain_offset, int num_steps, float noise_std, uint64_t seed,
                    const float* x_init_dev, const float* noise_dev, const float* unif_dev, float* x_out_dev,
                    float* e_out_dev, void* stream);
+
+/* dmip_mh_sample with a precision (ABI 9): DMIP_PREC_F32 = dmip_mh_sample; DMIP_PREC_F32X3 = the same chains with
+ * the surrogate's products as the three-term fp16 split of the fp32x3 samplers (the forward half of
+ * dmip_dps_sample_ex's surrogate pass) -- the same RNG stream, proposals, energy and acceptance test per chain.
+ * fp32x3 takes no injected draws (DMIP_ERR_UNSUPPORTED); a weight beyond fp16's range is refused
+ * (DMIP_ERR_UNSUPPORTED, "fp16 range"); a proposal or hidden activation beyond it is reported by
+ * dmip_device_status ("fp16 range"), and the Python caller then resamples with DMIP_PREC_F32. */
+int dmip_mh_sample_ex(const dmip_surrogate* s, const dmip_scat_noise* noise, const float* y_dev, int n_y,
+                      int64_t n_chains, int64_t chain_offset, int num_steps, float noise_std, uint64_t seed,
+                      const float* x_init_dev, const float* noise_dev, const float* unif_dev, int precision,
+                      float* x_out_dev, float* e_out_dev, void* stream);
 
 /* Diffusion posterior sampling (DPS, Chung et al. 2023) on the reference's Euler-Maruyama predictor:
  * BASELINE config 4. The reference has no sampling-time guidance (its "Posterior"

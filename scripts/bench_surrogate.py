@@ -24,6 +24,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 FLOPS_EVAL = 2 * (3 * 256 + 2 * 256 * 256 + 256 * 23)
 PEAK_F32_MFMA = 157.3  # TFLOP/s, MI355X dense f32-input MFMA (MI355X_MICROARCH.md)
+PEAK_FP16_MFMA = 2500.0  # TFLOP/s, dense fp16 MFMA (the same guide; bench.py PEAK_BF16_TFLOPS)
 
 
 def surrogate(dev):
@@ -70,6 +71,11 @@ def main():
     ms_mh = timed(mh, a.reps)
     chain_steps = a.rows * a.chains * a.steps
     mh_tf = chain_steps * FLOPS_EVAL / (ms_mh * 1e-3) / 1e12
+    # the fp32x3 kernel (dmip_dps_x3.hip mh_x3_kernel): 3 fp16 MFMA products per algorithmic one
+    mh3 = lambda: pr.mh_sample(fm, prm, rows, a.chains, a.steps, 0.5, seed=1, precision="fp32x3")
+    mh3()
+    ms_mh3 = timed(mh3, a.reps)
+    mh3_tf = chain_steps * FLOPS_EVAL / (ms_mh3 * 1e-3) / 1e12
 
     x = (torch.rand(a.eval_n, 3, device=dev) * 2.2 - 1.1)
     y = rows[:1].contiguous()
@@ -95,6 +101,9 @@ def main():
         "roofline": {"bound": "mfma", "achieved": mh_tf, "peak": PEAK_F32_MFMA, "unit": "TFLOP/s",
                      "frac": mh_tf / PEAK_F32_MFMA, "dtype": "f32 (v_mfma_f32_16x16x4_f32)",
                      "flops_per_chain_step": FLOPS_EVAL},
+        "mh_fp32x3": {"ms_per_launch": ms_mh3, "chain_steps_per_s": chain_steps / (ms_mh3 * 1e-3),
+                      "algorithmic_tflops": mh3_tf, "executed_fp16_tflops": 3 * mh3_tf,
+                      "frac_fp16_peak_executed": 3 * mh3_tf / PEAK_FP16_MFMA, "speedup_vs_f32": ms_mh / ms_mh3},
         "log_posterior_grad": {"rows": a.eval_n, "ms": ms_ev, "rows_per_s": a.eval_n / (ms_ev * 1e-3),
                                "tflops": ev_tf, "frac": ev_tf / PEAK_F32_MFMA},
         "log_posterior": {"rows": a.eval_n, "ms": ms_ev0, "rows_per_s": a.eval_n / (ms_ev0 * 1e-3),

@@ -32,7 +32,7 @@ def test_exports_every_declared_symbol(lib, dmip):
 
 
 def test_abi_version(lib, dmip):
-    assert lib.dmip_abi_version() == dmip._lib.ABI_VERSION == 8
+    assert lib.dmip_abi_version() == dmip._lib.ABI_VERSION == 9
 
 
 def test_supported_shapes(lib, dmip):
@@ -147,6 +147,9 @@ def test_surrogate_entry_points_reject_bad_arguments(lib, dmip):
     assert lib.dmip_log_posterior(None, ctypes.byref(nz), None, None, 0, 4, None, None, None) == L.DMIP_ERR_INVALID
     assert lib.dmip_mh_sample(None, ctypes.byref(nz), None, 1, 10, 0, 5, 0.5, 1, None, None, None, None, None,
                               None) == L.DMIP_ERR_INVALID
+    for prec in (L.DMIP_PREC_F32, L.DMIP_PREC_F32X3, 7):
+        assert lib.dmip_mh_sample_ex(None, ctypes.byref(nz), None, 1, 10, 0, 5, 0.5, 1, None, None, None, prec, None,
+                                     None, None) == L.DMIP_ERR_INVALID
 
 
 def test_dps_rejects_bad_arguments(lib, dmip):

@@ -131,18 +131,60 @@ def test_mh_replays_reference_draws(dmip, golden, fm):
     np.testing.assert_allclose(ed[0].cpu().numpy()[same], z["mh_ediff"][same], rtol=1e-4, atol=2e-3)
 
 
-def test_mh_product_rng_vs_oracle(dmip, golden, fm):
+@pytest.mark.parametrize("precision", ["fp32", "fp32x3"])
+def test_mh_product_rng_vs_oracle(dmip, golden, fm, precision):
+    """Chain by chain against the oracle on the same RNG stream. fp32x3 (three-term fp16 splits of every
+    surrogate product, ~1e-7 relative per product) takes the same accept/reject path on the same share."""
     model, pr, params = fm
     y = golden("data_scat.npz")["y_test"][5]
     n, S, seed = 300, 30, 1234
     x = pr.mh_sample(model, {"a": 0.2, "b": 0.01, "lambd_bd": 1000}, torch.from_numpy(y)[None], n, S, 0.5,
-                     seed=seed)[0].cpu().numpy()
+                     seed=seed, precision=precision)[0].cpu().numpy()
     ref, _ = O.mh_sample(params, y, S, 0.5, seed=seed, n_chains=n)
     same = np.all(np.abs(x - ref) <= 1e-5, axis=1)
     assert same.mean() >= 0.95, same.mean()
 
 
-def test_mh_distribution_vs_reference_sampler(dmip, golden, fm):
+def test_mh_fp32x3_vs_exact_f32_chains(dmip, golden, fm):
+    """fp32x3 against the exact-f32 kernel on 4 ys x 4096 chains x 200 steps from given starts: the same final
+    state on >= 95% of chains, and there the energy change E(x_S) - E(x_0) agrees to 1e-3 relative + 2e-3."""
+    model, pr, _ = fm
+    ys = torch.from_numpy(golden("data_scat.npz")["y_test"][10:14])
+    prm = {"a": 0.2, "b": 0.01, "lambd_bd": 1000}
+    x0 = torch.rand(4, 4096, 3, generator=torch.Generator().manual_seed(5)) * 2 - 1
+    xa, ea = pr.mh_sample(model, prm, ys, 4096, 200, 0.5, seed=21, x_init=x0, return_ediff=True)
+    xb, eb = pr.mh_sample(model, prm, ys, 4096, 200, 0.5, seed=21, x_init=x0, return_ediff=True, precision="fp32x3")
+    xa, xb, ea, eb = (t.cpu().numpy() for t in (xa, xb, ea, eb))
+    same = np.all(np.abs(xa - xb) <= 1e-5, axis=2)
+    assert same.mean() >= 0.95, same.mean()
+    np.testing.assert_allclose(eb[same], ea[same], rtol=1e-3, atol=2e-3)
+
+
+def test_mh_fp32x3_refusals_and_range_fallback(dmip, golden, fm):
+    model, pr, _ = fm
+    prm = {"a": 0.2, "b": 0.01, "lambd_bd": 1000}
+    y = torch.from_numpy(golden("data_scat.npz")["y_test"][2])[None]
+    with pytest.raises(ValueError, match="injected"):
+        pr.mh_sample(model, prm, y, 4, 2, 0.5, seed=0, noise=torch.zeros(2, 1, 4, 3), unif=torch.zeros(2, 1, 4),
+                     precision="fp32x3")
+    with pytest.raises(ValueError, match="precision"):
+        pr.mh_sample(model, prm, y, 4, 2, 0.5, seed=0, precision="fp16")
+    # a start beyond fp16's range: the split kernel reports it and every chain is resampled in exact f32
+    x0 = torch.rand(1, 200, 3, generator=torch.Generator().manual_seed(1)) * 2 - 1
+    x0[0, 17] = 1e5
+    ref = pr.mh_sample(model, prm, y, 200, 10, 0.5, seed=4, x_init=x0)
+    with pytest.warns(RuntimeWarning, match="fp16 range"):
+        got = pr.mh_sample(model, prm, y, 200, 10, 0.5, seed=4, x_init=x0, precision="fp32x3")
+    assert torch.equal(got, ref)
+    # and the status word is clear afterwards: an in-range fp32x3 launch does not warn
+    import warnings as _w
+    with _w.catch_warnings():
+        _w.simplefilter("error")
+        pr.mh_sample(model, prm, y, 200, 10, 0.5, seed=4, precision="fp32x3")
+
+
+@pytest.mark.parametrize("precision", ["fp32", "fp32x3"])
+def test_mh_distribution_vs_reference_sampler(dmip, golden, fm, precision):
     """30,000 fused chains x 1000 steps (the ground-truth generator's settings) against the
     reference anneal_to_energy's own 4,000 x 1000 run for y_test[0]: per-dimension two-sample KS
     below the alpha = 0.01 critical value."""
@@ -150,7 +192,7 @@ def test_mh_distribution_vs_reference_sampler(dmip, golden, fm):
     z = golden("surrogate_io.npz")
     ref = z["gt_samples"]
     x = pr.mh_sample(model, {"a": 0.2, "b": 0.01, "lambd_bd": 1000}, torch.from_numpy(z["mh_y"])[None], 30000,
-                     int(z["gt_steps"]), 0.5, seed=77)[0].cpu().numpy()
+                     int(z["gt_steps"]), 0.5, seed=77, precision=precision)[0].cpu().numpy()
     assert np.all(np.isfinite(x))
     crit = 1.63 * np.sqrt((x.shape[0] + ref.shape[0]) / (x.shape[0] * ref.shape[0]))
     for k in range(3):
@@ -158,18 +200,19 @@ def test_mh_distribution_vs_reference_sampler(dmip, golden, fm):
         assert ks < crit, (k, ks, crit)
 
 
-def test_mh_shards_and_rows_bit_identical(dmip, golden, fm):
+@pytest.mark.parametrize("precision", ["fp32", "fp32x3"])
+def test_mh_shards_and_rows_bit_identical(dmip, golden, fm, precision):
     model, pr, _ = fm
     ys = torch.from_numpy(golden("data_scat.npz")["y_test"][:3])
     prm = {"a": 0.2, "b": 0.01, "lambd_bd": 1000}
-    full = pr.mh_sample(model, prm, ys, 1000, 20, 0.5, seed=9)
-    shard = pr.mh_sample(model, prm, ys, 300, 20, 0.5, seed=9, chain_offset=500)
+    full = pr.mh_sample(model, prm, ys, 1000, 20, 0.5, seed=9, precision=precision)
+    shard = pr.mh_sample(model, prm, ys, 300, 20, 0.5, seed=9, chain_offset=500, precision=precision)
     assert torch.equal(full[:, 500:800], shard)
-    one = pr.mh_sample(model, prm, ys[1:2], 1000, 20, 0.5, seed=9)
+    one = pr.mh_sample(model, prm, ys[1:2], 1000, 20, 0.5, seed=9, precision=precision)
     # the RNG stream is the row index: row 1 of the batch is not row 0 of a single-y launch ...
     assert not torch.equal(full[1], one[0])
     # ... but re-running is deterministic
-    assert torch.equal(full, pr.mh_sample(model, prm, ys, 1000, 20, 0.5, seed=9))
+    assert torch.equal(full, pr.mh_sample(model, prm, ys, 1000, 20, 0.5, seed=9, precision=precision))
 
 
 def test_generate_gt_samples_files(dmip, golden, fm, tmp_path):
