@@ -217,6 +217,13 @@ __device__ __forceinline__ void store_pair(const float (&a)[4], int o, u32x4 (&O
 }
 
 __device__ __forceinline__ bool beyond_fp16(float v) { return !(__builtin_fabsf(v) <= 65504.0f); }
+// the running max |v| of the values a chain splits (RangeMax::mx, checked once at the end: a value beyond fp16's range
+// is finite and > 65504 or inf when it first appears -- what follows from it may be NaN, which max ignores, but the max
+// has seen the first one); one v_max3 per two values instead of a compare and a mask OR per value
+__device__ __forceinline__ void track4(float& mx, const float (&v)[4]) {
+  mx = fmaxf(fmaxf(mx, __builtin_fabsf(v[0])), __builtin_fabsf(v[1]));
+  mx = fmaxf(fmaxf(mx, __builtin_fabsf(v[2])), __builtin_fabsf(v[3]));
+}
 
 // The per-tile epilogues of a 256 -> 256 layer (tile o of the layer's output, f32 pre-activations z):
 //   PriorFwd:  r = 1 / (1 + 2^z) (z pre-scaled by 2 log2 e; the next layer is folded for r), D = 4 r (1 - r)
@@ -236,33 +243,27 @@ struct EpiPriorFwd {
 };
 struct EpiSurFwd {
   uint32_t* m;  // [2]: bit 4 (o & 7) + k of word o >> 3
-  bool* oor;
+  float* mx;
   __device__ __forceinline__ void operator()(const f32x4& z, int o, u32x4 (&Oh)[KQ], u32x4 (&Ol)[KQ]) const {
     float h[4];
-    bool bad = false;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const bool pos = z[k] > 0.0f;
       h[k] = pos ? z[k] : 0.0f;
       m[o >> 3] |= (pos ? 1u : 0u) << ((o & 7) * 4 + k);
-      bad |= beyond_fp16(h[k]);
     }
-    *oor |= bad;
+    track4(*mx, h);
     store_pair(h, o, Oh, Ol);
   }
 };
 struct EpiBackD {
   const float (*D)[4];
-  bool* oor;
+  float* mx;
   __device__ __forceinline__ void operator()(const f32x4& z, int o, u32x4 (&Oh)[KQ], u32x4 (&Ol)[KQ]) const {
     float v[4];
-    bool bad = false;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      v[k] = z[k] * D[o][k];
-      bad |= beyond_fp16(v[k]);
-    }
-    *oor |= bad;
+    for (int k = 0; k < 4; ++k) v[k] = z[k] * D[o][k];
+    track4(*mx, v);
     store_pair(v, o, Oh, Ol);
   }
 };
@@ -272,36 +273,30 @@ struct EpiBackL1 {
   const char* lds;
   int lane, g;
   u32x4 b1;
-  bool* oor;
+  float* mx;
   __device__ __forceinline__ void operator()(const f32x4& z, int o, u32x4 (&Oh)[KQ], u32x4 (&Ol)[KQ]) const {
     const u32x4 a = *(const u32x4*)(lds + PL1 + o * 512 + (lane & 31) * 16);
     const f32x4 c = *(const f32x4*)(lds + PB + (16 * o + 4 * g) * 4);
     const f32x4 z1 = mfma16(a, b1, c);
     float v[4];
-    bool bad = false;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const float r1 = x3::x3_act_r(z1[k]);
       const float r2 = x3::x3_act_r(__builtin_fmaf(-2.0f * kTanhScale, r1, kTanhScale));
       v[k] = z[k] * (16.0f * r1 * (1.0f - r1) * r2 * (1.0f - r2));
-      bad |= beyond_fp16(v[k]);
     }
-    *oor |= bad;
+    track4(*mx, v);
     store_pair(v, o, Oh, Ol);
   }
 };
 struct EpiBackMask {
   const uint32_t* m;
-  bool* oor;
+  float* mx;
   __device__ __forceinline__ void operator()(const f32x4& z, int o, u32x4 (&Oh)[KQ], u32x4 (&Ol)[KQ]) const {
     float v[4];
-    bool bad = false;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      v[k] = ((m[o >> 3] >> ((o & 7) * 4 + k)) & 1u) ? z[k] : 0.0f;
-      bad |= beyond_fp16(v[k]);
-    }
-    *oor |= bad;
+    for (int k = 0; k < 4; ++k) v[k] = ((m[o >> 3] >> ((o & 7) * 4 + k)) & 1u) ? z[k] : 0.0f;
+    track4(*mx, v);
     store_pair(v, o, Oh, Ol);
   }
 };
@@ -457,6 +452,7 @@ __global__ void __launch_bounds__(NW * 64, 1) dps_x3_kernel(DpsX3Params p) {
     for (int d = 0; d < 3; ++d) x[d] = __fadd_rn(__fmul_rn(n0[d], p.stdv), p.mean);
   }
   bool oor = false;
+  float vmax = 0.0f;  // track4's running max of the split values
   const int S = p.num_steps;
   for (int i = 0; i < S; ++i) {
     const float4 c4 = ((const float4*)p.coef)[2 * i];      // tau, beta, g (dmip_device.h step_coef)
@@ -501,12 +497,12 @@ __global__ void __launch_bounds__(NW * 64, 1) dps_x3_kernel(DpsX3Params p) {
         const bool pos = z[k] > 0.0f;
         h[k] = pos ? z[k] : 0.0f;
         m1[o >> 3] |= (pos ? 1u : 0u) << ((o & 7) * 4 + k);
-        oor |= beyond_fp16(h[k]);
       }
+      track4(vmax, h);
       store_pair(h, o, Ah, Al);
     });
-    layer256(e, Ah, Al, SB + W * 4, EpiSurFwd{m2, &oor}, Bh, Bl);
-    layer256(e, Bh, Bl, SB + 2 * W * 4, EpiSurFwd{m3, &oor}, Ah, Al);
+    layer256(e, Ah, Al, SB + W * 4, EpiSurFwd{m2, &vmax}, Bh, Bl);
+    layer256(e, Bh, Bl, SB + 2 * W * 4, EpiSurFwd{m3, &vmax}, Ah, Al);
     f32x4 f[2];
     small256<2>(e, Ah, Al, SB + 3 * W * 4, f);
 
@@ -570,9 +566,9 @@ __global__ void __launch_bounds__(NW * 64, 1) dps_x3_kernel(DpsX3Params p) {
       x3::split_pair(vs[0][2], vs[0][3], h1, l1);
       x3::split_pair(vs[1][0], vs[1][1], h2, l2);
       x3::split_pair(vs[1][2], vs[1][3], h3, l3);
-      wide1(e, u32x4{h0, h1, h2, h3}, u32x4{l0, l1, l2, l3}, EpiBackMask{m3, &oor}, Ah, Al);
-      layer256(e, Ah, Al, -1, EpiBackMask{m2, &oor}, Bh, Bl);
-      layer256(e, Bh, Bl, -1, EpiBackMask{m1, &oor}, Ah, Al);
+      wide1(e, u32x4{h0, h1, h2, h3}, u32x4{l0, l1, l2, l3}, EpiBackMask{m3, &vmax}, Ah, Al);
+      layer256(e, Ah, Al, -1, EpiBackMask{m2, &vmax}, Bh, Bl);
+      layer256(e, Bh, Bl, -1, EpiBackMask{m1, &vmax}, Ah, Al);
       f32x4 acc[1];
       small256<1>(e, Ah, Al, -1, acc);
 #pragma unroll
@@ -587,9 +583,9 @@ __global__ void __launch_bounds__(NW * 64, 1) dps_x3_kernel(DpsX3Params p) {
       const float u[4] = {gx[0] * is2, gx[1] * is2, gx[2] * is2, 0.0f};
       u32x4 bh, bl;
       vec_b(u, g, bh, bl);
-      wide1(e, bh, bl, EpiBackD{D3, &oor}, Ah, Al);
-      layer256(e, Ah, Al, -1, EpiBackD{D2, &oor}, Bh, Bl);
-      layer256(e, Bh, Bl, -1, EpiBackL1{lds, lane, g, b1p, &oor}, Ah, Al);
+      wide1(e, bh, bl, EpiBackD{D3, &vmax}, Ah, Al);
+      layer256(e, Ah, Al, -1, EpiBackD{D2, &vmax}, Bh, Bl);
+      layer256(e, Bh, Bl, -1, EpiBackL1{lds, lane, g, b1p, &vmax}, Ah, Al);
       f32x4 acc[1];
       small256<1>(e, Ah, Al, -1, acc);
 #pragma unroll
@@ -607,7 +603,7 @@ __global__ void __launch_bounds__(NW * 64, 1) dps_x3_kernel(DpsX3Params p) {
     }
   }
   wait_vmcnt<0>();  // the prefetched chunks of a step that never ran land before the workgroup exits
-  x3::report_range(oor && valid, p.err, lane);
+  x3::report_range((oor || !(vmax <= 65504.0f)) && valid, p.err, lane);
   if (valid && g == 0) {
     float* dst = p.x_out + ((size_t)yi * p.n_chains + c_local) * 3;
 #pragma unroll
@@ -652,20 +648,18 @@ __device__ __forceinline__ float mh_energy(const f32x4 (&f)[2], const float* y, 
 }
 
 // the surrogate's forward pass at x (every lane of the chain holds x): output rows f (tiles 0, 1), range flag
-__device__ __forceinline__ void sur_forward(Eng& e, const float (&x)[3], int g, bool& oor, f32x4 (&f)[2]) {
+__device__ __forceinline__ void sur_forward(Eng& e, const float (&x)[3], int g, float& vmax, f32x4 (&f)[2]) {
   u32x4 Ah[KQ], Al[KQ], Bh[KQ], Bl[KQ];
   uint32_t m2[2] = {0u, 0u}, m3[2] = {0u, 0u};
   layer1(e, SL1, SB, l1_b<3>(x, g), [&](const f32x4& z, int o) {
     float h[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      h[k] = z[k] > 0.0f ? z[k] : 0.0f;
-      oor |= beyond_fp16(h[k]);
-    }
+    for (int k = 0; k < 4; ++k) h[k] = z[k] > 0.0f ? z[k] : 0.0f;
+    track4(vmax, h);
     store_pair(h, o, Ah, Al);
   });
-  layer256(e, Ah, Al, SB + W * 4, EpiSurFwd{m2, &oor}, Bh, Bl);
-  layer256(e, Bh, Bl, SB + 2 * W * 4, EpiSurFwd{m3, &oor}, Ah, Al);
+  layer256(e, Ah, Al, SB + W * 4, EpiSurFwd{m2, &vmax}, Bh, Bl);
+  layer256(e, Bh, Bl, SB + 2 * W * 4, EpiSurFwd{m3, &vmax}, Ah, Al);
   small256<2>(e, Ah, Al, SB + 3 * W * 4, f);
 }
 
@@ -702,8 +696,10 @@ __global__ void __launch_bounds__(NW * 64, 1) mh_x3_kernel(MhX3Params p) {
     for (int d = 0; d < 3; ++d) x[d] = (float)(rng_next(rng) >> 8) * 0x1p-24f * 2.0f - 1.0f;
   }
   bool oor = false;
+  float vmax = 0.0f;  // track4's running max of the split values
+  for (int d = 0; d < 3; ++d) oor |= beyond_fp16(x[d]);
   f32x4 f[2];
-  sur_forward(e, x, g, oor, f);
+  sur_forward(e, x, g, vmax, f);
   const float e0 = mh_energy(f, ylds, x, p.a, p.b2, p.lam, g);
   float e_cur = e0;
   for (int s = 0; s < p.num_steps; ++s) {
@@ -716,7 +712,7 @@ __global__ void __launch_bounds__(NW * 64, 1) mh_x3_kernel(MhX3Params p) {
       xp[d] = x[d] + p.noise_std * xi[d];
       oor |= beyond_fp16(xp[d]);
     }
-    sur_forward(e, xp, g, oor, f);
+    sur_forward(e, xp, g, vmax, f);
     const float e_prop = mh_energy(f, ylds, xp, p.a, p.b2, p.lam, g);
     const bool acc = u < expf(-e_prop + e_cur);
 #pragma unroll
@@ -724,7 +720,7 @@ __global__ void __launch_bounds__(NW * 64, 1) mh_x3_kernel(MhX3Params p) {
     e_cur = acc ? e_prop : e_cur;
   }
   wait_vmcnt<0>();  // the prefetched chunks of a step that never ran land before the workgroup exits
-  x3::report_range(oor && valid, p.err, lane);
+  x3::report_range((oor || !(vmax <= 65504.0f)) && valid, p.err, lane);
   if (valid && g == 0) {
     float* dst = p.x_out + ((size_t)yi * p.n_chains + c_local) * 3;
 #pragma unroll
