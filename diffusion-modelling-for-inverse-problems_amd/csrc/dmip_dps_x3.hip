@@ -25,6 +25,9 @@
 // do, and the Python default resamples in exact f32.
 #include "dmip_x3.h"
 
+#include <cstdlib>
+#include <utility>
+
 namespace dmip {
 namespace dx3 {
 
@@ -223,6 +226,10 @@ __device__ __forceinline__ bool beyond_fp16(float v) { return !(__builtin_fabsf(
 __device__ __forceinline__ void track4(float& mx, const float (&v)[4]) {
   mx = fmaxf(fmaxf(mx, __builtin_fabsf(v[0])), __builtin_fabsf(v[1]));
   mx = fmaxf(fmaxf(mx, __builtin_fabsf(v[2])), __builtin_fabsf(v[3]));
+  // pinned: otherwise the compiler re-associates a whole pass's max chain into one tree at its end and keeps every
+  // tracked value alive until then (DPS: 176 B of scratch and 55 more AGPRs; the multi-tile MH engine: hundreds of
+  // spilled registers)
+  asm("" : "+v"(mx));
 }
 
 // The per-tile epilogues of a 256 -> 256 layer (tile o of the layer's output, f32 pre-activations z):
@@ -663,6 +670,244 @@ __device__ __forceinline__ void sur_forward(Eng& e, const float (&x)[3], int g, 
   small256<2>(e, Ah, Al, SB + 3 * W * 4, f);
 }
 
+// ---- the multi-tile forward engine of the MH kernel (MT tiles of 16 chains per wave; DPS keeps one tile because the
+// prior's forward derivatives must live until its reverse pass). The hidden layers run k-major, as dmip_x3k.h's
+// sampler does: chunk q of a layer is k-step q for all 16 output tiles, gathered by the LDS-DMA pieces straight from
+// the DPS image's m-major chunks (a 1 KiB piece is one (tile, k-step, hi|lo) fragment, so the gather costs only the
+// piece addresses). Every A fragment pair then feeds 3 MT MFMAs, a tile's 16 accumulators (64 registers) are the
+// only per-tile state beside its input operands, and the input's k-step q dies after chunk q -- so MT tiles fit
+// where the m-major order (input and output operands live together, 128 registers a tile) does not. The chunk's
+// LDS reads and its share of the refill (the guide's 60-185 issue cycles per 1 KiB piece) are spread over MT times
+// the matrix work. Same ring and mid-chunk barrier protocol as mid_units; the output layer's chunk stays m-major.
+// compile-time loops (the per-tile register arrays must be indexed by constants from the start, before any unrolling,
+// or SROA leaves them in scratch)
+template <typename F, int... I>
+__device__ __forceinline__ void sfor_impl(const F& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void sfor(const F& f) {
+  sfor_impl(f, std::make_integer_sequence<int, N>{});
+}
+struct EngK {
+  char* lds;
+  const char* img;  // the surrogate's DPS image: S2 | S3 (8 m-major chunks each) | Sout | ...
+  int c_issue, s_issue, s_read;
+  int w, lane, g;
+  static constexpr int NSTR = 2 * NCH + 1;  // 16 k-major hidden chunks + the output chunk per step
+  const char* dma_src;
+  char* dma_dst;
+  int dma_a, dma_b;  // piece Q's source: dma_src + (Q / 4) dma_a + ((Q / 2) % 2) dma_b + (Q % 2) KiB
+  __device__ __forceinline__ void ring_target() {
+    const int c = __builtin_amdgcn_readfirstlane(c_issue);
+    // hidden chunk c (layer c / 8, k-step q = c % 8): wave w's pieces 8 w + Q are the fragments (tile 4 w + Q / 2,
+    // k-step q, Q % 2) at m-major chunk 2 w + Q / 4, unit 8 ((Q / 2) % 2) + q; the output chunk is contiguous
+    const bool hid = c < 2 * NCH;
+    const char* src = hid ? img + (size_t)(c >> 3) * NCH * CHUNK + (c & 7) * 2048 + w * 2 * CHUNK
+                          : img + (size_t)2 * NCH * CHUNK + w * PPW * 1024;
+    dma_a = __builtin_amdgcn_readfirstlane(hid ? CHUNK : 4096);
+    dma_b = __builtin_amdgcn_readfirstlane(hid ? CHUNK / 2 : 2048);
+    const uint64_t addr = (uint64_t)src;
+    const char* base = (const char*)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(addr >> 32)) << 32) |
+                                     (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)addr));
+    asm volatile("" : "+s"(base));
+    dma_src = base;
+    dma_dst = lds + RING + __builtin_amdgcn_readfirstlane(s_issue) * CHUNK + w * PPW * 1024;
+    c_issue = c + 1 == NSTR ? 0 : c + 1;
+    s_issue = s_issue + 1 == R ? 0 : s_issue + 1;
+  }
+  template <int Q>
+  __device__ __forceinline__ void ring_piece() const {
+    glds16(dma_src + (Q / 4) * dma_a + ((Q / 2) % 2) * dma_b + (Q % 2) * 1024, dma_dst + Q * 1024, lane);
+  }
+  __device__ __forceinline__ void ring_issue() {
+    ring_target();
+    ring_piece<0>(), ring_piece<1>(), ring_piece<2>(), ring_piece<3>();
+    ring_piece<4>(), ring_piece<5>(), ring_piece<6>(), ring_piece<7>();
+  }
+  __device__ __forceinline__ f32x4 bias4(int off_bytes, int tile) const {
+    return *(const f32x4*)(lds + off_bytes + (16 * tile + 4 * g) * 4);
+  }
+  u32x4 nxt0, nxt1;
+  __device__ __forceinline__ void start_mid() {
+    for (int q = 0; q < R - 1; ++q) ring_issue();
+    wait_vmcnt<(R - 2) * PPW>();
+    lds_barrier();
+    const lds_cptr b0 = (lds_cptr)(lds + RING + lane * 16);
+    nxt0 = x3::lds_rd<0>(b0);
+    nxt1 = x3::lds_rd<1024>(b0);
+    x3::lds_wait2<0>(nxt0, nxt1);
+  }
+  __device__ __forceinline__ lds_cptr take(lds_cptr& nb) {
+    const lds_cptr b = (lds_cptr)(lds + RING + s_read * CHUNK + lane * 16);
+    s_read = s_read + 1 == R ? 0 : s_read + 1;
+    nb = (lds_cptr)(lds + RING + s_read * CHUNK + lane * 16);
+    return b;
+  }
+};
+static_assert(PPW == 8, "EngK::ring_issue");
+template <int NU, int U, int Q = 0>
+__device__ __forceinline__ void mid_pieces_k(const EngK& e) {
+  if constexpr (Q < PPW) {
+    constexpr int MIDU = NU / 2;
+    if constexpr (MIDU + 1 + (Q * (NU - 1 - MIDU)) / PPW == U) e.template ring_piece<Q>();
+    mid_pieces_k<NU, U, Q + 1>(e);
+  }
+}
+// k-step q's B operand pair of tile m from the previous layer's pre-activations In[m][2q], In[m][2q + 1] (store_pair's
+// dword order): relu, the running max (track4), the split
+template <int MT, typename M>
+__device__ __forceinline__ void act_pair(const f32x4 (&In)[MT][ST], int q, M m, float (&vmax)[MT], u32x4& nh,
+                                         u32x4& nl) {
+  float a[4], b[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    a[k] = In[m][2 * q][k] > 0.0f ? In[m][2 * q][k] : 0.0f;
+    b[k] = In[m][2 * q + 1][k] > 0.0f ? In[m][2 * q + 1][k] : 0.0f;
+  }
+  track4(vmax[m], a);
+  track4(vmax[m], b);
+  uint32_t h0, l0, h1, l1, h2, l2, h3, l3;
+  x3::split_pair(a[0], a[1], h0, l0);
+  x3::split_pair(a[2], a[3], h1, l1);
+  x3::split_pair(b[0], b[1], h2, l2);
+  x3::split_pair(b[2], b[3], h3, l3);
+  nh = u32x4{h0, h1, h2, h3};
+  nl = u32x4{l0, l1, l2, l3};
+}
+// one 16-unit chunk for MT tiles. OUT = false: k-major hidden chunk QK (unit U = output tile U, LDS fragment pair U);
+// OUT = true: the output layer's m-major chunk walked k-step by k-step (unit U = tile U % 2 at k-step U / 2, LDS pair
+// 8 (U % 2) + U / 2). (Hh, Hl): the current k-step's operands; the next k-step's are formed from In beside the MFMAs
+// into (Nh, Nl) -- hidden: tile m's at unit m, taken over after the chunk; output: all at the k-step's second unit.
+template <int MT, bool OUT, int QK, int NA, int U = 0>
+__device__ __forceinline__ void units_k(EngK& e, lds_cptr base, lds_cptr nbase, const f32x4 (&In)[MT][ST],
+                                        f32x4 (&Out)[MT][NA], u32x4 (&Hh)[MT], u32x4 (&Hl)[MT], u32x4 (&Nh)[MT],
+                                        u32x4 (&Nl)[MT], u32x4 (&fa)[2][2], float (&vmax)[MT]) {
+  constexpr int NU = 16;
+  if constexpr (U < NU) {
+    constexpr int MIDU = NU / 2;
+    constexpr int PAIR = OUT ? 8 * ((U + 1) % 2) + (U + 1) / 2 : U + 1;  // the next unit's fragment pair
+    if constexpr (U + 1 < NU) {
+      fa[(U + 1) % 2][0] = x3::lds_rd<(2 * PAIR) * 1024>(base);
+      fa[(U + 1) % 2][1] = x3::lds_rd<(2 * PAIR + 1) * 1024>(base);
+    } else {
+      e.nxt0 = x3::lds_rd<0>(nbase);
+      e.nxt1 = x3::lds_rd<1024>(nbase);
+    }
+    x3::lds_wait2<2>(fa[U % 2][0], fa[U % 2][1]);
+    constexpr int t = OUT ? U % 2 : U;
+    sfor<MT>([&](auto m) {
+      Out[m][t] = mfma16(fa[U % 2][0], Hl[m], Out[m][t]);
+      Out[m][t] = mfma16(fa[U % 2][1], Hh[m], Out[m][t]);
+      Out[m][t] = mfma16(fa[U % 2][0], Hh[m], Out[m][t]);
+    });
+    if constexpr (OUT) {
+      if constexpr (U % 2 == 1 && U / 2 + 1 < KQ) {
+        sfor<MT>([&](auto m) { act_pair(In, U / 2 + 1, m, vmax, Nh[m], Nl[m]); });
+        sfor<MT>([&](auto m) { Hh[m] = Nh[m], Hl[m] = Nl[m]; });
+      }
+    } else if constexpr (QK + 1 < KQ && U < MT) {
+      act_pair(In, QK + 1, std::integral_constant<int, U>{}, vmax, Nh[U], Nl[U]);
+    }
+    if constexpr (U == MIDU) {
+      wait_vmcnt<PPW>();
+      lds_barrier();
+      e.ring_target();
+    }
+    if constexpr (U > MIDU) mid_pieces_k<NU, U>(e);
+    units_k<MT, OUT, QK, NA, U + 1>(e, base, nbase, In, Out, Hh, Hl, Nh, Nl, fa, vmax);
+  }
+}
+template <int MT, bool OUT, int QK, int NA>
+__device__ __forceinline__ void chunk_k(EngK& e, const f32x4 (&In)[MT][ST], f32x4 (&Out)[MT][NA], u32x4 (&Hh)[MT],
+                                        u32x4 (&Hl)[MT], float (&vmax)[MT]) {
+  lds_cptr nb;
+  const lds_cptr b = e.take(nb);
+  u32x4 fa[2][2], Nh[MT], Nl[MT];
+  fa[0][0] = e.nxt0, fa[0][1] = e.nxt1;
+  units_k<MT, OUT, QK, NA>(e, b, nb, In, Out, Hh, Hl, Nh, Nl, fa, vmax);
+  x3::lds_wait2<0>(e.nxt0, e.nxt1);
+  if constexpr (!OUT && QK + 1 < KQ) sfor<MT>([&](auto m) { Hh[m] = Nh[m], Hl[m] = Nl[m]; });
+}
+// a 256 -> 256 hidden layer, k-major: In (the previous layer's pre-activations) -> Out (bias first)
+template <int MT, int QK = 0>
+__device__ __forceinline__ void hidden_k(EngK& e, const f32x4 (&In)[MT][ST], f32x4 (&Out)[MT][ST], u32x4 (&Hh)[MT],
+                                         u32x4 (&Hl)[MT], float (&vmax)[MT]) {
+  if constexpr (QK < KQ) {
+    chunk_k<MT, false, QK, ST>(e, In, Out, Hh, Hl, vmax);
+    hidden_k<MT, QK + 1>(e, In, Out, Hh, Hl, vmax);
+  }
+}
+
+template <int MT, int O, typename Act>
+__device__ __forceinline__ void l1_step_mt(lds_cptr la, lds_cptr lb, u32x4 (&fa)[3], u32x4 (&fb)[3],
+                                           const u32x4 (&b)[MT], const Act& act) {
+  if constexpr (O < ST) {
+    if constexpr (O + 2 < ST) fa[(O + 2) % 3] = x3::lds_rd<(O + 2) * 512>(la), fb[(O + 2) % 3] = x3::lds_rd<(O + 2) * 64>(lb);
+    x3::lds_wait2<(O + 2 < ST) ? 4 : ((O + 1 < ST) ? 2 : 0)>(fa[O % 3], fb[O % 3]);
+    sfor<MT>([&](auto m) {
+      act(mfma16(fa[O % 3], b[m], __builtin_bit_cast(f32x4, fb[O % 3])), std::integral_constant<int, O>{}, m);
+    });
+    l1_step_mt<MT, O + 1>(la, lb, fa, fb, b, act);
+  }
+}
+
+// the surrogate's forward pass for MT tiles (tile m's chains hold x[m]): output rows f[m] (tiles 0, 1). The same
+// products, in the same order per output, as mh_x3_kernel's one-tile m-major pass: the results are bit-identical.
+// the LDS base as an opaque value: the bias reads below are loop-invariant to the compiler, which otherwise keeps all
+// 50 bias tiles of the pass in registers across the step loop (200 VGPRs: the spills of the first multi-tile build)
+__device__ __forceinline__ const char* opaque(const char* p) {
+  asm volatile("" : "+s"(p));
+  return p;
+}
+__device__ __forceinline__ f32x4 bias4_at(const char* l, int off_bytes, int tile, int g) {
+  return *(const f32x4*)(l + off_bytes + (16 * tile + 4 * g) * 4);
+}
+
+template <int MT>
+__device__ __forceinline__ void sur_forward_mt(EngK& e, const float (&x)[MT][3], int g, float (&vmax)[MT],
+                                               f32x4 (&f)[MT][2]) {
+  f32x4 P[MT][ST], Q[MT][ST];
+  {  // layer 1, resident: one MFMA per tile and chain tile, pre-activations into P
+    u32x4 b[MT];
+    sfor<MT>([&](auto m) { b[m] = l1_b<3>(x[m], g); });
+    const lds_cptr la = (lds_cptr)(e.lds + SL1 + (e.lane & 31) * 16);
+    const lds_cptr lb = (lds_cptr)(e.lds + SB + 16 * e.g);
+    u32x4 fa[3], fb[3];
+    fa[0] = x3::lds_rd<0>(la), fb[0] = x3::lds_rd<0>(lb);
+    fa[1] = x3::lds_rd<512>(la), fb[1] = x3::lds_rd<64>(lb);
+    l1_step_mt<MT, 0>(la, lb, fa, fb, b, [&](const f32x4& z, auto o, auto m) { P[m][o] = z; });
+  }
+  u32x4 Hh[MT], Hl[MT];
+  sfor<MT>([&](auto m) { act_pair(P, 0, m, vmax, Hh[m], Hl[m]); });
+  {
+    const char* l = opaque(e.lds);
+    sfor<ST>([&](auto t) {
+      const f32x4 b = bias4_at(l, SB + W * 4, t, g);
+      sfor<MT>([&](auto m) { Q[m][t] = b; });
+    });
+  }
+  hidden_k<MT>(e, P, Q, Hh, Hl, vmax);
+  sfor<MT>([&](auto m) { act_pair(Q, 0, m, vmax, Hh[m], Hl[m]); });
+  {
+    const char* l = opaque(e.lds);
+    sfor<ST>([&](auto t) {
+      const f32x4 b = bias4_at(l, SB + 2 * W * 4, t, g);
+      sfor<MT>([&](auto m) { P[m][t] = b; });
+    });
+  }
+  hidden_k<MT>(e, Q, P, Hh, Hl, vmax);
+  sfor<MT>([&](auto m) { act_pair(P, 0, m, vmax, Hh[m], Hl[m]); });
+  {
+    const char* l = opaque(e.lds);
+    sfor<2>([&](auto t) {
+      const f32x4 b = bias4_at(l, SB + 3 * W * 4, t, g);
+      sfor<MT>([&](auto m) { f[m][t] = b; });
+    });
+  }
+  chunk_k<MT, true, 0, 2>(e, P, f, Hh, Hl, vmax);
+}
+
 __global__ void __launch_bounds__(NW * 64, 1) mh_x3_kernel(MhX3Params p) {
   __shared__ __attribute__((aligned(16))) char lds[TOTAL];
   const int lane = threadIdx.x & 63;
@@ -729,6 +974,90 @@ __global__ void __launch_bounds__(NW * 64, 1) mh_x3_kernel(MhX3Params p) {
   }
 }
 
+// mh_x3_kernel on the k-major multi-tile engine: 16 MT chains per wave, tile m's chain j at 64 MT block + 16 (MT w + m)
+// + j; per chain the same RNG stream, proposals, energy and acceptance test as mh_x3_kernel
+template <int MT>
+__global__ void __launch_bounds__(NW * 64, 1) mh_x3_mt_kernel(MhX3Params p) {
+  __shared__ __attribute__((aligned(16))) char lds[TOTAL];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, j = lane & 15;
+  const int yi = blockIdx.y;
+  long long c_local[MT];
+  bool valid[MT];
+  sfor<MT>([&](auto m) {
+    c_local[m] = (long long)blockIdx.x * (NW * 16 * MT) + (MT * w + m) * 16 + j;
+    valid[m] = c_local[m] < p.n_chains;
+  });
+  EngK e{lds, p.simg, 0, 0, 0, w, lane, g};
+  {
+    const uint4* s2 = (const uint4*)p.sl1;
+    uint4* d2 = (uint4*)(lds + SL1);
+    for (int i = threadIdx.x; i < ST * 32; i += NW * 64) d2[i] = s2[(i >> 5) * 64 + (i & 31)];
+    float* sb = (float*)(lds + SB);
+    for (int i = threadIdx.x; i < 3 * W + 32; i += NW * 64) sb[i] = p.sbias[i];
+    float* yo = (float*)(lds + YO);
+    for (int i = threadIdx.x; i < 32; i += NW * 64) yo[i] = i < kSurYdim ? p.y[(size_t)yi * kSurYdim + i] : 0.0f;
+    __syncthreads();
+    e.start_mid();
+  }
+  const float* ylds = (const float*)(lds + YO);
+  Rng rng[MT];
+  float x[MT][3];
+  bool oor = false;
+  sfor<MT>([&](auto m) {
+    rng[m] = rng_init(p.seed, (uint64_t)(p.chain_offset + c_local[m]), (uint64_t)yi);
+    const long long cc = valid[m] ? c_local[m] : 0;
+    if (p.x_init) {
+#pragma unroll
+      for (int d = 0; d < 3; ++d) x[m][d] = p.x_init[((size_t)yi * p.n_chains + cc) * 3 + d];
+    } else {  // torch.rand(n, 3) * 2 - 1 (generate_scatterometry_ground_truth.py:27)
+#pragma unroll
+      for (int d = 0; d < 3; ++d) x[m][d] = (float)(rng_next(rng[m]) >> 8) * 0x1p-24f * 2.0f - 1.0f;
+    }
+#pragma unroll
+    for (int d = 0; d < 3; ++d) oor |= valid[m] && beyond_fp16(x[m][d]);
+  });
+  float vmax[MT];
+  sfor<MT>([&](auto m) { vmax[m] = 0.0f; });
+  f32x4 f[MT][2];
+  sur_forward_mt<MT>(e, x, g, vmax, f);
+  float e0[MT], e_cur[MT];
+  sfor<MT>([&](auto m) { e_cur[m] = e0[m] = mh_energy(f[m], ylds, x[m], p.a, p.b2, p.lam, g); });
+  for (int s = 0; s < p.num_steps; ++s) {
+    float xp[MT][3], u[MT];
+    sfor<MT>([&](auto m) {
+      float xi[3];
+      rng_normals<3>(rng[m], xi);
+      u[m] = (float)(rng_next(rng[m]) >> 8) * 0x1p-24f;
+#pragma unroll
+      for (int d = 0; d < 3; ++d) {
+        xp[m][d] = x[m][d] + p.noise_std * xi[d];
+        oor |= valid[m] && beyond_fp16(xp[m][d]);
+      }
+    });
+    sur_forward_mt<MT>(e, xp, g, vmax, f);
+    sfor<MT>([&](auto m) {
+      const float e_prop = mh_energy(f[m], ylds, xp[m], p.a, p.b2, p.lam, g);
+      const bool acc = u[m] < expf(-e_prop + e_cur[m]);
+#pragma unroll
+      for (int d = 0; d < 3; ++d) x[m][d] = acc ? xp[m][d] : x[m][d];
+      e_cur[m] = acc ? e_prop : e_cur[m];
+    });
+  }
+  wait_vmcnt<0>();  // the prefetched chunks of a step that never ran land before the workgroup exits
+  sfor<MT>([&](auto m) { oor |= valid[m] && !(vmax[m] <= 65504.0f); });
+  x3::report_range(oor, p.err, lane);
+  sfor<MT>([&](auto m) {
+    if (valid[m] && g == 0) {
+      float* dst = p.x_out + ((size_t)yi * p.n_chains + c_local[m]) * 3;
+#pragma unroll
+      for (int d = 0; d < 3; ++d) dst[d] = x[m][d];
+      if (p.e_out) p.e_out[(size_t)yi * p.n_chains + c_local[m]] = e_cur[m] - e0[m];
+    }
+  });
+}
+
 // the per-step coefficients: (tau, beta, g, 0), (mean_weight, var, 0, 0) -- the device functions every sampler uses
 __global__ void dps_x3_coef_kernel(float4* coef, int S, float T, float bmin, float bdiff) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -743,9 +1072,22 @@ __global__ void dps_x3_coef_kernel(float4* coef, int S, float T, float bmin, flo
 }  // namespace dx3
 
 hipError_t launch_mh_x3(const MhX3Params& p, int n_y, hipStream_t st) {
-  const long long per_wg = dx3::NW * 16;
+  static const int mt = [] {
+    // A/B knob: 1 = the one-tile m-major kernel, 2 (default) or 3 tiles k-major -- all three bit-identical.
+    // Same box, 10 x 30k x 1000 (profiles/r5_mh_mt/): 232 / 204 / 229 ms (MT = 3 spills 156 B and its 192-chain
+    // workgroups leave a longer tail)
+    const char* v = getenv("DMIP_MH_MT");
+    const int n = v ? atoi(v) : 2;
+    return n == 1 || n == 3 ? n : 2;
+  }();
+  const long long per_wg = dx3::NW * 16 * mt;
   const dim3 grid((unsigned)((p.n_chains + per_wg - 1) / per_wg), (unsigned)n_y), block(dx3::NW * 64);
-  hipLaunchKernelGGL(dx3::mh_x3_kernel, grid, block, 0, st, p);
+  if (mt == 1)
+    hipLaunchKernelGGL(dx3::mh_x3_kernel, grid, block, 0, st, p);
+  else if (mt == 2)
+    hipLaunchKernelGGL(dx3::mh_x3_mt_kernel<2>, grid, block, 0, st, p);
+  else
+    hipLaunchKernelGGL(dx3::mh_x3_mt_kernel<3>, grid, block, 0, st, p);
   return hipGetLastError();
 }
 
