@@ -145,6 +145,21 @@ def test_mh_product_rng_vs_oracle(dmip, golden, fm, precision):
     assert same.mean() >= 0.95, same.mean()
 
 
+@pytest.mark.parametrize("n", [1, 17, 129, 257])
+def test_mh_fp32x3_ragged_chain_counts_vs_oracle(dmip, golden, fm, n):
+    """The multi-tile MH kernel (two 16-chain tiles per wave, 128 chains per workgroup) on chain counts that leave
+    partial tiles and idle waves, over two ys: chain by chain against the oracle (30 steps)."""
+    model, pr, params = fm
+    ys = golden("data_scat.npz")["y_test"][7:9]
+    x = pr.mh_sample(model, {"a": 0.2, "b": 0.01, "lambd_bd": 1000}, torch.from_numpy(ys), n, 30, 0.5, seed=n,
+                     precision="fp32x3").cpu().numpy()
+    assert x.shape == (2, n, 3) and np.all(np.isfinite(x))
+    for k in range(2):
+        ref, _ = O.mh_sample(params, ys[k], 30, 0.5, seed=n, n_chains=n, stream=k)
+        same = np.all(np.abs(x[k] - ref) <= 1e-5, axis=1)
+        assert same.mean() >= (0.95 if n >= 17 else 1.0), (k, same.mean())
+
+
 def test_mh_fp32x3_vs_exact_f32_chains(dmip, golden, fm):
     """fp32x3 against the exact-f32 kernel on 4 ys x 4096 chains x 200 steps from given starts: the same final
     state on >= 95% of chains, and there the energy change E(x_S) - E(x_0) agrees to 1e-3 relative + 2e-3."""
