@@ -220,17 +220,28 @@ __device__ __forceinline__ void store_pair(const float (&a)[4], int o, u32x4 (&O
 }
 
 __device__ __forceinline__ bool beyond_fp16(float v) { return !(__builtin_fabsf(v) <= 65504.0f); }
-// the running max |v| of the values a chain splits (RangeMax::mx, checked once at the end: a value beyond fp16's range
-// is finite and > 65504 or inf when it first appears -- what follows from it may be NaN, which max ignores, but the max
-// has seen the first one); one v_max3 per two values instead of a compare and a mask OR per value
-__device__ __forceinline__ void track4(float& mx, const float (&v)[4]) {
-  mx = fmaxf(fmaxf(mx, __builtin_fabsf(v[0])), __builtin_fabsf(v[1]));
-  mx = fmaxf(fmaxf(mx, __builtin_fabsf(v[2])), __builtin_fabsf(v[3]));
-  // pinned: otherwise the compiler re-associates a whole pass's max chain into one tree at its end and keeps every
-  // tracked value alive until then (DPS: 176 B of scratch and 55 more AGPRs; the multi-tile MH engine: hundreds of
-  // spilled registers)
+// the running max |v| of the values a chain splits, checked once at the end (range_bad): a value beyond fp16's range
+// is finite and > 65504 or inf when it first appears -- what follows from it may be NaN, but the max has seen the
+// first one. Kept as float bits in a signed int: for non-negative floats the integer order is the float order, and
+// v_max3_i32 needs none of the NaN-quieting v_max a float max inserts before each operand; |v| is v's bits with the
+// sign cleared (a NaN then sorts above inf). Pinned by an empty asm: otherwise the compiler re-associates a whole
+// pass's max chain into one tree at its end and keeps every tracked value alive until then (DPS: 176 B of scratch and
+// 55 more AGPRs; the multi-tile MH engine: hundreds of spilled registers)
+__device__ __forceinline__ void track4(int& mx, const float (&v)[4]) {  // any sign
+  constexpr int M = 0x7fffffff;
+  mx = max(max(mx, __float_as_int(v[0]) & M), __float_as_int(v[1]) & M);
+  mx = max(max(mx, __float_as_int(v[2]) & M), __float_as_int(v[3]) & M);
   asm("" : "+v"(mx));
 }
+__device__ __forceinline__ void track4_pos(int& mx, const float (&v)[4]) {  // v >= +0 (relu outputs)
+  mx = max(max(mx, __float_as_int(v[0])), __float_as_int(v[1]));
+  mx = max(max(mx, __float_as_int(v[2])), __float_as_int(v[3]));
+  asm("" : "+v"(mx));
+}
+__device__ __forceinline__ bool range_bad(int mx) { return !(__int_as_float(mx) <= 65504.0f); }
+// relu on the bits (v_max_i32 with 0; the float select costs a NaN-quieting v_max more): z > 0 passes, every other
+// value (-0 and the negative NaNs included) becomes +0
+__device__ __forceinline__ float relu_bits(float z) { return __int_as_float(max(__float_as_int(z), 0)); }
 
 // The per-tile epilogues of a 256 -> 256 layer (tile o of the layer's output, f32 pre-activations z):
 //   PriorFwd:  r = 1 / (1 + 2^z) (z pre-scaled by 2 log2 e; the next layer is folded for r), D = 4 r (1 - r)
@@ -250,22 +261,22 @@ struct EpiPriorFwd {
 };
 struct EpiSurFwd {
   uint32_t* m;  // [2]: bit 4 (o & 7) + k of word o >> 3
-  float* mx;
+  int* mx;
   __device__ __forceinline__ void operator()(const f32x4& z, int o, u32x4 (&Oh)[KQ], u32x4 (&Ol)[KQ]) const {
     float h[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const bool pos = z[k] > 0.0f;
+      const bool pos = z[k] > 0.0f;  // (the float select here: relu_bits plus a separate mask compare spills)
       h[k] = pos ? z[k] : 0.0f;
       m[o >> 3] |= (pos ? 1u : 0u) << ((o & 7) * 4 + k);
     }
-    track4(*mx, h);
+    track4_pos(*mx, h);
     store_pair(h, o, Oh, Ol);
   }
 };
 struct EpiBackD {
   const float (*D)[4];
-  float* mx;
+  int* mx;
   __device__ __forceinline__ void operator()(const f32x4& z, int o, u32x4 (&Oh)[KQ], u32x4 (&Ol)[KQ]) const {
     float v[4];
 #pragma unroll
@@ -280,7 +291,7 @@ struct EpiBackL1 {
   const char* lds;
   int lane, g;
   u32x4 b1;
-  float* mx;
+  int* mx;
   __device__ __forceinline__ void operator()(const f32x4& z, int o, u32x4 (&Oh)[KQ], u32x4 (&Ol)[KQ]) const {
     const u32x4 a = *(const u32x4*)(lds + PL1 + o * 512 + (lane & 31) * 16);
     const f32x4 c = *(const f32x4*)(lds + PB + (16 * o + 4 * g) * 4);
@@ -298,7 +309,7 @@ struct EpiBackL1 {
 };
 struct EpiBackMask {
   const uint32_t* m;
-  float* mx;
+  int* mx;
   __device__ __forceinline__ void operator()(const f32x4& z, int o, u32x4 (&Oh)[KQ], u32x4 (&Ol)[KQ]) const {
     float v[4];
 #pragma unroll
@@ -459,7 +470,7 @@ __global__ void __launch_bounds__(NW * 64, 1) dps_x3_kernel(DpsX3Params p) {
     for (int d = 0; d < 3; ++d) x[d] = __fadd_rn(__fmul_rn(n0[d], p.stdv), p.mean);
   }
   bool oor = false;
-  float vmax = 0.0f;  // track4's running max of the split values
+  int vmax = 0;  // track4's running max of the split values (float bits)
   const int S = p.num_steps;
   for (int i = 0; i < S; ++i) {
     const float4 c4 = ((const float4*)p.coef)[2 * i];      // tau, beta, g (dmip_device.h step_coef)
@@ -505,7 +516,7 @@ __global__ void __launch_bounds__(NW * 64, 1) dps_x3_kernel(DpsX3Params p) {
         h[k] = pos ? z[k] : 0.0f;
         m1[o >> 3] |= (pos ? 1u : 0u) << ((o & 7) * 4 + k);
       }
-      track4(vmax, h);
+      track4_pos(vmax, h);
       store_pair(h, o, Ah, Al);
     });
     layer256(e, Ah, Al, SB + W * 4, EpiSurFwd{m2, &vmax}, Bh, Bl);
@@ -610,7 +621,7 @@ __global__ void __launch_bounds__(NW * 64, 1) dps_x3_kernel(DpsX3Params p) {
     }
   }
   wait_vmcnt<0>();  // the prefetched chunks of a step that never ran land before the workgroup exits
-  x3::report_range((oor || !(vmax <= 65504.0f)) && valid, p.err, lane);
+  x3::report_range((oor || range_bad(vmax)) && valid, p.err, lane);
   if (valid && g == 0) {
     float* dst = p.x_out + ((size_t)yi * p.n_chains + c_local) * 3;
 #pragma unroll
@@ -655,14 +666,14 @@ __device__ __forceinline__ float mh_energy(const f32x4 (&f)[2], const float* y, 
 }
 
 // the surrogate's forward pass at x (every lane of the chain holds x): output rows f (tiles 0, 1), range flag
-__device__ __forceinline__ void sur_forward(Eng& e, const float (&x)[3], int g, float& vmax, f32x4 (&f)[2]) {
+__device__ __forceinline__ void sur_forward(Eng& e, const float (&x)[3], int g, int& vmax, f32x4 (&f)[2]) {
   u32x4 Ah[KQ], Al[KQ], Bh[KQ], Bl[KQ];
   uint32_t m2[2] = {0u, 0u}, m3[2] = {0u, 0u};
   layer1(e, SL1, SB, l1_b<3>(x, g), [&](const f32x4& z, int o) {
     float h[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) h[k] = z[k] > 0.0f ? z[k] : 0.0f;
-    track4(vmax, h);
+    for (int k = 0; k < 4; ++k) h[k] = relu_bits(z[k]);
+    track4_pos(vmax, h);
     store_pair(h, o, Ah, Al);
   });
   layer256(e, Ah, Al, SB + W * 4, EpiSurFwd{m2, &vmax}, Bh, Bl);
@@ -755,18 +766,21 @@ __device__ __forceinline__ void mid_pieces_k(const EngK& e) {
   }
 }
 // k-step q's B operand pair of tile m from the previous layer's pre-activations In[m][2q], In[m][2q + 1] (store_pair's
-// dword order): relu, the running max (track4), the split
+// dword order): relu, the running max (track4_pos's, over the pre-activations: a negative one sorts below the +0 its
+// relu gives), the split
 template <int MT, typename M>
-__device__ __forceinline__ void act_pair(const f32x4 (&In)[MT][ST], int q, M m, float (&vmax)[MT], u32x4& nh,
+__device__ __forceinline__ void act_pair(const f32x4 (&In)[MT][ST], int q, M m, int (&vmax)[MT], u32x4& nh,
                                          u32x4& nl) {
   float a[4], b[4];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    a[k] = In[m][2 * q][k] > 0.0f ? In[m][2 * q][k] : 0.0f;
-    b[k] = In[m][2 * q + 1][k] > 0.0f ? In[m][2 * q + 1][k] : 0.0f;
-  }
-  track4(vmax[m], a);
-  track4(vmax[m], b);
+  for (int k = 0; k < 4; ++k) a[k] = relu_bits(In[m][2 * q][k]), b[k] = relu_bits(In[m][2 * q + 1][k]);
+  int v = vmax[m];
+  v = max(max(v, __float_as_int(In[m][2 * q][0])), __float_as_int(In[m][2 * q][1]));
+  v = max(max(v, __float_as_int(In[m][2 * q][2])), __float_as_int(In[m][2 * q][3]));
+  v = max(max(v, __float_as_int(In[m][2 * q + 1][0])), __float_as_int(In[m][2 * q + 1][1]));
+  v = max(max(v, __float_as_int(In[m][2 * q + 1][2])), __float_as_int(In[m][2 * q + 1][3]));
+  asm("" : "+v"(v));  // pinned (track4)
+  vmax[m] = v;
   uint32_t h0, l0, h1, l1, h2, l2, h3, l3;
   x3::split_pair(a[0], a[1], h0, l0);
   x3::split_pair(a[2], a[3], h1, l1);
@@ -782,7 +796,7 @@ __device__ __forceinline__ void act_pair(const f32x4 (&In)[MT][ST], int q, M m, 
 template <int MT, bool OUT, int QK, int NA, int U = 0>
 __device__ __forceinline__ void units_k(EngK& e, lds_cptr base, lds_cptr nbase, const f32x4 (&In)[MT][ST],
                                         f32x4 (&Out)[MT][NA], u32x4 (&Hh)[MT], u32x4 (&Hl)[MT], u32x4 (&Nh)[MT],
-                                        u32x4 (&Nl)[MT], u32x4 (&fa)[2][2], float (&vmax)[MT]) {
+                                        u32x4 (&Nl)[MT], u32x4 (&fa)[2][2], int (&vmax)[MT]) {
   constexpr int NU = 16;
   if constexpr (U < NU) {
     constexpr int MIDU = NU / 2;
@@ -820,7 +834,7 @@ __device__ __forceinline__ void units_k(EngK& e, lds_cptr base, lds_cptr nbase, 
 }
 template <int MT, bool OUT, int QK, int NA>
 __device__ __forceinline__ void chunk_k(EngK& e, const f32x4 (&In)[MT][ST], f32x4 (&Out)[MT][NA], u32x4 (&Hh)[MT],
-                                        u32x4 (&Hl)[MT], float (&vmax)[MT]) {
+                                        u32x4 (&Hl)[MT], int (&vmax)[MT]) {
   lds_cptr nb;
   const lds_cptr b = e.take(nb);
   u32x4 fa[2][2], Nh[MT], Nl[MT];
@@ -832,7 +846,7 @@ __device__ __forceinline__ void chunk_k(EngK& e, const f32x4 (&In)[MT][ST], f32x
 // a 256 -> 256 hidden layer, k-major: In (the previous layer's pre-activations) -> Out (bias first)
 template <int MT, int QK = 0>
 __device__ __forceinline__ void hidden_k(EngK& e, const f32x4 (&In)[MT][ST], f32x4 (&Out)[MT][ST], u32x4 (&Hh)[MT],
-                                         u32x4 (&Hl)[MT], float (&vmax)[MT]) {
+                                         u32x4 (&Hl)[MT], int (&vmax)[MT]) {
   if constexpr (QK < KQ) {
     chunk_k<MT, false, QK, ST>(e, In, Out, Hh, Hl, vmax);
     hidden_k<MT, QK + 1>(e, In, Out, Hh, Hl, vmax);
@@ -865,7 +879,7 @@ __device__ __forceinline__ f32x4 bias4_at(const char* l, int off_bytes, int tile
 }
 
 template <int MT>
-__device__ __forceinline__ void sur_forward_mt(EngK& e, const float (&x)[MT][3], int g, float (&vmax)[MT],
+__device__ __forceinline__ void sur_forward_mt(EngK& e, const float (&x)[MT][3], int g, int (&vmax)[MT],
                                                f32x4 (&f)[MT][2]) {
   f32x4 P[MT][ST], Q[MT][ST];
   {  // layer 1, resident: one MFMA per tile and chain tile, pre-activations into P
@@ -941,7 +955,7 @@ __global__ void __launch_bounds__(NW * 64, 1) mh_x3_kernel(MhX3Params p) {
     for (int d = 0; d < 3; ++d) x[d] = (float)(rng_next(rng) >> 8) * 0x1p-24f * 2.0f - 1.0f;
   }
   bool oor = false;
-  float vmax = 0.0f;  // track4's running max of the split values
+  int vmax = 0;  // track4's running max of the split values (float bits)
   for (int d = 0; d < 3; ++d) oor |= beyond_fp16(x[d]);
   f32x4 f[2];
   sur_forward(e, x, g, vmax, f);
@@ -965,7 +979,7 @@ __global__ void __launch_bounds__(NW * 64, 1) mh_x3_kernel(MhX3Params p) {
     e_cur = acc ? e_prop : e_cur;
   }
   wait_vmcnt<0>();  // the prefetched chunks of a step that never ran land before the workgroup exits
-  x3::report_range((oor || !(vmax <= 65504.0f)) && valid, p.err, lane);
+  x3::report_range((oor || range_bad(vmax)) && valid, p.err, lane);
   if (valid && g == 0) {
     float* dst = p.x_out + ((size_t)yi * p.n_chains + c_local) * 3;
 #pragma unroll
@@ -1018,8 +1032,8 @@ __global__ void __launch_bounds__(NW * 64, 1) mh_x3_mt_kernel(MhX3Params p) {
 #pragma unroll
     for (int d = 0; d < 3; ++d) oor |= valid[m] && beyond_fp16(x[m][d]);
   });
-  float vmax[MT];
-  sfor<MT>([&](auto m) { vmax[m] = 0.0f; });
+  int vmax[MT];  // act_pair's running max (float bits)
+  sfor<MT>([&](auto m) { vmax[m] = 0; });
   f32x4 f[MT][2];
   sur_forward_mt<MT>(e, x, g, vmax, f);
   float e0[MT], e_cur[MT];
@@ -1046,7 +1060,7 @@ __global__ void __launch_bounds__(NW * 64, 1) mh_x3_mt_kernel(MhX3Params p) {
     });
   }
   wait_vmcnt<0>();  // the prefetched chunks of a step that never ran land before the workgroup exits
-  sfor<MT>([&](auto m) { oor |= valid[m] && !(vmax[m] <= 65504.0f); });
+  sfor<MT>([&](auto m) { oor |= valid[m] && range_bad(vmax[m]); });
   x3::report_range(oor, p.err, lane);
   sfor<MT>([&](auto m) {
     if (valid[m] && g == 0) {
