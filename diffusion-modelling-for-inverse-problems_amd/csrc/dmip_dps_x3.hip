@@ -1086,14 +1086,27 @@ __global__ void dps_x3_coef_kernel(float4* coef, int S, float T, float bmin, flo
 }  // namespace dx3
 
 hipError_t launch_mh_x3(const MhX3Params& p, int n_y, hipStream_t st) {
-  static const int mt = [] {
-    // A/B knob: 1 = the one-tile m-major kernel, 2 (default) or 3 tiles k-major -- all three bit-identical.
-    // Same box, 10 x 30k x 1000 (profiles/r5_mh_mt/): 232 / 204 / 229 ms (MT = 3 spills 156 B and its 192-chain
-    // workgroups leave a longer tail)
+  // DMIP_MH_MT (A/B knob): 1 = the one-tile m-major kernel, 2 or 3 tiles k-major -- all three bit-identical. Unset:
+  // 2 or 3 by the workgroup rounds each leaves on the CUs (one workgroup per CU). Same box (profiles/r5_mh_mt/,
+  // r5_mh_rows/): a 3-tile workgroup takes 1.45x a 2-tile one (100 rows x 30k: 359 vs 371 ms), so 3 tiles win once
+  // their rounds are full -- 10 rows x 30k x 1000: MT = 2 204 ms (10 rounds) against 229 ms (7 rounds of 192-chain
+  // workgroups); 1000 rows: MT = 3
+  static const int forced = [] {
     const char* v = getenv("DMIP_MH_MT");
-    const int n = v ? atoi(v) : 2;
-    return n == 1 || n == 3 ? n : 2;
+    const int n = v ? atoi(v) : 0;
+    return n >= 1 && n <= 3 ? n : 0;
   }();
+  int mt = forced;
+  if (!mt) {
+    int n_cu = 256;
+    (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, stream_device(st));
+    if (n_cu < 1) n_cu = 256;
+    auto rounds = [&](int t) {
+      const long long wg = (p.n_chains + dx3::NW * 16 * t - 1) / (dx3::NW * 16 * t) * n_y;
+      return (double)((wg + n_cu - 1) / n_cu);
+    };
+    mt = rounds(3) * 1.45 < rounds(2) ? 3 : 2;
+  }
   const long long per_wg = dx3::NW * 16 * mt;
   const dim3 grid((unsigned)((p.n_chains + per_wg - 1) / per_wg), (unsigned)n_y), block(dx3::NW * 64);
   if (mt == 1)

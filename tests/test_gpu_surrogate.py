@@ -160,6 +160,20 @@ def test_mh_fp32x3_ragged_chain_counts_vs_oracle(dmip, golden, fm, n):
         assert same.mean() >= (0.95 if n >= 17 else 1.0), (k, same.mean())
 
 
+def test_mh_fp32x3_three_tile_launch_matches_two_tile(dmip, golden, fm):
+    """300 rows x 1920 chains: the launcher picks three tiles per wave on a 256-CU MI355X (12 full workgroup rounds
+    against 18 for two); rows 0 and 1 must equal a 2-row launch of the same ys (two tiles, few rounds) bit for bit --
+    the RNG stream is the row index and the variants compute the same products in the same order."""
+    model, pr, _ = fm
+    prm = {"a": 0.2, "b": 0.01, "lambd_bd": 1000}
+    y = torch.from_numpy(golden("data_scat.npz")["y_test"])
+    ys = y[torch.arange(300) % y.shape[0]]
+    big = pr.mh_sample(model, prm, ys, 1920, 20, 0.5, seed=31, precision="fp32x3")
+    small = pr.mh_sample(model, prm, ys[:2], 1920, 20, 0.5, seed=31, precision="fp32x3")
+    assert torch.equal(big[:2], small)
+    assert torch.isfinite(big).all()
+
+
 def test_mh_fp32x3_vs_exact_f32_chains(dmip, golden, fm):
     """fp32x3 against the exact-f32 kernel on 4 ys x 4096 chains x 200 steps from given starts: the same final
     state on >= 95% of chains, and there the energy change E(x_S) - E(x_0) agrees to 1e-3 relative + 2e-3."""

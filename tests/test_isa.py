@@ -66,10 +66,10 @@ def test_bf16_samplers_have_no_scratch(isa):
 # wave-uniform job and the lane id after the step loop) 3 dwords of schedule setup, stored and loaded only in the
 # segment setup -- none in the step loop.
 # The fp32x3 DPS and MH kernels: none since the running range max is pinned (round 5; it had kept every tracked value
-# alive, 176 B in DPS); the three-tile MH kernel (an A/B variant, DMIP_MH_MT=3) spills 156 B.
+# alive, 176 B in DPS); the three-tile MH kernel (launched when its workgroup rounds are full) spills 20 B.
 _SCRATCH_CAP = {"x3_sampler_kernel": 0, "x3k_sampler_kernel": 128, "loss_grad_kernel": 0, "x3p_sampler_kernel": 0,
                 "dps_x3_kernel": 0, "mh_x3_kernel": 0, "mh_x3_mt_kernel": 0}
-_SCRATCH_CAP_KERNEL = {"x3_sampler_kernelILi2ELi512ELi3ELi23E": 12, "mh_x3_mt_kernelILi3E": 160}
+_SCRATCH_CAP_KERNEL = {"x3_sampler_kernelILi2ELi512ELi3ELi23E": 12, "mh_x3_mt_kernelILi3E": 24}
 
 
 @pytest.mark.parametrize("family", list(_SCRATCH_CAP))
