@@ -122,6 +122,17 @@ def sample_checked(model, y, n, num_steps, mean, std, seed=None, chain_offset=0,
                                **dict(kw, precision="fp32"))
 
 
+def chains_sharded(n, run, seed, device):
+    """A chain-keyed kernel launched over all ranks (the MH ground truth, problems.generate_gt_samples): rank r calls
+    run(n_local, chain_offset, seed, agree) -> its (n_y, n_local, d) shard for its contiguous chain range, with the
+    common seed; every rank receives the (n_y, n, d) union, bit-identical to one launch of all n chains. `agree` is
+    any_rank, for a fallback decided by all ranks together (as sample_checked's)."""
+    rank, ws = world()
+    seed = common_seed(seed, device)
+    lo, hi = shard_range(n, rank, ws)
+    return gather_shards(run(hi - lo, lo, seed, any_rank), n, device)
+
+
 def map_sharded(n, fn, width):
     """Evaluate-style multi-y runs (shard over (y, chain) pairs): rank r computes
     `fn(i)` -> `width` floats for its contiguous range of the n items (each item = one y with all

@@ -202,13 +202,13 @@ class ScatterometryEnergy:
 
 
 def mh_sample(forward_model, params, ys, n_chains, num_steps, noise_std, seed=None, chain_offset=0, x_init=None,
-              noise=None, unif=None, return_ediff=False, precision="fp32"):
+              noise=None, unif=None, return_ediff=False, precision="fp32", agree=None):
     """Fused random-walk MH (dmip_mh_sample_ex) for every row of ys (n_y, 23): device tensor
     (n_y, n_chains, 3). x_init (n_y, n_chains, 3) or None for x0 ~ U[-1, 1]^3 from the chain RNG;
     noise (S, n_y, n_chains, 3) / unif (S, n_y, n_chains) replay captured draws (exact f32 only).
     precision "fp32": the exact-f32 kernel; "fp32x3": the surrogate's products as three-term fp16 splits (same
     RNG stream and acceptance test per chain) -- a weight, proposal or activation beyond fp16's range resamples
-    every chain with "fp32" (RuntimeWarning)."""
+    every chain with "fp32" (RuntimeWarning); `agree(flag) -> bool` makes that decision collective (parallel)."""
     from . import _lib
     ys = torch.as_tensor(ys)
     if not torch.cuda.is_available():
@@ -230,16 +230,20 @@ def mh_sample(forward_model, params, ys, n_chains, num_steps, noise_std, seed=No
     nz = _lib.scat_noise(params['a'], params['b'], params['lambd_bd'])
     x0 = prep(x_init)
     if precision == "fp32x3":
+        err = None
         try:
             _lib.clear_range_status(dev)
             _lib.mh_sample(h, nz, ys, n_chains, chain_offset, num_steps, noise_std, seed, out, x0, None, None, ed,
                            precision="fp32x3")
             _lib.device_status(dev)
-            return (out, ed) if return_ediff else out
         except (ValueError, RuntimeError) as e:
             if not _lib.is_range_error(e):
                 raise
-            warnings.warn(f"{e}; sampled with the exact-f32 engine instead", RuntimeWarning)
+            err = e
+        if not (agree(err is not None) if agree is not None else err is not None):
+            return (out, ed) if return_ediff else out
+        warnings.warn(f"{err or 'fp16 range (another rank)'}; sampled with the exact-f32 engine instead",
+                      RuntimeWarning)
     _lib.mh_sample(h, nz, ys, n_chains, chain_offset, num_steps, noise_std, seed, out, x0, prep(noise), prep(unif),
                    ed)
     return (out, ed) if return_ediff else out
@@ -275,13 +279,22 @@ def generate_gt_samples(forward_model, params, ys, out_dir=None, n_samples_x=300
                         noise_std=0.5, seed=None, precision="fp32"):
     """generate_scatterometry_ground_truth.py:26-63 on the device: for every y and repeat j,
     n_samples_x MH chains from U[-1, 1]^3 for metr_steps steps (NOISE_STD_MCMC, METR_STEPS of
-    config_scatterometry.yml), all in one launch (precision as mh_sample); optionally written as
-    out_dir/<i>/<j>.npy. Returns a device tensor (n_y, n_repeats, n_samples_x, 3)."""
+    config_scatterometry.yml), all in one launch (precision as mh_sample); under torch.distributed the chains
+    are sharded over the ranks (parallel.chains_sharded: every rank gets the whole, bit-identical to one GPU; rank 0
+    writes the files); optionally written as out_dir/<i>/<j>.npy. Returns a device tensor (n_y, n_repeats, n_samples_x, 3)."""
+    from . import parallel
     ys = torch.as_tensor(ys, dtype=torch.float32).reshape(-1, 23)
     rows = ys.repeat_interleave(n_repeats, dim=0)
-    x = mh_sample(forward_model, params, rows, n_samples_x, metr_steps, noise_std, seed=seed, precision=precision)
+    if not torch.cuda.is_available():
+        raise RuntimeError("dmip: MH sampling needs a HIP device (fused kernel; there is no CPU path)")
+    if seed is None:
+        seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+    dev = ys.device if ys.is_cuda else torch.device("cuda", torch.cuda.current_device())
+    run = lambda n, off, s, agree: mh_sample(forward_model, params, rows, n, metr_steps, noise_std, seed=s,
+                                             chain_offset=off, precision=precision, agree=agree)
+    x = parallel.chains_sharded(n_samples_x, run, seed, dev)  # one process: a single launch of all chains
     x = x.reshape(ys.shape[0], n_repeats, n_samples_x, 3)
-    if out_dir:
+    if out_dir and parallel.world()[0] == 0:
         xh = x.cpu().numpy()
         for i in range(ys.shape[0]):
             d = os.path.join(out_dir, str(i))

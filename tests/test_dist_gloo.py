@@ -196,3 +196,59 @@ def test_range_fallback_is_decided_by_all_ranks(bad):
         assert (out[:, 0] == torch.arange(n).numpy()).all()
         assert (out == one).all(), r                      # the 1-rank run, bit for bit
         assert n_warn == (1 if bad < n else 0), r          # every rank resampled (and said so), or none did
+
+
+def _gt_worker(rank, world, port, n, bad, q):
+    """parallel.chains_sharded as generate_gt_samples drives it: a chain-keyed MH stand-in (rows = (y, repeat)
+    pairs, output a pure function of (seed, global chain, row)) whose fp32x3 launch reports a range error when
+    its shard holds a chain >= bad; mh_sample's fallback is decided through `agree`."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import importlib
+    import warnings
+    par = importlib.import_module("diffusion-modelling-for-inverse-problems_amd.parallel")
+    torch.manual_seed(3 + rank)
+    local_seed = int(torch.randint(0, 2 ** 40, (1,)).item())
+
+    def run(n_local, off, seed, agree):
+        err = off + n_local > bad  # this rank's fp32x3 launch reported the range
+        engine = 1.0 if agree(err) else 0.0  # every rank falls back if any rank's shard did
+        c = torch.arange(off, off + n_local, dtype=torch.float32)
+        rows = torch.arange(4, dtype=torch.float32)[:, None].expand(4, n_local)
+        return torch.stack([c.expand(4, n_local), rows, c.expand(4, n_local) * 0 + float(seed % 997),
+                            c.expand(4, n_local) * 0 + engine], dim=2)
+
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        out = par.chains_sharded(n, run, local_seed, torch.device("cpu"))
+    q.put((rank, out.numpy()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n,bad", [(2, 1001, 10 ** 9), (3, 10, 10 ** 9), (2, 1, 10 ** 9), (2, 600, 450)])
+def test_ground_truth_chains_sharded(world, n, bad):
+    """The multi-GPU MH ground truth (problems.generate_gt_samples under torch.distributed): every rank receives
+    every (row, chain) exactly once, in order, from one seed and one engine."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if root not in sys.path:
+        sys.path.insert(0, root)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gt_worker, args=(r, world, port, n, bad, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref = res[0]
+    assert ref.shape == (4, n, 4)
+    assert (ref[:, :, 0] == torch.arange(n).numpy()[None]).all()     # every chain once, in order, per row
+    assert (ref[:, :, 1] == torch.arange(4).numpy()[:, None]).all()  # rows in order
+    assert len(set(ref[:, :, 2].ravel().tolist())) == 1                # one seed
+    assert (ref[:, :, 3] == (1.0 if bad < n else 0.0)).all()          # one engine for all chains
+    for r in range(1, world):
+        assert (res[r] == ref).all()
