@@ -690,8 +690,7 @@ __device__ __forceinline__ void sur_forward(Eng& e, const float (&x)[3], int g, 
 // where the m-major order (input and output operands live together, 128 registers a tile) does not. The chunk's
 // LDS reads and its share of the refill (the guide's 60-185 issue cycles per 1 KiB piece) are spread over MT times
 // the matrix work. Same ring and mid-chunk barrier protocol as mid_units; the output layer's chunk stays m-major.
-// compile-time loops (the per-tile register arrays must be indexed by constants from the start, before any unrolling,
-// or SROA leaves them in scratch)
+// compile-time loops over the tiles (the index is a constant in every body)
 template <typename F, int... I>
 __device__ __forceinline__ void sfor_impl(const F& f, std::integer_sequence<int, I...>) {
   (f(std::integral_constant<int, I>{}), ...);
@@ -868,16 +867,6 @@ __device__ __forceinline__ void l1_step_mt(lds_cptr la, lds_cptr lb, u32x4 (&fa)
 
 // the surrogate's forward pass for MT tiles (tile m's chains hold x[m]): output rows f[m] (tiles 0, 1). The same
 // products, in the same order per output, as mh_x3_kernel's one-tile m-major pass: the results are bit-identical.
-// the LDS base as an opaque value: the bias reads below are loop-invariant to the compiler, which otherwise keeps all
-// 50 bias tiles of the pass in registers across the step loop (200 VGPRs: the spills of the first multi-tile build)
-__device__ __forceinline__ const char* opaque(const char* p) {
-  asm volatile("" : "+s"(p));
-  return p;
-}
-__device__ __forceinline__ f32x4 bias4_at(const char* l, int off_bytes, int tile, int g) {
-  return *(const f32x4*)(l + off_bytes + (16 * tile + 4 * g) * 4);
-}
-
 template <int MT>
 __device__ __forceinline__ void sur_forward_mt(EngK& e, const float (&x)[MT][3], int g, int (&vmax)[MT],
                                                f32x4 (&f)[MT][2]) {
@@ -894,31 +883,22 @@ __device__ __forceinline__ void sur_forward_mt(EngK& e, const float (&x)[MT][3],
   }
   u32x4 Hh[MT], Hl[MT];
   sfor<MT>([&](auto m) { act_pair(P, 0, m, vmax, Hh[m], Hl[m]); });
-  {
-    const char* l = opaque(e.lds);
-    sfor<ST>([&](auto t) {
-      const f32x4 b = bias4_at(l, SB + W * 4, t, g);
-      sfor<MT>([&](auto m) { Q[m][t] = b; });
-    });
-  }
+  sfor<ST>([&](auto t) {
+    const f32x4 b = e.bias4(SB + W * 4, t);
+    sfor<MT>([&](auto m) { Q[m][t] = b; });
+  });
   hidden_k<MT>(e, P, Q, Hh, Hl, vmax);
   sfor<MT>([&](auto m) { act_pair(Q, 0, m, vmax, Hh[m], Hl[m]); });
-  {
-    const char* l = opaque(e.lds);
-    sfor<ST>([&](auto t) {
-      const f32x4 b = bias4_at(l, SB + 2 * W * 4, t, g);
-      sfor<MT>([&](auto m) { P[m][t] = b; });
-    });
-  }
+  sfor<ST>([&](auto t) {
+    const f32x4 b = e.bias4(SB + 2 * W * 4, t);
+    sfor<MT>([&](auto m) { P[m][t] = b; });
+  });
   hidden_k<MT>(e, Q, P, Hh, Hl, vmax);
   sfor<MT>([&](auto m) { act_pair(P, 0, m, vmax, Hh[m], Hl[m]); });
-  {
-    const char* l = opaque(e.lds);
-    sfor<2>([&](auto t) {
-      const f32x4 b = bias4_at(l, SB + 3 * W * 4, t, g);
-      sfor<MT>([&](auto m) { f[m][t] = b; });
-    });
-  }
+  sfor<2>([&](auto t) {
+    const f32x4 b = e.bias4(SB + 3 * W * 4, t);
+    sfor<MT>([&](auto m) { f[m][t] = b; });
+  });
   chunk_k<MT, true, 0, 2>(e, P, f, Hh, Hl, vmax);
 }
 
