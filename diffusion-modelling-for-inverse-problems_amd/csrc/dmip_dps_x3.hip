@@ -66,35 +66,38 @@ struct Eng {
   int na = NPF, nb = NS, nstream = NSTREAM;
 
   // the next refill: its source chunk and ring slot (the stream position advances); its PPW pieces per wave go out at
-  // once (ring_issue) or beside the consuming chunk's MFMAs (Spread, split_product_h)
-  const char* dma_src;
+  // once (ring_issue) or beside the consuming chunk's MFMAs (Spread, split_product_h). The pieces are buffer LDS-DMA
+  // (dmip_x3k.h's form): the image's buffer resource, the chunk's byte offset as the scalar offset, the wave's and
+  // lane's part as the per-lane offset -- no per-piece 64-bit address arithmetic (a VALU and two SALU a piece with
+  // global_load_lds)
+  __amdgpu_buffer_rsrc_t rp, rs, dma_rsrc;
+  unsigned voff;  // w PPW KiB + 16 lane
+  int dma_soff;
   char* dma_dst;
+  __device__ __forceinline__ void init_dma() {
+    rp = __builtin_amdgcn_make_buffer_rsrc((void*)pimg, 0, kDpsX3PriorChunks * CHUNK, 0x00020000);
+    rs = __builtin_amdgcn_make_buffer_rsrc((void*)simg, 0, kDpsX3SurChunks * CHUNK, 0x00020000);
+    voff = (unsigned)(w * PPW * 1024 + lane * 16);
+  }
   __device__ __forceinline__ void ring_target() {
     const int c = __builtin_amdgcn_readfirstlane(c_issue);
     const int a = __builtin_amdgcn_readfirstlane(na), b = __builtin_amdgcn_readfirstlane(nb);
-    const char* src = c < a ? pimg + (size_t)c * CHUNK
-                            : (c < a + b ? simg + (size_t)(c - a) * CHUNK : pimg + (size_t)(c - b) * CHUNK);
-    const uint64_t addr = (uint64_t)src;
-    const char* base = (const char*)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(addr >> 32)) << 32) |
-                                     (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)addr));
-    asm volatile("" : "+s"(base));  // keep the per-chunk address out of the loop-invariant hoist
-    dma_src = base;
+    const bool prior = c < a || c >= a + b;
+    dma_rsrc = prior ? rp : rs;
+    dma_soff = __builtin_amdgcn_readfirstlane((c < a ? c : (c < a + b ? c - a : c - b)) * CHUNK);
     dma_dst = lds + RING + __builtin_amdgcn_readfirstlane(s_issue) * CHUNK;
     c_issue = c_issue + 1 == nstream ? 0 : c_issue + 1;
     s_issue = s_issue + 1 == R ? 0 : s_issue + 1;
   }
   template <int Q>
   __device__ __forceinline__ void ring_piece() const {
-    const int piece = w * PPW + Q;
-    glds16(dma_src + piece * 1024, dma_dst + piece * 1024, lane);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(dma_rsrc, (lds_void*)(dma_dst + (w * PPW + Q) * 1024), 16, voff,
+                                             dma_soff + Q * 1024, 0, 0);
   }
   __device__ __forceinline__ void ring_issue() {
     ring_target();
-#pragma unroll
-    for (int q = 0; q < PPW; ++q) {
-      const int piece = w * PPW + q;
-      glds16(dma_src + piece * 1024, dma_dst + piece * 1024, lane);
-    }
+    ring_piece<0>(), ring_piece<1>(), ring_piece<2>(), ring_piece<3>();
+    ring_piece<4>(), ring_piece<5>(), ring_piece<6>(), ring_piece<7>();
   }
   // the hook of x3::split_product_h: piece Q of the pending refill beside k-step unit (Q NU) / PPW (round 5: a burst
   // of PPW LDS-DMA instructions at the chunk start held the wave's issue ~100-185 cycles a piece)
@@ -440,6 +443,7 @@ __global__ void __launch_bounds__(NW * 64, 1) dps_x3_kernel(DpsX3Params p) {
   const long long c_local = (long long)blockIdx.x * (NW * 16) + w * 16 + j;
   const bool valid = c_local < p.n_chains;
   Eng e{lds, p.pimg, p.simg, 0, 0, 0, w, lane, g};
+  e.init_dma();
   {
     // resident parts: the two layer-1 images (lanes 0-31 of each tile), the biases, y
     const uint4* s1 = (const uint4*)p.pl1;
@@ -705,6 +709,8 @@ struct EngK {
   int c_issue, s_issue, s_read;
   int w, lane, g;
   static constexpr int NSTR = 2 * NCH + 1;  // 16 k-major hidden chunks + the output chunk per step
+  // (global_load_lds here, not Eng's buffer form: with it the three-tile variant spills 184 B instead of 20 and runs
+  // 5 % slower, profiles/r5_dma_buffer/)
   const char* dma_src;
   char* dma_dst;
   int dma_a, dma_b;  // piece Q's source: dma_src + (Q / 4) dma_a + ((Q / 2) % 2) dma_b + (Q % 2) KiB
@@ -912,6 +918,7 @@ __global__ void __launch_bounds__(NW * 64, 1) mh_x3_kernel(MhX3Params p) {
   const bool valid = c_local < p.n_chains;
   const long long cc = valid ? c_local : 0;
   Eng e{lds, p.simg, p.simg, 0, 0, 0, w, lane, g};
+  e.init_dma();
   e.na = kDpsX3SurFwdChunks, e.nb = 0, e.nstream = kDpsX3SurFwdChunks;
   {
     const uint4* s2 = (const uint4*)p.sl1;
