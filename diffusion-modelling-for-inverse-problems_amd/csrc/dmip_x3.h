@@ -248,36 +248,41 @@ struct XEngine {
     nl = n_hidden;
     ncn = NL1C + (nl - 1) * NCH + 1;
     c_issue = s_issue = s_read = 0;
+    voff = (unsigned)(w * PPW * 1024 + lane * 16);
   }
 
   // the refill of the next chunk to issue: its source and ring slot (then the stream position advances); its PPW
   // pieces per wave go out at once (ring_issue) or spread beside the consuming chunk's MFMAs (SpreadPieces)
-  const char* dma_src;
+  // (buffer LDS-DMA, as dmip_x3k.h's: the network image's buffer resource, the chunk's byte offset as the scalar
+  // offset, the wave's and lane's part as the per-lane offset -- no per-piece 64-bit address arithmetic)
+  __amdgpu_buffer_rsrc_t dma_rsrc;
+  unsigned voff;  // w PPW KiB + 16 lane
+  int dma_soff;
   char* dma_dst;
   __device__ __forceinline__ void ring_target() {
     const int c = __builtin_amdgcn_readfirstlane(c_issue);
     const int n = __builtin_amdgcn_readfirstlane(ncn);
-    const uint64_t addr = (uint64_t)((c < n ? img[0] : img[1]) + (size_t)(c < n ? c : c - n) * CHUNK);
-    const char* base = (const char*)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(addr >> 32)) << 32) |
-                                     (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)addr));
-    asm volatile("" : "+s"(base));  // keep the per-chunk address out of the loop-invariant hoist
-    dma_src = base;
+    dma_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(c < n ? img[0] : img[1]), 0, n * CHUNK, 0x00020000);
+    dma_soff = __builtin_amdgcn_readfirstlane((c < n ? c : c - n) * CHUNK);
     dma_dst = lds + RING_OFF + __builtin_amdgcn_readfirstlane(s_issue) * CHUNK;
     c_issue = c_issue + 1 == NNET * ncn ? 0 : c_issue + 1;
     s_issue = s_issue + 1 == R ? 0 : s_issue + 1;
   }
   template <int Q>
   __device__ __forceinline__ void ring_piece() const {
-    const int piece = w * PPW + Q;
-    glds16(dma_src + piece * 1024, dma_dst + piece * 1024, lane);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(dma_rsrc, (lds_void*)(dma_dst + (w * PPW + Q) * 1024), 16, voff,
+                                             dma_soff + Q * 1024, 0, 0);
+  }
+  template <int Q = 0>
+  __device__ __forceinline__ void ring_pieces() const {
+    if constexpr (Q < PPW) {
+      ring_piece<Q>();
+      ring_pieces<Q + 1>();
+    }
   }
   __device__ __forceinline__ void ring_issue() {
     ring_target();
-#pragma unroll
-    for (int q = 0; q < PPW; ++q) {
-      const int piece = w * PPW + q;
-      glds16(dma_src + piece * 1024, dma_dst + piece * 1024, lane);
-    }
+    ring_pieces();
   }
   // the hook of split_product_h: piece Q of the pending refill beside k-step U = (Q NU) / PPW of the chunk
   struct SpreadPieces {
