@@ -62,14 +62,14 @@ def test_bf16_samplers_have_no_scratch(isa):
 # round 3); the cap keeps that from growing unnoticed.
 # The paired-tile kernels (x3p, 185 VGPRs + 256 AGPRs) have none. One-tile x3: none, except CDiffE (3, 23) at width
 # 512, whose layer 1 streams through the ring (L1R, one wave per SIMD at ~512 registers): round 4 spilled ~17 dwords
-# of segment state, reloaded a handful of times per step; since round 5 (the chain index recomputed from the
-# wave-uniform job and the lane id after the step loop) 3 dwords of schedule setup, stored and loaded only in the
-# segment setup -- none in the step loop.
+# of segment state, reloaded a handful of times per step; round 5 cut that to 3 dwords of schedule setup (the chain
+# index recomputed from the wave-uniform job and the lane id after the step loop), and the buffer LDS-DMA refills
+# (no per-piece 64-bit addresses) to none.
 # The fp32x3 DPS and MH kernels: none since the running range max is pinned (round 5; it had kept every tracked value
 # alive, 176 B in DPS); the three-tile MH kernel (launched when its workgroup rounds are full) spills 20 B.
 _SCRATCH_CAP = {"x3_sampler_kernel": 0, "x3k_sampler_kernel": 128, "loss_grad_kernel": 0, "x3p_sampler_kernel": 0,
                 "dps_x3_kernel": 0, "mh_x3_kernel": 0, "mh_x3_mt_kernel": 0}
-_SCRATCH_CAP_KERNEL = {"x3_sampler_kernelILi2ELi512ELi3ELi23E": 12, "mh_x3_mt_kernelILi3E": 24}
+_SCRATCH_CAP_KERNEL = {"mh_x3_mt_kernelILi3E": 24}
 
 
 @pytest.mark.parametrize("family", list(_SCRATCH_CAP))
