@@ -26,7 +26,8 @@ Prints ONE JSON line on rank 0 (driver contract) with
   * `dist`: the world size torch.distributed reports after init and every rank's device (PCI bus id).
 Other workloads (not the headline): --workload cdiffe-pc (BASELINE config 3: CDiffE + 1 Langevin
 corrector step, --chains-total 1000000 sharded over the ranks: strong scaling) and --workload dps
-(config 4: DPS with surrogate guidance, exact f32, --chains-total 262144).
+(config 4: DPS with surrogate guidance, --chains-total 262144; fp32x3 by default, --precision fp32 for the
+exact-f32 kernel).
 """
 import argparse
 import datetime
@@ -350,20 +351,31 @@ def timed(wl, steps, dist, world, dev, seed0=0, **over):
     """barrier + sync, K steps (HIP events around each sampling call on its stream), sync + barrier;
     (elapsed max over ranks, mean launch ms, last output)."""
     import torch
-    stream = torch.cuda.current_stream(dev)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    gpu = dev.type == "cuda"  # the CPU launcher test (--stub) times the stand-in with the host clock
+    sync = torch.cuda.synchronize if gpu else (lambda: None)
+    if gpu:
+        stream = torch.cuda.current_stream(dev)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    else:
+        ev = [[0.0, 0.0] for _ in range(steps)]
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     x = None
     for i in range(steps):
-        ev[i][0].record(stream)
+        if gpu:
+            ev[i][0].record(stream)
+        else:
+            ev[i][0] = time.perf_counter()
         x = wl.sample_local(seed0 + i, **over)
-        ev[i][1].record(stream)
+        if gpu:
+            ev[i][1].record(stream)
+        else:
+            ev[i][1] = time.perf_counter()
         if world > 1:
             x = wl.par.gather_shards(x, wl.n_total, dev)
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -371,7 +383,7 @@ def timed(wl, steps, dist, world, dev, seed0=0, **over):
         t = torch.tensor([elapsed], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    launch_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    launch_ms = float(np.mean([a.elapsed_time(b) if gpu else (b - a) * 1e3 for a, b in ev]))
     return elapsed, launch_ms, x
 
 
@@ -553,24 +565,35 @@ def main_worker(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.stub:
-        return stub_worker(args, rank, world)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        world = init_dist("nccl", dev, args.dist_timeout)
-    devices = rank_devices(dist, world, dev)
+    if args.stub:  # CPU / gloo launcher test: the real line with a chain-keyed stand-in for the sampler
+        dev = torch.device("cpu")
+        if world > 1:
+            world = init_dist("gloo", None, args.dist_timeout)
+        devices = rank_devices(dist, world, None)
+        if rank == args.stub_fail_rank:
+            sys.stderr.write(f"stub rank {rank}: failing on purpose\n")
+            return 1
+    else:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+        if world > 1:
+            world = init_dist("nccl", dev, args.dist_timeout)
+        devices = rank_devices(dist, world, dev)
     pkg = importlib.import_module(PKG)
     lib = importlib.import_module(PKG + "._lib")
     metrics = importlib.import_module(PKG + ".metrics")
     wl = Workload(args, pkg, dev, rank, world)
+    if args.stub:
+        wl.sample_local = stub_sampler(wl)
     S = args.num_steps
 
     for i in range(args.warmup):
         wl.step(1000 + i)
-    torch.cuda.synchronize()
+    if not args.stub:
+        torch.cuda.synchronize()
     elapsed, launch_ms, x_last = timed(wl, args.steps, dist, world, dev)
-    lib.device_status(dev)  # no asynchronous kernel failure in the timed region
+    if not args.stub:
+        lib.device_status(dev)  # no asynchronous kernel failure in the timed region
 
     ms_per_step = elapsed / args.steps * 1e3
     value = wl.n_total * args.steps / elapsed
@@ -607,6 +630,15 @@ def main_worker(args):
         "dist": {"world_size_observed": world, "backend": "nccl (RCCL)" if world > 1 else None,
                  "devices": devices},
     }
+    if args.stub:
+        line["stub"] = stub_check(wl, x_last)
+        if world > 1:
+            dist.barrier()
+        if rank == 0:
+            print(json.dumps(line), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return 0 if line["stub"]["gather_ok"] else 1
     rep = None
     if args.workload == "cde" and rank == 0:
         rep = parity_vs_reference(metrics, x_last.reshape(-1, XDIM).cpu().numpy(), S, wl.weights)
@@ -628,33 +660,28 @@ def main_worker(args):
     return 0
 
 
-def stub_worker(args, rank, world):
-    """CPU / gloo stand-in for the sampler (launcher test only): every rank contributes its chain
-    range [lo, hi) as x[c] = (c, c, c); rank 0 checks the gathered tensor and prints the line.
-    --stub-fail-rank R: rank R exits 1 after init while the others block in the gather (fail-fast test)."""
+def stub_sampler(wl):
+    """The launcher test's stand-in for the fused sampler (--stub, CPU): x[c] = (c, seed mod 997, lo) for the rank's
+    global chains c in [lo, hi) -- a pure function of (seed, global chain index), the property the HIP kernels keep
+    (chain-keyed RNG), plus the producing rank's range start, so the gathered union shows who produced what."""
     import torch
-    import torch.distributed as dist
-    par = importlib.import_module(PKG + ".parallel")
-    if world > 1:
-        world = init_dist("gloo", None, args.dist_timeout)
-    devices = rank_devices(dist, world, None)
-    if rank == args.stub_fail_rank:
-        sys.stderr.write(f"stub rank {rank}: failing on purpose\n")
-        return 1
-    n_total = args.chains_total if args.chains_total > 0 else args.chains * world
-    lo, hi = par.shard_range(n_total, rank, world)
-    local = torch.arange(lo, hi, dtype=torch.float32)[None, :, None].expand(1, hi - lo, XDIM).contiguous()
-    x = par.gather_shards(local, n_total, torch.device("cpu")) if world > 1 else local
-    ok = bool(torch.equal(x[0, :, 0], torch.arange(n_total, dtype=torch.float32)))
-    if world > 1:
-        dist.barrier()
-    if rank == 0:
-        print(json.dumps({"metric": "stub", "n_gpus": world, "chains_total": n_total,
-                          "gathered_shape": list(x.shape), "gather_ok": ok,
-                          "dist": {"world_size_observed": world, "devices": devices}}), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
-    return 0 if ok else 1
+
+    def sample_local(seed, **over):
+        c = torch.arange(wl.lo, wl.hi, dtype=torch.float32)
+        return torch.stack([c, c * 0 + float(seed % 997), c * 0 + float(wl.lo)], dim=1)[None].contiguous()
+    return sample_local
+
+
+def stub_check(wl, x):
+    """Every chain exactly once, in global order, each from the rank whose shard_range holds it."""
+    import torch
+    n = wl.n_total
+    lo_of = torch.tensor([float(wl.par.shard_range(n, r, wl.world)[0]) for r in range(wl.world)
+                          for _ in range(*wl.par.shard_range(n, r, wl.world))])
+    ok = (tuple(x.shape) == (1, n, XDIM) and torch.equal(x[0, :, 0], torch.arange(n, dtype=torch.float32))
+          and torch.equal(x[0, :, 2], lo_of) and bool((x[0, :, 1] == x[0, 0, 1]).all()))
+    return {"gathered_shape": list(x.shape), "gather_ok": bool(ok), "chains_total": n,
+            "rank0_chains": wl.n_local}
 
 
 def main():

@@ -7,7 +7,7 @@ namespace dmip {
 
 #ifdef DMIP_DIAG
 // Diagnostic library only (make diag; never the product build): DMIP_X3_DIAG=d (1..7) runs the timing ablation
-// DIAG = d of the width-256, xdim-3 CDE kernel (dmip_x3.h XEngine); see profiles/README.md.
+// DIAG = d of the width-256 / width-512, xdim-3 CDE kernels (dmip_x3.h XEngine); see profiles/README.md.
 static int x3_diag() {
   const char* e = getenv("DMIP_X3_DIAG");
   return e ? atoi(e) : 0;
@@ -17,10 +17,12 @@ static int x3_diag() {
 hipError_t launch_x3_sampler_cde(const X3SamplerParams& p, int width, int xdim, int n_y, hipStream_t st, bool* ok) {
   *ok = true;
 #ifdef DMIP_DIAG
-  if (width == 256 && xdim == 3 && !p.noise) {
+  if ((width == 256 || width == 512) && xdim == 3 && !p.noise) {
     switch (x3_diag()) {
-#define DG(d) \
-  case d: return launch_x3_sampler_t<SAMPLER_CDE, 256, 3, 0, false, d>(p, n_y, st);
+#define DG(d)                                                                                   \
+  case d:                                                                                       \
+    return width == 256 ? launch_x3_sampler_t<SAMPLER_CDE, 256, 3, 0, false, d>(p, n_y, st)    \
+                        : launch_x3_sampler_t<SAMPLER_CDE, 512, 3, 0, false, d>(p, n_y, st);
       DG(1) DG(2) DG(3) DG(4) DG(6) DG(7)
 #undef DG
       default: break;

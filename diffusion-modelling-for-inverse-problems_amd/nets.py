@@ -12,7 +12,8 @@ arithmetic, e.g. for the evaluate drivers' score MSE), or with 16-bit operands (
 fp16 hidden and output layers; `"bf16"` is its deprecated name); the weights
 are packed once per parameter snapshot. Autograd (the training losses) uses the eager module chain.
 The activation is the reference's constructor argument: nn.Tanh runs on every engine, nn.SiLU on the exact-f32
-forward and CDE sampler (`dmip_act`); any other activation has no HIP kernel and the HIP paths refuse it.
+forward and CDE sampler (`dmip_act`); any other activation has no HIP kernel: its forward is the module chain (as the
+reference's, on the device), and the fused samplers refuse it.
 """
 import collections
 
@@ -107,7 +108,7 @@ class MLP(_TanhChainMLP):
     """Score network a(x, y, t) on cat[x, y, t] (nets.py:17-35)."""
 
     def forward(self, x, y, t):
-        if x.is_cuda and not self._wants_autograd(x, y, t):
+        if x.is_cuda and self.dmip_act is not None and not self._wants_autograd(x, y, t):
             return self._hip_forward(x, y, t, x.shape[1])
         inp = torch.cat([x, y, t.view(len(x), 1)], dim=1)
         assert inp.ndim == 2, 'Input Tensor is expected to be 2D with shape (batch_size, ydim+ydim+embeddim)'
@@ -119,7 +120,7 @@ class MLP2(_TanhChainMLP):
     input_layout = _lib.DMIP_INPUT_X_T
 
     def forward(self, x, t):
-        if x.is_cuda and not self._wants_autograd(x, t):
+        if x.is_cuda and self.dmip_act is not None and not self._wants_autograd(x, t):
             return self._hip_forward(x, None, t, x.shape[1])
         inp = torch.cat([x, t.view(len(x), 1)], dim=1)
         assert inp.ndim == 2, 'Input Tensor is expected to be 2D with shape (batch_size, ydim+ydim+embeddim)'

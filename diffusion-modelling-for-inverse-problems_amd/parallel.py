@@ -74,52 +74,75 @@ def _sample_local(model, y, n, num_steps, mean, std, seed, lo, kw):
     return sample_checked(model, y, n, num_steps, mean, std, seed=seed, chain_offset=lo, agree=any_rank, **kw)
 
 
-def any_rank(flag):
-    """True on every rank when `flag` is true on any rank (one all_reduce MAX of a scalar; no-op at world size 1)."""
+# per-rank outcome of a guarded launch; any_rank's MAX over ranks picks the worst
+OK, RANGE, FAILED = 0, 1, 2
+
+
+def any_rank(state):
+    """The maximum of `state` (a bool or one of OK / RANGE / FAILED) over all ranks: one all_reduce MAX of a scalar,
+    no-op at world size 1. As a flag: true on every rank when true on any rank."""
     _, ws = world()
     if ws == 1:
-        return bool(flag)
+        return int(state)
     dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
-    buf = torch.tensor([1 if flag else 0], dtype=torch.int32, device=dev)
+    buf = torch.tensor([int(state)], dtype=torch.int32, device=dev)
     dist.all_reduce(buf, op=dist.ReduceOp.MAX)
-    return bool(buf.item())
+    return int(buf.item())
+
+
+def guarded(dev, launch, fallback=None, agree=None):
+    """launch() with the device status word cleared before it and read after it, so an asynchronous failure of THIS
+    launch surfaces here (a split-fp16 engine's fp16-range report, a hand-over timeout) and a stale report of an
+    earlier launch is not taken for it. Each rank's outcome is OK, RANGE (the split's range refusal or report) or
+    FAILED (any other error); `agree` (any_rank) makes it the maximum over all ranks, so the ranks leave together and
+    none is left blocked in a collective another rank never reaches. RANGE with a `fallback` returns
+    fallback() (the exact-f32 engine) on every rank; RANGE without one, or FAILED on any rank, raises on every rank."""
+    import warnings
+    from . import _lib
+    err, state, res = None, OK, None
+    try:
+        _lib.clear_range_status(dev)
+        res = launch()
+        _lib.device_status(dev)
+    except Exception as e:  # noqa: BLE001 -- every error takes part in the agreement, then is re-raised
+        err, state = e, (RANGE if _lib.is_range_error(e) else FAILED)
+    outcome = agree(state) if agree is not None else state
+    if outcome == OK:
+        return res
+    if outcome == RANGE and fallback is not None:
+        warnings.warn(f"{err or 'fp16 range (another rank)'}; sampled with the exact-f32 engine instead", RuntimeWarning)
+        return fallback()
+    if err is not None:
+        raise err
+    raise RuntimeError("dmip: another rank's launch failed (" + ("fp16 range" if outcome == RANGE else "error") +
+                       "); this rank's shard is discarded")
 
 
 def sample_checked(model, y, n, num_steps, mean, std, seed=None, chain_offset=0, agree=None, **kw):
-    """model.sample_device(...) with the default precision's fp16-range guard.
+    """model.sample_device(...) under `guarded`: the device status word is read after EVERY launch, whichever engine
+    the request resolved to (a "fp16" request runs the split-fp16 fp32x3 engine for shapes without a 16-bit kernel,
+    and DPS has no 16-bit engine at all).
 
-    At the default precision (fp32x3: the reference's fp32 arithmetic from fp16 hi/lo splits) a network or a
-    trajectory outside the split's fp16 range -- a scaled weight, or a returned chain's layer-1 input, beyond
-    65504 -- is refused (at launch) or reported (device status word) by the library; the call is then sampled
-    again with the exact-f32 engine, so the default path never returns the split's inf/NaN where the reference's
-    fp32 stays finite. The status word is cleared before the launch (a stale range report of an earlier launch
-    is not this call's) and read after it. `agree(flag) -> bool` makes the decision collective: under
-    sample_sharded every rank resamples if any rank's shard left the range, so the gathered union is always one
-    engine's chains (bit-identical to the 1-GPU run). An explicit `precision` keeps the error."""
-    import warnings
-    from . import _lib
-    default = kw.get("precision") is None and getattr(model, "precision", None) == "fp32x3"
-    if not default:
-        return model.sample_device(y, n, num_steps, mean, std, seed=seed, chain_offset=chain_offset, **kw)
+    Without an explicit `precision` (the model's default: fp32x3, the reference's fp32 arithmetic from fp16 hi/lo
+    splits, or fp16) a network or a trajectory outside the split's fp16 range -- a scaled weight, or a chain's
+    layer-1 input, beyond 65504 -- is refused (at launch) or reported (device status word) by the library; the call
+    is then sampled again with the exact-f32 engine, so the default path never returns the split's inf/NaN where
+    the reference's fp32 stays finite. `agree(state)` makes the decision collective: under sample_sharded every rank
+    resamples if any rank's shard left the range, so the gathered union is always one engine's chains (bit-identical
+    to the 1-GPU run), and every rank raises if any rank failed otherwise. An explicit `precision` keeps the error."""
+    from .estimators import canonical_precision
+    explicit = kw.get("precision") is not None
+    prec = canonical_precision(kw.get("precision") or getattr(model, "precision", "fp32x3"))
     if seed is None:  # one seed for both attempts: the fallback resamples the same chains
         from .estimators import _draw_seed
         seed = _draw_seed()
     dev = model._exec_device(y)
-    _lib.clear_range_status(dev)
-    err = None
-    try:
-        x = model.sample_device(y, n, num_steps, mean, std, seed=seed, chain_offset=chain_offset, **kw)
-        _lib.device_status(x.device)
-    except (ValueError, RuntimeError) as e:
-        if not _lib.is_range_error(e):
-            raise
-        err = e
-    out_of_range = agree(err is not None) if agree is not None else err is not None
-    if not out_of_range:
-        return x
-    warnings.warn(f"{err or 'fp16 range (another rank)'}; sampled with the exact-f32 engine instead", RuntimeWarning)
-    return model.sample_device(y, n, num_steps, mean, std, seed=seed, chain_offset=chain_offset,
-                               **dict(kw, precision="fp32"))
+
+    def call(**over):
+        return model.sample_device(y, n, num_steps, mean, std, seed=seed, chain_offset=chain_offset, **dict(kw, **over))
+
+    fallback = None if explicit or prec == "fp32" else (lambda: call(precision="fp32"))
+    return guarded(dev, call, fallback, agree)
 
 
 def chains_sharded(n, run, seed, device):

@@ -208,7 +208,8 @@ def mh_sample(forward_model, params, ys, n_chains, num_steps, noise_std, seed=No
     noise (S, n_y, n_chains, 3) / unif (S, n_y, n_chains) replay captured draws (exact f32 only).
     precision "fp32": the exact-f32 kernel; "fp32x3": the surrogate's products as three-term fp16 splits (same
     RNG stream and acceptance test per chain) -- a weight, proposal or activation beyond fp16's range resamples
-    every chain with "fp32" (RuntimeWarning); `agree(flag) -> bool` makes that decision collective (parallel)."""
+    every chain with "fp32" (RuntimeWarning); `agree` (parallel.any_rank) makes that decision, and any other failure,
+    collective (parallel.guarded)."""
     from . import _lib
     ys = torch.as_tensor(ys)
     if not torch.cuda.is_available():
@@ -229,24 +230,22 @@ def mh_sample(forward_model, params, ys, n_chains, num_steps, noise_std, seed=No
         raise ValueError("mh_sample: injected draws replay the exact-f32 kernel (precision=\"fp32\")")
     nz = _lib.scat_noise(params['a'], params['b'], params['lambd_bd'])
     x0 = prep(x_init)
-    if precision == "fp32x3":
-        err = None
-        try:
-            _lib.clear_range_status(dev)
-            _lib.mh_sample(h, nz, ys, n_chains, chain_offset, num_steps, noise_std, seed, out, x0, None, None, ed,
-                           precision="fp32x3")
-            _lib.device_status(dev)
-        except (ValueError, RuntimeError) as e:
-            if not _lib.is_range_error(e):
-                raise
-            err = e
-        if not (agree(err is not None) if agree is not None else err is not None):
+    from . import parallel
+
+    def run(prec):
+        def launch():
+            if prec == "fp32x3":
+                _lib.mh_sample(h, nz, ys, n_chains, chain_offset, num_steps, noise_std, seed, out, x0, None, None, ed,
+                               precision="fp32x3")
+            else:
+                _lib.mh_sample(h, nz, ys, n_chains, chain_offset, num_steps, noise_std, seed, out, x0, prep(noise),
+                               prep(unif), ed)
             return (out, ed) if return_ediff else out
-        warnings.warn(f"{err or 'fp16 range (another rank)'}; sampled with the exact-f32 engine instead",
-                      RuntimeWarning)
-    _lib.mh_sample(h, nz, ys, n_chains, chain_offset, num_steps, noise_std, seed, out, x0, prep(noise), prep(unif),
-                   ed)
-    return (out, ed) if return_ediff else out
+        return launch
+
+    # the status word is read after the launch either way; a fp32x3 range report resamples every chain in exact f32,
+    # decided by all ranks together under `agree` (parallel.guarded)
+    return parallel.guarded(dev, run(precision), run("fp32") if precision == "fp32x3" else None, agree)
 
 
 def anneal_to_energy(x_curr, energy, metr_steps_per_block, noise_std=0.1, langevin_prop=False, lang_steps=None,
@@ -294,7 +293,8 @@ def generate_gt_samples(forward_model, params, ys, out_dir=None, n_samples_x=300
                                              chain_offset=off, precision=precision, agree=agree)
     x = parallel.chains_sharded(n_samples_x, run, seed, dev)  # one process: a single launch of all chains
     x = x.reshape(ys.shape[0], n_repeats, n_samples_x, 3)
-    if out_dir and parallel.world()[0] == 0:
+    rank, ws = parallel.world()
+    if out_dir and rank == 0:
         xh = x.cpu().numpy()
         for i in range(ys.shape[0]):
             d = os.path.join(out_dir, str(i))
@@ -302,6 +302,9 @@ def generate_gt_samples(forward_model, params, ys, out_dir=None, n_samples_x=300
             for j in range(n_repeats):
                 with open(os.path.join(d, '%d.npy' % j), 'wb') as fh:
                     np.save(fh, xh[i, j])
+    if out_dir and ws > 1:
+        import torch.distributed as dist
+        dist.barrier()  # no rank returns (and reads gt_dir) before rank 0's files are complete
     return x
 
 

@@ -415,7 +415,9 @@ int dmip_rng_normals(uint64_t seed, int64_t chain_offset, uint64_t stream_id, in
  * (models/diffusion.py:34, sdes.py:21-35). */
 int dmip_schedule(int num_steps, const dmip_vpsde* sde, float* out_dev, void* stream);
 
-/* Diagnostic build of the sampler (same math, internal RNG, chain_offset 0) that also writes per-wave
+/* ---- DIAGNOSTIC entry point: not part of the drop-in boundary (no reference interface; the package only declares
+ * its ctypes signature; scripts/stamps.py calls it). Exported by libdmip.so so the phase stamps need no second library.
+ * Diagnostic build of the sampler (same math, internal RNG, chain_offset 0) that also writes per-wave
  * cycle sums of the three step phases [layer 1, hidden layers, output layer + EM update], then the
  * s_memtime and s_memrealtime (100 MHz) spans of the whole step loop, to
  * stamps_dev[(workgroup * waves_per_workgroup + wave) * 5 + k]. Never used on the product path; its

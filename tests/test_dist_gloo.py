@@ -19,7 +19,7 @@ class _KeyedModel:
     def _exec_device(self, y):
         return torch.device("cpu")
 
-    def sample_device(self, y, n, num_steps, mean, std, seed=None, chain_offset=0):
+    def sample_device(self, y, n, num_steps, mean, std, seed=None, chain_offset=0, precision=None):
         c = torch.arange(chain_offset, chain_offset + n, dtype=torch.float32)
         x = torch.stack([c, c * 0 + float(seed % 1000), c * 0 + num_steps], dim=1)
         return x[None]
@@ -39,6 +39,7 @@ def _worker(rank, world, port, n, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import importlib
     par = importlib.import_module("diffusion-modelling-for-inverse-problems_amd.parallel")
+    _no_status(par)
     torch.manual_seed(100 + rank)  # different local seeds: common_seed must unify them
     out = par.sample_sharded(_KeyedModel(), torch.zeros(2), n, 17, 0.0, 1.0)
     q.put((rank, out.numpy()))
@@ -252,3 +253,61 @@ def test_ground_truth_chains_sharded(world, n, bad):
     assert (ref[:, :, 3] == (1.0 if bad < n else 0.0)).all()          # one engine for all chains
     for r in range(1, world):
         assert (res[r] == ref).all()
+
+
+class _FailModel(_RangeModel):
+    """Rank `fail_rank`'s launch fails: with a non-range error ("args"), or with a range error under an explicit
+    precision ("range-explicit", which keeps the error)."""
+
+    def __init__(self, fail_rank, kind):
+        super().__init__(10 ** 9)
+        self.fail_rank, self.kind = fail_rank, kind
+
+    def sample_device(self, y, n, num_steps, mean, std, seed=None, chain_offset=0, precision=None):
+        if dist.get_rank() == self.fail_rank:
+            if self.kind == "args":
+                raise ValueError("dmip: bad argument (test)")
+            raise RuntimeError("dmip: fp32x3 sampler: a chain's layer-1 input left the fp16 range (test)")
+        return super().sample_device(y, n, num_steps, mean, std, seed, chain_offset, precision)
+
+
+def _fail_worker(rank, world, port, kind, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import importlib
+    par = importlib.import_module("diffusion-modelling-for-inverse-problems_amd.parallel")
+    _no_status(par)
+    prec = "fp32x3" if kind == "range-explicit" else None
+    try:
+        par.sample_sharded(_FailModel(world - 1, kind), torch.zeros(2), 100, 17, 0.0, 1.0, precision=prec)
+        q.put((rank, None))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, f"{type(e).__name__}: {e}"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind", ["args", "range-explicit"])
+def test_one_rank_failure_raises_on_every_rank(kind):
+    """a rank whose launch fails with anything but a fallback-able range report must not leave the other
+    ranks blocked in the agreement collective: the outcome (OK / RANGE / FAILED) is all-reduced, and every rank
+    raises -- the failing rank its own error, the others "another rank's launch failed"."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if root not in sys.path:
+        sys.path.insert(0, root)
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fail_worker, args=(r, world, port, kind, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[world - 1] is not None and ("bad argument" in res[world - 1] if kind == "args"
+                                           else "fp16 range" in res[world - 1])
+    for r in range(world - 1):
+        assert res[r] is not None and "another rank's launch failed" in res[r], res[r]

@@ -151,3 +151,19 @@ def test_silu_cde_trains_through_autograd(dmip):
     assert dmip._lib.calls.get("loss_grad", 0) == calls.get("loss_grad", 0)
     assert dmip._lib.calls.get("loss_grad_f32", 0) == calls.get("loss_grad_f32", 0)
     assert np.isfinite(l1) and l1 < l0
+
+
+def test_activation_without_kernel_forward_is_the_module_chain(dmip):
+    """an MLP / MLP2 with an activation that has no HIP kernel (ReLU) evaluates as the reference does --
+    the module chain, on the device -- instead of raising; only the fused samplers refuse it (test above)."""
+    torch.manual_seed(3)
+    for cls, args in ((dmip.MLP, (27, 3)), (dmip.MLP2, (4, 3))):
+        net = cls(*args, [64] * 3, torch.nn.ReLU()).to(DEV)
+        x = torch.randn(128, 3, device=DEV)
+        y = torch.randn(128, 23, device=DEV)
+        t = torch.rand(128, 1, device=DEV)
+        inp = torch.cat([x, y, t], 1) if cls is dmip.MLP else torch.cat([x, t], 1)
+        with torch.no_grad():
+            out = net(x, y, t) if cls is dmip.MLP else net(x, t)
+            ref = torch.nn.Sequential.forward(net, inp)
+        assert torch.equal(out, ref)

@@ -350,6 +350,29 @@ def test_dps_trained_prior_vs_oracle(dmip, golden, fm, guidance, zeta, precision
     assert err < 1e-4 * max(1.0, np.abs(ref).max()), err
 
 
+@pytest.mark.parametrize("precision", ["fp32x3", "fp32"])
+def test_dps_guided_worst_chain_vs_f64_oracle_50_steps(dmip, golden, fm, precision):
+    """A worst-chain bound for guided DPS over a long horizon: 'norm' guidance, zeta = 0.005, the
+    fixture-trained prior, y_test[0], 200 chains x 50 steps, both engines against the f64 oracle (oracle.dps_sample,
+    same chain-keyed RNG): EVERY chain within 1e-3 max(1, |ref|). Measured before this test existed
+    (profiles/r5_dps_engine_drift.jsonl, same chains): fp32x3 2.4e-5, exact f32 1.4e-4 -- the split engine is the
+    closer of the two to the f64 map. The 200-step statistical gate (next test) stays as a second check."""
+    _, _, sur = fm
+    m = _trained_dps(dmip, golden, fm, 0.005, "norm")
+    prior = [(l.weight.detach().cpu().numpy(), l.bias.detach().cpu().numpy())
+             for l in m.prior_net if isinstance(l, torch.nn.Linear)]
+    y = golden("data_scat.npz")["y_test"][0]
+    n, S = 200, 50
+    x = m.sample_device(torch.from_numpy(y).to(DEV), n, S, seed=11, precision=precision)[0].cpu().numpy()
+    dmip._lib.device_status(torch.device(DEV))
+    ref = O.dps_sample(prior, sur, y, n, S, 11, zeta=0.005, mode="norm")
+    assert np.all(np.isfinite(x))
+    e = np.abs(x.astype(np.float64) - ref).max(1) / max(1.0, np.abs(ref).max())
+    print(f"\n[dps] {precision} vs f64 oracle, guided 'norm' zeta=0.005, {S} steps, {n} chains: "
+          f"worst chain {e.max():.2e}, median {np.median(e):.2e}")
+    assert e.max() < 1e-3, e.max()
+
+
 def test_dps_fp32x3_vs_exact_f32_many_steps(dmip, golden, fm):
     """The two DPS engines chain by chain (same RNG), 2000 chains, fixture-trained prior:
     * unguided (zeta = 0), the full 1000 steps: every chain within 1e-5 (measured 6.3e-7) -- the split-fp16

@@ -241,3 +241,53 @@ def test_bench_parity_fields(golden):
     assert not bench.ks_field(shifted)["pass"] and not shifted["pass"]
     assert bench.parity_vs_reference(metrics, ref, 200, w) is None
     assert bench.parity_vs_reference(metrics, ref, 1000, "random-init") is None
+
+
+class _StatusModel:
+    """A sampler stand-in whose launch 'reports' an fp16-range status for split-engine precisions (None = the model's
+    default, "fp32x3", "fp16") and succeeds in exact f32; records the precision of every launch."""
+    xdim = 1
+
+    def __init__(self, precision):
+        self.precision = precision
+        self.launches = []
+        self.pending = None
+
+    def _exec_device(self, y):
+        return torch.device("cpu")
+
+    def sample_device(self, y, n, num_steps, mean, std, seed=None, chain_offset=0, precision=None):
+        self.launches.append(precision)
+        if (precision or self.precision) != "fp32":
+            self.pending = "dmip: fp32x3 sampler: a chain's layer-1 input left the fp16 range (status 3)"
+        return torch.full((1, n, 1), 0.0 if (precision or self.precision) == "fp32" else float("nan"))
+
+
+@pytest.mark.parametrize("model_prec,explicit", [("fp32x3", None), ("fp16", None), ("fp32x3", "fp16"),
+                                                 ("fp32x3", "fp32x3"), ("fp32", None)])
+def test_sample_checked_reads_status_for_every_engine(dmip, monkeypatch, model_prec, explicit):
+    """the status word is read after EVERY launch, not only at the fp32x3 default. A "fp16"
+    request can run the split engine (shapes without a 16-bit kernel, and DPS), so its range report must not be
+    dropped: the model default (fp32x3 or fp16) resamples in exact f32; an explicit precision raises."""
+    import importlib
+    par = importlib.import_module("diffusion-modelling-for-inverse-problems_amd.parallel")
+    m = _StatusModel(model_prec)
+
+    def status(dev):
+        msg, m.pending = m.pending, None
+        if msg:
+            raise RuntimeError(msg)
+    monkeypatch.setattr(dmip._lib, "device_status", status)
+    monkeypatch.setattr(dmip._lib, "clear_range_status", lambda dev: setattr(m, "pending", None))
+    kw = {} if explicit is None else {"precision": explicit}
+    if explicit is not None:
+        with pytest.raises(RuntimeError, match="fp16 range"):
+            par.sample_checked(m, torch.zeros(1), 8, 3, 0.0, 1.0, seed=1, **kw)
+        assert m.launches == [explicit]
+    elif model_prec == "fp32":
+        x = par.sample_checked(m, torch.zeros(1), 8, 3, 0.0, 1.0, seed=1)
+        assert m.launches == [None] and torch.isfinite(x).all()
+    else:
+        with pytest.warns(RuntimeWarning, match="exact-f32"):
+            x = par.sample_checked(m, torch.zeros(1), 8, 3, 0.0, 1.0, seed=1)
+        assert m.launches == [None, "fp32"] and torch.isfinite(x).all()
