@@ -123,8 +123,14 @@ struct TrainParams {
   float* partials;            // [n_waves][partial stride]
   char* packed;               // the shared LDS image of the weight fragments (written by the pack kernel)
   float* adj;                 // split build: [n][kTrainAdj] per-sample loss adjoints + loss terms (forward -> reverse)
+  // split build, record reverse (train_rec()): per tile and hidden layer li, the forward's activations of the P, V, C
+  // streams (bf16) and the reverse's activation-derivative coefficients (dmip_train.hip, "records"); null: the
+  // reverse half recomputes the forward instead
+  uint32_t* rec;
 };
 constexpr int kTrainAdj = 12;  // abP[2] abV[2] abC[2] dsm ic pde, padded to 48 bytes
+constexpr int kTrainRecQ = 6;  // record quantities per unit: h_P, h_V, h_C (bf16), d1 (fp16), d2 z_V (bf16), d1_C (fp16)
+constexpr int kTrainRecTileBytes = kTrainRecQ * 64 * 16 * 2;  // one (tile, layer): 16 units x 16 samples per lane group
 
 bool train_split();
 int train_nparam(int n_hidden);
@@ -132,7 +138,8 @@ int train_partial_stride(int n_hidden);
 int train_waves_per_wg();
 int train_partials_per_wg();
 int train_packed_bytes(int n_hidden);
-size_t train_adj_bytes(long long batch);  // 0 unless the forward / reverse split kernels run
+size_t train_adj_bytes(long long batch);  // 0 unless the forward / reverse split kernels run (incl. the records)
+bool train_rec();  // the record reverse half (DMIP_TRAIN_REC, default on) instead of the recomputing one
 hipError_t launch_loss_grad(const TrainParams& p, int n_hidden, float* grads, float* loss_out, float* partials,
                             int n_wg, hipStream_t st);
 

@@ -82,10 +82,10 @@ static_assert(3 * IN + 2 <= 32, "layer-1 split operand fits one k-step");
 template <int NL, int PH = 0>
 struct TL {
   static constexpr int NW = PH == 0 ? NWV : 4;               // waves per workgroup
-  static constexpr bool OWN = PH == 2;                       // each wave owns fixed gradient blocks in registers
+  static constexpr bool OWN = PH >= 2;                       // each wave owns fixed gradient blocks in registers
   static constexpr int NBUF = OWN ? 2 : 1;                   // transposed scratch sets per wave (layer-parity buffered)
   static constexpr bool GG = PH == 0 ? GACC_GLOBAL : false;  // gradient partial rows in global memory
-  static constexpr int RSV = PH == 2 ? 16 : RS;              // scratch row stride (reverse half: unpadded, to fit)
+  static constexpr int RSV = PH >= 2 ? 16 : RS;              // scratch row stride (reverse half: unpadded, to fit)
   static constexpr int p_w(int l) { return l == 0 ? 0 : W * IN + W + (l - 1) * (W * W + W); }
   static constexpr int p_b(int l) { return l == NL ? p_w(NL) + OUT * W : p_w(l) + (l == 0 ? W * IN : W * W); }
   static constexpr int NPARAM = p_w(NL) + OUT * W + OUT;
@@ -101,7 +101,7 @@ struct TL {
   static constexpr int AOL = AO + 2048;                  // its lo residuals (forward)
   static constexpr int COL = AOL + 2048;                 // fp32 [D][64]: layer-1 weight columns of x (forward)
   static constexpr int WAVE = COL + D * W * 4;
-  static constexpr int IMG = PH == 2 ? AO : WAVE;        // image bytes this kernel copies (reverse: no forward-only parts)
+  static constexpr int IMG = PH >= 2 ? AO : WAVE;        // image bytes this kernel copies (reverse: no forward-only parts)
   static constexpr int GACC = 0;                         // per wave: fp32 gradient partial (param order, LDS mode)
   static constexpr int SCR = (GG || OWN) ? 0 : ((PART * 4 + 15) / 16) * 16;  // per wave: 6 transposed [64][16] bf16
   static constexpr int SET = 6 * W * RSV * 2;            // one transposed scratch set (bytes)
@@ -218,6 +218,59 @@ __device__ __forceinline__ bf16x8 tread(const __bf16* scr, int row, bool ok, int
   const u32x4 v = *(const u32x4*)(scr + sidx<RSV>(row, 8 * hh));
   const u32x4 z = {0u, 0u, 0u, 0u};
   return __builtin_bit_cast(bf16x8, ok ? v : z);
+}
+
+// Records (the record reverse half, PH = 3; p.rec): the forward half keeps, per tile and hidden layer li (z_li = the
+// layer's pre-activation: layer 1 at li = 0), what the reverse pass needs of that layer instead of recomputing the
+// forward: the activations of the P, V and C streams (h_P, h_V = d1 z_V, h_C: the operands of the next layer's weight-
+// gradient contraction, which rounds them to bf16 anyway, so bf16 records are bit-identical to recomputed ones) and the
+// three coefficients of the activation's reverse, zbar_P = d1 hbar_P + (d2 z_V) hbar_V, zbar_V = d1 hbar_V,
+// zbar_C = d1_C hbar_C (d1, d1_C in (0, 1]: fp16; d2 z_V: bf16). Layout: for each (tile, li, row tile R, quantity q)
+// lane l's 4 values r -- unit 16 R + 4 (l >> 4) + r of sample l & 15 -- as one 8-byte piece, piece (R, q) being
+// 64 lanes x 8 B contiguous (one coalesced 512-byte access per wave instruction; the forward half writes each R as soon
+// as its values exist, holding nothing across R); value r is half r & 1 of dword r >> 1. 12 KiB per (tile, layer):
+// 36 KiB per 16-sample tile at NL = 3, 151 MB at batch 65,536.
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
+  return (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)a) | ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)b) << 16);
+}
+__device__ __forceinline__ uint32_t pk_f16(float a, float b) {
+  return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)a) | ((uint32_t)__builtin_bit_cast(uint16_t, (_Float16)b) << 16);
+}
+constexpr bool rec_f16(int q) { return q == 3 || q == 5; }
+
+template <int NL>
+__device__ __forceinline__ u32x2* rec_at(uint32_t* rec, long long tile, int li, int q, int R, int lane) {
+  return (u32x2*)rec + ((((size_t)tile * NL + li) * 4 + R) * kTrainRecQ + q) * 64 + lane;
+}
+
+// value (R, r) of a quantity's four pieces
+template <bool F16>
+__device__ __forceinline__ float rec_val(const u32x2 (&d)[4], int R, int r) {
+  const uint32_t wd = d[R][r >> 1];
+  const uint16_t h = (r & 1) ? (uint16_t)(wd >> 16) : (uint16_t)(wd & 0xffffu);
+  if constexpr (F16) return (float)__builtin_bit_cast(_Float16, h);
+  return __builtin_bit_cast(float, (uint32_t)h << 16);
+}
+
+// the forward half's record writes: row tile R's coefficients (q 3..5) as soon as they exist, and the activations
+// (q 0..2) straight from the packed bf16 B operand of the next layer once its R pair is complete -- the bf16 hi part,
+// the same RNE rounding -- so the writes hold no extra registers across R
+template <int NL>
+__device__ __forceinline__ void rec_put_coef(uint32_t* rec, long long tile, int li, int R, int lane, const float (&d1)[4],
+                                             const float (&b)[4], const float (&d1c)[4]) {
+  *rec_at<NL>(rec, tile, li, 3, R, lane) = u32x2{pk_f16(d1[0], d1[1]), pk_f16(d1[2], d1[3])};
+  *rec_at<NL>(rec, tile, li, 4, R, lane) = u32x2{pk_bf16(b[0], b[1]), pk_bf16(b[2], b[3])};
+  *rec_at<NL>(rec, tile, li, 5, R, lane) = u32x2{pk_f16(d1c[0], d1c[1]), pk_f16(d1c[2], d1c[3])};
+}
+template <int NL>
+__device__ __forceinline__ void rec_put_h(uint32_t* rec, long long tile, int li, int Rp, int lane, const bf16x8 (&h)[3][2]) {
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const u32x4 v = __builtin_bit_cast(u32x4, h[q][Rp]);
+    *rec_at<NL>(rec, tile, li, q, 2 * Rp, lane) = u32x2{v[0], v[1]};
+    *rec_at<NL>(rec, tile, li, q, 2 * Rp + 1, lane) = u32x2{v[2], v[3]};
+  }
 }
 
 // The shared part of the LDS image (weight fragments, biases, layer-1 columns), packed ONCE per
@@ -372,6 +425,24 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
   const long long n_tiles = (p.n + NS - 1) / NS;
   // OWN: every wave of the workgroup runs the same rounds (a wave past the end runs an all-invalid tile),
   // so the layer barriers match
+  // REC: the records of the wave's tile, all hidden layers. They are loaded one tile ahead: layer li's registers are
+  // refilled with the NEXT tile's layer li as soon as this tile's pass B has used them (its coefficients, at step li),
+  // so a tile's records are in flight during the previous tile's later layers. The first tile's are loaded here. A
+  // wave past the end reads the last tile's (finite) records: its adjoints are zero, so they add nothing.
+  constexpr bool REC = PH == 3;
+  u32x2 rc[REC ? NL : 1][kTrainRecQ][4];
+  const long long tile_step = (long long)gridDim.x * NWV;
+  auto rec_load = [&](long long tl, int li) {
+    const long long tt = tl < n_tiles ? tl : n_tiles - 1;
+#pragma unroll
+    for (int q = 0; q < kTrainRecQ; ++q)
+#pragma unroll
+      for (int R = 0; R < 4; ++R) rc[li][q][R] = *rec_at<NL>(p.rec, tt, li, q, R, lane);
+  };
+  if constexpr (REC) {
+#pragma unroll
+    for (int li = NL - 1; li >= 0; --li) rec_load((long long)blockIdx.x * NWV + w, li);
+  }
   for (long long tile0 = (long long)blockIdx.x * NWV + (L::OWN ? 0 : w); tile0 < n_tiles;
        tile0 += (long long)gridDim.x * NWV) {
     const long long tile = tile0 + (L::OWN ? w : 0);
@@ -416,7 +487,7 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
     const bf16x8 BP = b1_operand(uP, 1.0f, g), BV = b1_operand(uV, 0.0f, g), BC = b1_operand(uC, 1.0f, g);
 
     float abP[OUT], abV[OUT], abC[OUT];
-    if constexpr (PH == 2) {  // the forward half's adjoints and loss terms of this sample
+    if constexpr (PH >= 2) {  // the forward half's adjoints and loss terms of this sample
       const float4* rec = (const float4*)(p.adj + (valid ? si : 0) * kTrainAdj);
       const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2];
       const bool ok = valid;
@@ -431,11 +502,14 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
     // ======================================================== pass F: forward with jets
     float aS[NSTREAM][OUT];
     {
+      // the record reverse half's input (PH 1 with p.rec; a uniform branch per layer)
+      const bool recw = PH == 1 && p.rec != nullptr;
       bf16x8 H[NSTREAM][2], HL[3][2];  // HL: lo residuals of the split streams P, V, C
 #pragma unroll
       for (int R = 0; R < 4; ++R) {
         const bf16x8 a = frag(a1r, R, lane);
         const f32x4 zP = mfma16(a, BP, f32x4{}), zV = mfma16(a, BV, f32x4{}), zC = mfma16(a, BC, f32x4{});
+        float cd1[4], cb[4], cd1c[4];  // records: the reverse's coefficients
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int u = 16 * R + 4 * g + r;
@@ -443,12 +517,19 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
           const float q = 1.0f - pz * pz, k1 = 1.0f - h * h;
           const float d1 = k1 * q, d2 = -2.0f * q * (h * d1 + pz * k1);
           const float w0 = col[u], w1 = col[W + u];
-          const float v[NSTREAM] = {h, d1 * zV[r], tanh_f(tanh_f(zC[r])), d1 * w0, d1 * w1,
+          const float pc = tanh_f(zC[r]), hc = tanh_f(pc);
+          const float v[NSTREAM] = {h, d1 * zV[r], hc, d1 * w0, d1 * w1,
                                     d2 * w0 * w0, d2 * w0 * w1, d2 * w1 * w1};
 #pragma unroll
           for (int S = 0; S < NSTREAM; ++S) H[S][R >> 1][4 * (R & 1) + r] = bf_hi(v[S]);
 #pragma unroll
           for (int S = 0; S < 3; ++S) HL[S][R >> 1][4 * (R & 1) + r] = bf_lo(v[S]);
+          // the reverse's layer-1 coefficients (pass B, li == 0): d1, d2 z_V, d1_C of the double tanh
+          cd1[r] = d1, cb[r] = d2 * zV[r], cd1c[r] = (1.0f - hc * hc) * (1.0f - pc * pc);
+        }
+        if (recw) {
+          rec_put_coef<NL>(p.rec, tile, 0, R, lane, cd1, cb, cd1c);
+          if (R & 1) rec_put_h<NL>(p.rec, tile, 0, R >> 1, lane, *(const bf16x8(*)[3][2])H);
         }
       }
 #pragma unroll
@@ -470,13 +551,15 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
             if (S < 3) Z[S] = mm3(a0, a1, l0, l1, H[S], HL[S], Z[S]);
             else Z[S] = mm(a0, a1, H[S], Z[S]);
           }
+          float cd1[4], cb[4], cd1c[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const float h = tanh_f(Z[0][r]);
             const float d1 = 1.0f - h * h, d2 = -2.0f * h * d1;
+            const float hc = tanh_f(Z[2][r]);
             const float v[NSTREAM] = {h,
                                       d1 * Z[1][r],
-                                      tanh_f(Z[2][r]),
+                                      hc,
                                       d1 * Z[3][r],
                                       d1 * Z[4][r],
                                       d1 * Z[5][r] + d2 * Z[3][r] * Z[3][r],
@@ -486,6 +569,11 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
             for (int S = 0; S < NSTREAM; ++S) Hn[S][R >> 1][4 * (R & 1) + r] = bf_hi(v[S]);
 #pragma unroll
             for (int S = 0; S < 3; ++S) HLn[S][R >> 1][4 * (R & 1) + r] = bf_lo(v[S]);
+            cd1[r] = d1, cb[r] = d2 * Z[1][r], cd1c[r] = 1.0f - hc * hc;
+          }
+          if (recw) {
+            rec_put_coef<NL>(p.rec, tile, l, R, lane, cd1, cb, cd1c);
+            if (R & 1) rec_put_h<NL>(p.rec, tile, l, R >> 1, lane, *(const bf16x8(*)[3][2])Hn);
           }
         }
 #pragma unroll
@@ -612,14 +700,28 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
     f32x4 hbar[3][4];  // adjoint of the current layer's output, streams P, V, C (acc form)
     // the reverse half is specialised per layer (every branch on li and the bias-partial index constant);
     // the fused kernel keeps the loop (its code size)
-    constexpr int kLiUnroll = PH == 2 ? NL + 1 : 1;
+    constexpr int kLiUnroll = PH >= 2 ? NL + 1 : 1;
 #pragma unroll kLiUnroll
     for (int li = NL; li >= 0; --li) {
       if constexpr (L::OWN) sbuf ^= 1;
       // ---- recompute P, V, C forward: h_{li-1} (B form + transposed into scratch 3..5) and z_li
       bf16x8 H[3][2], HL[3][2];
       f32x4 Z[3][4];
-      {
+      if constexpr (REC) {  // h_{li-1} from the records instead: the recompute's put_t, bit for bit, 16-bit stores
+        if (li >= 1) {
+#pragma unroll
+          for (int S = 0; S < 3; ++S) {
+            __bf16* sc = S_(3 + S);
+#pragma unroll
+            for (int R = 0; R < 4; ++R)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const uint32_t wd = rc[li >= 1 ? li - 1 : 0][S][R][r >> 1];
+                sc[sidx<RS>(16 * R + 4 * g + r, c16)] = __builtin_bit_cast(__bf16, (uint16_t)((r & 1) ? wd >> 16 : wd));
+              }
+          }
+        }
+      } else {
 #pragma unroll
         for (int R = 0; R < 4; ++R) {
           const bf16x8 a = frag(a1r, R, lane);
@@ -729,6 +831,20 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
 
       // ---- tanh layer li (li == 0: the double tanh of layer 1): zbar from hbar
       f32x4 zb[3][4];
+      if constexpr (REC) {  // the coefficients from the records
+        const int lr = li < NL ? li : 0;
+#pragma unroll
+        for (int R = 0; R < 4; ++R)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float d1 = rec_val<true>(rc[lr][3], R, r), b = rec_val<false>(rc[lr][4], R, r);
+            const float d1c = rec_val<true>(rc[lr][5], R, r);
+            zb[0][R][r] = d1 * hbar[0][R][r] + b * hbar[1][R][r];
+            zb[1][R][r] = d1 * hbar[1][R][r];
+            zb[2][R][r] = d1c * hbar[2][R][r];
+          }
+        rec_load(tile + tile_step, lr);  // this tile is done with layer lr's records: the next tile's
+      } else {
 #pragma unroll
       for (int R = 0; R < 4; ++R)
 #pragma unroll
@@ -752,6 +868,7 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
           zb[1][R][r] = d1 * hbar[1][R][r];
           zb[2][R][r] = d1c * hbar[2][R][r];
         }
+      }
 #pragma unroll
       for (int S = 0; S < 3; ++S) put_t<RS>(S_(S), zb[S], g, c16);
       if (li == 0) {
@@ -1046,6 +1163,32 @@ bool train_split() {
   return v;
 }
 
+// the record reverse half (loss_grad_kernel<NL, 3>) or the recomputing one (<NL, 2>); DMIP_TRAIN_REC=0 selects the
+// latter (A/B knob, read once per process)
+bool train_rec() {
+  static const bool v = [] {
+    const char* e = getenv("DMIP_TRAIN_REC");
+    return e ? atoi(e) != 0 : true;
+  }();
+  return v;
+}
+
+// the records follow the adjoint rows in the adj allocation (train_adj_bytes)
+static size_t rec_offset(long long batch) { return ((size_t)batch * kTrainAdj * sizeof(float) + 255) / 256 * 256; }
+static uint32_t* rec_ptr(float* adj, long long batch) {
+  return adj && train_rec() ? (uint32_t*)((char*)adj + rec_offset(batch)) : nullptr;
+}
+
+// the reverse half's kernel
+template <int NL>
+static void launch_reverse(const TrainParams& q, int n_wg, hipStream_t st) {
+  using namespace train;
+  if (q.rec)
+    hipLaunchKernelGGL((loss_grad_kernel<NL, 3>), dim3(n_wg), dim3(TL<NL, 3>::NW * 64), 0, st, q);
+  else
+    hipLaunchKernelGGL((loss_grad_kernel<NL, 2>), dim3(n_wg), dim3(TL<NL, 2>::NW * 64), 0, st, q);
+}
+
 int train_nparam(int n_hidden) {
   return n_hidden == 3 ? train::TL<3>::NPARAM : (n_hidden == 2 ? train::TL<2>::NPARAM : -1);
 }
@@ -1057,6 +1200,7 @@ hipError_t launch_loss_grad(const TrainParams& p, int n_hidden, float* grads, fl
   const int nparam = train_nparam(n_hidden);
   TrainParams q = p;
   q.partials = partials;
+  q.rec = rec_ptr(p.adj, p.n);
   if (n_hidden == 3)
     hipLaunchKernelGGL(train_pack_kernel<3>, dim3(kPackBlocks), dim3(256), 0, st, q);
   else
@@ -1070,10 +1214,10 @@ hipError_t launch_loss_grad(const TrainParams& p, int n_hidden, float* grads, fl
     const long long g1 = std::min<long long>(2LL * n_wg, (tiles + 3) / 4);
     if (n_hidden == 3) {
       hipLaunchKernelGGL((loss_grad_kernel<3, 1>), dim3((unsigned)g1), dim3(TL<3, 1>::NW * 64), 0, st, q);
-      hipLaunchKernelGGL((loss_grad_kernel<3, 2>), dim3(n_wg), dim3(TL<3, 2>::NW * 64), 0, st, q);
+      launch_reverse<3>(q, n_wg, st);
     } else {
       hipLaunchKernelGGL((loss_grad_kernel<2, 1>), dim3((unsigned)g1), dim3(TL<2, 1>::NW * 64), 0, st, q);
-      hipLaunchKernelGGL((loss_grad_kernel<2, 2>), dim3(n_wg), dim3(TL<2, 2>::NW * 64), 0, st, q);
+      launch_reverse<2>(q, n_wg, st);
     }
   } else if (n_hidden == 3) {
     hipLaunchKernelGGL(loss_grad_kernel<3>, dim3(n_wg), dim3(NWV * 64), 0, st, q);
@@ -1107,6 +1251,7 @@ hipError_t launch_loss_grad_fused(const TrainParams& p, int n_hidden, float* gra
   if (f.adam.off[f.adam.n] != nparam) return hipErrorInvalidValue;  // Adam's flat order is the gradient's
   TrainParams q = p;
   q.partials = partials;
+  q.rec = rec_ptr(p.adj, p.n);
   const unsigned draw_blocks = (unsigned)((f.draws.batch + 255) / 256);
   const dim3 pg(kPackBlocks + draw_blocks), pb(256);
   if (n_hidden == 3)
@@ -1119,10 +1264,10 @@ hipError_t launch_loss_grad_fused(const TrainParams& p, int n_hidden, float* gra
   const long long g1 = std::min<long long>(2LL * n_wg, (tiles + 3) / 4);
   if (n_hidden == 3) {
     hipLaunchKernelGGL((loss_grad_kernel<3, 1>), dim3((unsigned)g1), dim3(TL<3, 1>::NW * 64), 0, st, q);
-    hipLaunchKernelGGL((loss_grad_kernel<3, 2>), dim3(n_wg), dim3(TL<3, 2>::NW * 64), 0, st, q);
+    launch_reverse<3>(q, n_wg, st);
   } else {
     hipLaunchKernelGGL((loss_grad_kernel<2, 1>), dim3((unsigned)g1), dim3(TL<2, 1>::NW * 64), 0, st, q);
-    hipLaunchKernelGGL((loss_grad_kernel<2, 2>), dim3(n_wg), dim3(TL<2, 2>::NW * 64), 0, st, q);
+    launch_reverse<2>(q, n_wg, st);
   }
   if ((e = hipGetLastError()) != hipSuccess) return e;
   const bool fused_total = nparam / 64 == (nparam + 2) / 64;
@@ -1139,6 +1284,11 @@ int train_partial_stride(int n_hidden) { return n_hidden == 3 ? train::TL<3>::PA
 int train_packed_bytes(int n_hidden) { return n_hidden == 3 ? train::TL<3>::WAVE : train::TL<2>::WAVE; }
 int train_partials_per_wg() { return train_split() ? 1 : (train::GACC_GLOBAL ? train::NWV : 1); }
 int train_waves_per_wg() { return train_split() ? train::TL<3, 2>::NW : train::NWV; }
-size_t train_adj_bytes(long long batch) { return train_split() ? (size_t)batch * kTrainAdj * sizeof(float) : 0; }
+size_t train_adj_bytes(long long batch) {
+  if (!train_split()) return 0;
+  if (!train_rec()) return (size_t)batch * kTrainAdj * sizeof(float);
+  // the adjoint rows, then the records: 16-sample tiles x at most 3 hidden layers
+  return rec_offset(batch) + (size_t)((batch + 15) / 16) * 3 * kTrainRecTileBytes;
+}
 
 }  // namespace dmip
