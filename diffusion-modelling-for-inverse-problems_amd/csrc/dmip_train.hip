@@ -225,11 +225,12 @@ __device__ __forceinline__ bf16x8 tread(const __bf16* scr, int row, bool ok, int
 // forward: the activations of the P, V and C streams (h_P, h_V = d1 z_V, h_C: the operands of the next layer's weight-
 // gradient contraction, which rounds them to bf16 anyway, so bf16 records are bit-identical to recomputed ones) and the
 // three coefficients of the activation's reverse, zbar_P = d1 hbar_P + (d2 z_V) hbar_V, zbar_V = d1 hbar_V,
-// zbar_C = d1_C hbar_C (d1, d1_C in (0, 1]: fp16; d2 z_V: bf16). Layout: for each (tile, li, row tile R, quantity q)
-// lane l's 4 values r -- unit 16 R + 4 (l >> 4) + r of sample l & 15 -- as one 8-byte piece, piece (R, q) being
-// 64 lanes x 8 B contiguous (one coalesced 512-byte access per wave instruction; the forward half writes each R as soon
-// as its values exist, holding nothing across R); value r is half r & 1 of dword r >> 1. 12 KiB per (tile, layer):
-// 36 KiB per 16-sample tile at NL = 3, 151 MB at batch 65,536.
+// zbar_C = d1_C hbar_C (d1, d1_C in (0, 1]: fp16; d2 z_V: bf16). Layout: for each (tile, li, row-tile pair Rp,
+// quantity q) lane l's 8 values (R = 2 Rp + (0, 1), r) -- unit 16 R + 4 (l >> 4) + r of sample l & 15 -- as one
+// 16-byte piece, piece (Rp, q) being 64 lanes x 16 B contiguous: the reverse half reads it with one coalesced dwordx4
+// per lane (36 loads per tile, so a tile's loads fit the 6-bit vmcnt counter beside the inputs'); the forward half
+// writes each R's 8-byte half as soon as its values exist, holding nothing across R. Value (R, r) is half r & 1 of
+// dword 2 (R & 1) + (r >> 1). 12 KiB per (tile, layer): 36 KiB per 16-sample tile at NL = 3, 151 MB at batch 65,536.
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
   return (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)a) | ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)b) << 16);
@@ -237,17 +238,21 @@ __device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
 __device__ __forceinline__ uint32_t pk_f16(float a, float b) {
   return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)a) | ((uint32_t)__builtin_bit_cast(uint16_t, (_Float16)b) << 16);
 }
-constexpr bool rec_f16(int q) { return q == 3 || q == 5; }
 
 template <int NL>
-__device__ __forceinline__ u32x2* rec_at(uint32_t* rec, long long tile, int li, int q, int R, int lane) {
-  return (u32x2*)rec + ((((size_t)tile * NL + li) * 4 + R) * kTrainRecQ + q) * 64 + lane;
+__device__ __forceinline__ u32x4* rec_at(uint32_t* rec, long long tile, int li, int Rp, int q, int lane) {
+  return (u32x4*)rec + ((((size_t)tile * NL + li) * 2 + Rp) * kTrainRecQ + q) * 64 + lane;
+}
+// row tile R's 8-byte half of its piece
+template <int NL>
+__device__ __forceinline__ u32x2* rec_half(uint32_t* rec, long long tile, int li, int R, int q, int lane) {
+  return (u32x2*)rec_at<NL>(rec, tile, li, R >> 1, q, lane) + (R & 1);
 }
 
-// value (R, r) of a quantity's four pieces
+// value (R, r) of a quantity's two pieces
 template <bool F16>
-__device__ __forceinline__ float rec_val(const u32x2 (&d)[4], int R, int r) {
-  const uint32_t wd = d[R][r >> 1];
+__device__ __forceinline__ float rec_val(const u32x4 (&d)[2], int R, int r) {
+  const uint32_t wd = d[R >> 1][2 * (R & 1) + (r >> 1)];
   const uint16_t h = (r & 1) ? (uint16_t)(wd >> 16) : (uint16_t)(wd & 0xffffu);
   if constexpr (F16) return (float)__builtin_bit_cast(_Float16, h);
   return __builtin_bit_cast(float, (uint32_t)h << 16);
@@ -259,18 +264,14 @@ __device__ __forceinline__ float rec_val(const u32x2 (&d)[4], int R, int r) {
 template <int NL>
 __device__ __forceinline__ void rec_put_coef(uint32_t* rec, long long tile, int li, int R, int lane, const float (&d1)[4],
                                              const float (&b)[4], const float (&d1c)[4]) {
-  *rec_at<NL>(rec, tile, li, 3, R, lane) = u32x2{pk_f16(d1[0], d1[1]), pk_f16(d1[2], d1[3])};
-  *rec_at<NL>(rec, tile, li, 4, R, lane) = u32x2{pk_bf16(b[0], b[1]), pk_bf16(b[2], b[3])};
-  *rec_at<NL>(rec, tile, li, 5, R, lane) = u32x2{pk_f16(d1c[0], d1c[1]), pk_f16(d1c[2], d1c[3])};
+  *rec_half<NL>(rec, tile, li, R, 3, lane) = u32x2{pk_f16(d1[0], d1[1]), pk_f16(d1[2], d1[3])};
+  *rec_half<NL>(rec, tile, li, R, 4, lane) = u32x2{pk_bf16(b[0], b[1]), pk_bf16(b[2], b[3])};
+  *rec_half<NL>(rec, tile, li, R, 5, lane) = u32x2{pk_f16(d1c[0], d1c[1]), pk_f16(d1c[2], d1c[3])};
 }
 template <int NL>
 __device__ __forceinline__ void rec_put_h(uint32_t* rec, long long tile, int li, int Rp, int lane, const bf16x8 (&h)[3][2]) {
 #pragma unroll
-  for (int q = 0; q < 3; ++q) {
-    const u32x4 v = __builtin_bit_cast(u32x4, h[q][Rp]);
-    *rec_at<NL>(rec, tile, li, q, 2 * Rp, lane) = u32x2{v[0], v[1]};
-    *rec_at<NL>(rec, tile, li, q, 2 * Rp + 1, lane) = u32x2{v[2], v[3]};
-  }
+  for (int q = 0; q < 3; ++q) *rec_at<NL>(rec, tile, li, Rp, q, lane) = __builtin_bit_cast(u32x4, h[q][Rp]);
 }
 
 // The shared part of the LDS image (weight fragments, biases, layer-1 columns), packed ONCE per
@@ -351,6 +352,19 @@ __device__ __forceinline__ void turn_barrier() {
 #endif
 }
 
+// inclusive scan over each 16-lane row by DPP row shifts: lane 15 of a row holds the sum of the row's 16 lanes, always
+// summed in the same order (deterministic)
+__device__ __forceinline__ float row_sum16(float v) {
+#define DMIP_ROW_SHR(n) \
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x110 + (n), 0xf, 0xf, true))
+  DMIP_ROW_SHR(1);
+  DMIP_ROW_SHR(2);
+  DMIP_ROW_SHR(4);
+  DMIP_ROW_SHR(8);
+#undef DMIP_ROW_SHR
+  return v;
+}
+
 template <bool GG>
 __device__ __forceinline__ void gadd(float* a, float v) {
   if constexpr (GG) (void)__hip_atomic_fetch_add(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -375,8 +389,15 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
     static_assert(L::IMG % 16 == 0, "LDS image is a whole number of 16-byte pieces");
     const uint4* src = (const uint4*)p.packed;
     uint4* dst = (uint4*)lds;
+    if constexpr (PH == 3) {  // the record reverse reads the transposed images only (W^T for hbar, the output's)
+      static_assert(L::A1 - L::WT == L::AOT - L::WT - 4096 && L::WT % 16 == 0 && L::AOT % 16 == 0, "image layout");
 #pragma unroll 4
-    for (int e = tid; e < L::IMG / 16; e += NWV * 64) dst[e] = src[e];
+      for (int e = tid; e < (L::A1 - L::WT) / 16; e += NWV * 64) dst[L::WT / 16 + e] = src[L::WT / 16 + e];
+      for (int e = tid; e < 4096 / 16; e += NWV * 64) dst[L::AOT / 16 + e] = src[L::AOT / 16 + e];
+    } else {
+#pragma unroll 4
+      for (int e = tid; e < L::IMG / 16; e += NWV * 64) dst[e] = src[e];
+    }
     if constexpr (PH == 1 || L::OWN) {
     } else if constexpr (!GACC_GLOBAL) {
       float* gacc = (float*)(lds + L::WAVE + w * L::WAVE_BYTES + L::GACC);
@@ -430,18 +451,44 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
   // so a tile's records are in flight during the previous tile's later layers. The first tile's are loaded here. A
   // wave past the end reads the last tile's (finite) records: its adjoints are zero, so they add nothing.
   constexpr bool REC = PH == 3;
-  u32x2 rc[REC ? NL : 1][kTrainRecQ][4];
+  u32x4 rc[REC ? NL : 1][kTrainRecQ][2];
   const long long tile_step = (long long)gridDim.x * NWV;
   auto rec_load = [&](long long tl, int li) {
     const long long tt = tl < n_tiles ? tl : n_tiles - 1;
 #pragma unroll
     for (int q = 0; q < kTrainRecQ; ++q)
 #pragma unroll
-      for (int R = 0; R < 4; ++R) rc[li][q][R] = *rec_at<NL>(p.rec, tt, li, q, R, lane);
+      for (int Rp = 0; Rp < 2; ++Rp) rc[li][q][Rp] = *rec_at<NL>(p.rec, tt, li, Rp, q, lane);
   };
+  // REC: the per-sample inputs and the forward half's adjoint record are loaded one tile ahead as well, and issued at
+  // the start of the previous tile, i.e. before that tile's record refills: waiting for them (vmcnt counts in issue
+  // order) then never waits for the younger record loads too
+  struct In {
+    float x[D], y[M], eps[D], t;
+    float4 a0, a1, a2;
+  };
+  auto in_load = [&](long long tl) {
+    In v;
+    const long long sj = tl * NS + c16;
+    const long long sc = sj < p.n ? sj : p.n - 1;  // a sample past the end loads sample n - 1 (masked by `valid`)
+    static_assert(D == 2 && M == 2, "the inputs load as float2");
+    const float2 xv = *(const float2*)(p.x + sc * D), ev = *(const float2*)(p.eps + sc * D);
+    const float2 yv = *(const float2*)(p.y + sc * M);
+    v.x[0] = xv.x, v.x[1] = xv.y, v.eps[0] = ev.x, v.eps[1] = ev.y, v.y[0] = yv.x, v.y[1] = yv.y;
+    v.t = p.t[sc];
+    const float4* ar = (const float4*)(p.adj + sc * kTrainAdj);
+    v.a0 = ar[0], v.a1 = ar[1], v.a2 = ar[2];
+    return v;
+  };
+  In in_next{};
   if constexpr (REC) {
+    in_next = in_load((long long)blockIdx.x * NWV + w);
 #pragma unroll
     for (int li = NL - 1; li >= 0; --li) rec_load((long long)blockIdx.x * NWV + w, li);
+    // the first tile's loads land before the loop: otherwise the compiler's wait counts at the loop head, merged
+    // over the prologue path (where it may have issued the records before the inputs) and the back edge, drain the
+    // previous tile's record refills in every iteration
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   }
   for (long long tile0 = (long long)blockIdx.x * NWV + (L::OWN ? 0 : w); tile0 < n_tiles;
        tile0 += (long long)gridDim.x * NWV) {
@@ -450,7 +497,16 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
     const bool valid = si < p.n;
     // ---------------------------------------------------------------- per-sample inputs
     float x[D], y[M], eps[D], t;
-    if (valid) {
+    In in_cur{};
+    if constexpr (REC) {
+      in_cur = in_next;
+      in_next = in_load(tile + tile_step);
+#pragma unroll
+      for (int k = 0; k < D; ++k) x[k] = valid ? in_cur.x[k] : 0.0f, eps[k] = valid ? in_cur.eps[k] : 0.0f;
+#pragma unroll
+      for (int k = 0; k < M; ++k) y[k] = valid ? in_cur.y[k] : 0.0f;
+      t = valid ? in_cur.t : 0.5f;
+    } else if (valid) {
 #pragma unroll
       for (int k = 0; k < D; ++k) x[k] = p.x[si * D + k], eps[k] = p.eps[si * D + k];
 #pragma unroll
@@ -489,7 +545,7 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
     float abP[OUT], abV[OUT], abC[OUT];
     if constexpr (PH >= 2) {  // the forward half's adjoints and loss terms of this sample
       const float4* rec = (const float4*)(p.adj + (valid ? si : 0) * kTrainAdj);
-      const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2];
+      const float4 r0 = REC ? in_cur.a0 : rec[0], r1 = REC ? in_cur.a1 : rec[1], r2 = REC ? in_cur.a2 : rec[2];
       const bool ok = valid;
       abP[0] = ok ? r0.x : 0.0f, abP[1] = ok ? r0.y : 0.0f, abV[0] = ok ? r0.z : 0.0f, abV[1] = ok ? r0.w : 0.0f;
       abC[0] = ok ? r1.x : 0.0f, abC[1] = ok ? r1.y : 0.0f;
@@ -716,7 +772,7 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
             for (int R = 0; R < 4; ++R)
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
-                const uint32_t wd = rc[li >= 1 ? li - 1 : 0][S][R][r >> 1];
+                const uint32_t wd = rc[li >= 1 ? li - 1 : 0][S][R >> 1][2 * (R & 1) + (r >> 1)];
                 sc[sidx<RS>(16 * R + 4 * g + r, c16)] = __builtin_bit_cast(__bf16, (uint16_t)((r & 1) ? wd >> 16 : wd));
               }
           }
@@ -972,8 +1028,10 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
 
   if constexpr (PH == 1) return;  // the forward half: its adjoints and loss terms are in p.adj
   // ---- flush: bias partials (reduce the 16 sample lanes of each lane group) and loss sums; OWN: the weight
-  // blocks straight from registers to the workgroup's row, the bias / loss partials one wave at a time (wave order)
-  // into an LDS partial in the (now free) scratch, then that partial to the row
+  // blocks straight from registers to the workgroup's row; each wave reduces its bias / loss partials over its 16
+  // sample lanes by DPP row shifts (no LDS, all waves at once), the four waves' results meet in LDS in wave order
+  // (one barrier; deterministic), then that partial goes to the row. (Round 5 reduced by lane shuffles, one wave at a
+  // time: ~128 dependent LDS permutes per wave, serialised over the four waves -- a fixed cost of every launch.)
   if constexpr (L::OWN) {
     float* row = p.partials + (size_t)blockIdx.x * L::PART;
     {
@@ -995,8 +1053,40 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
 #pragma unroll
       for (int o = 0; o < OUT; ++o) row[L::p_w(NL) + o * W + 32 * (w - 2) + i32] = gX[o];
     }
-    turn_barrier();  // the last tile's scratch reads are done: the bias / loss partial may take the scratch
-    for (int e = tid; e < L::PART; e += NWV * 64) gacc[e] = 0.0f;
+    constexpr int NB = (NL - 1) * W + OUT + 3;  // hidden biases, output bias, loss sums
+    float* bp = gacc;                            // [NWV][NB] in the (now free) scratch
+    turn_barrier();  // the last tile's scratch reads are done
+#pragma unroll
+    for (int l = 0; l < NL - 1; ++l)
+#pragma unroll
+      for (int R = 0; R < 4; ++R)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = row_sum16(bbar[l][R][r]);
+          if (c16 == 15) bp[w * NB + l * W + 16 * R + 4 * g + r] = v;
+        }
+    // the output bias and the loss sums live in lane group 0 only: row 0's sum is the wave's
+#pragma unroll
+    for (int o = 0; o < OUT; ++o) {
+      const float v = row_sum16(g == 0 ? bobar[o] : 0.0f);
+      if (lane == 15) bp[w * NB + (NL - 1) * W + o] = v;
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const float v = row_sum16(g == 0 ? lsum[k] : 0.0f);
+      if (lane == 15) bp[w * NB + (NL - 1) * W + OUT + k] = v;
+    }
+    turn_barrier();
+    for (int e = tid; e < NB; e += NWV * 64) {
+      float v = bp[e];
+#pragma unroll
+      for (int v_ = 1; v_ < NWV; ++v_) v += bp[v_ * NB + e];
+      const int idx = e < (NL - 1) * W ? L::p_b(e / W + 1) + e % W
+                                       : (e < (NL - 1) * W + OUT ? L::p_b(NL) + e - (NL - 1) * W
+                                                                 : L::NPARAM + e - (NL - 1) * W - OUT);
+      row[idx] = v;
+    }
+    return;
   }
   for (int turn = 0; turn < (L::OWN ? NWV : 1); ++turn) {
     if constexpr (L::OWN) {
