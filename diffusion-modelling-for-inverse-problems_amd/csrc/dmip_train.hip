@@ -261,13 +261,29 @@ __device__ __forceinline__ float rec_val(const u32x4 (&d)[2], int R, int r) {
 // the forward half's record writes: row tile R's coefficients (q 3..5) as soon as they exist, and the activations
 // (q 0..2) straight from the packed bf16 B operand of the next layer once its R pair is complete -- the bf16 hi part,
 // the same RNE rounding -- so the writes hold no extra registers across R
-template <int NL>
-__device__ __forceinline__ void rec_put_coef(uint32_t* rec, long long tile, int li, int R, int lane, const float (&d1)[4],
-                                             const float (&b)[4], const float (&d1c)[4]) {
-  *rec_half<NL>(rec, tile, li, R, 3, lane) = u32x2{pk_f16(d1[0], d1[1]), pk_f16(d1[2], d1[3])};
-  *rec_half<NL>(rec, tile, li, R, 4, lane) = u32x2{pk_bf16(b[0], b[1]), pk_bf16(b[2], b[3])};
-  *rec_half<NL>(rec, tile, li, R, 5, lane) = u32x2{pk_f16(d1c[0], d1c[1]), pk_f16(d1c[2], d1c[3])};
-}
+// row tile R's coefficients (q 3..5)
+struct RecCoef {
+  uint32_t st[3][2];
+  template <int NL>
+  __device__ __forceinline__ void put(uint32_t* rec, long long tile, int li, int R, int lane, const float (&d1)[4],
+                                      const float (&b)[4], const float (&d1c)[4]) {
+    const uint32_t v[3][2] = {{pk_f16(d1[0], d1[1]), pk_f16(d1[2], d1[3])},
+                              {pk_bf16(b[0], b[1]), pk_bf16(b[2], b[3])},
+                              {pk_f16(d1c[0], d1c[1]), pk_f16(d1c[2], d1c[3])}};
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+#ifdef DMIP_REC_STASH  // A/B variant (scripts/build_variant.sh): full 16-byte pieces at odd R
+      if ((R & 1) == 0) {
+        st[q][0] = v[q][0], st[q][1] = v[q][1];
+      } else {
+        *rec_at<NL>(rec, tile, li, R >> 1, 3 + q, lane) = u32x4{st[q][0], st[q][1], v[q][0], v[q][1]};
+      }
+#else  // each R's 8-byte half at once (holds nothing across R: fewer spills in the two-waves-per-SIMD forward half)
+      *rec_half<NL>(rec, tile, li, R, 3 + q, lane) = u32x2{v[q][0], v[q][1]};
+#endif
+    }
+  }
+};
 template <int NL>
 __device__ __forceinline__ void rec_put_h(uint32_t* rec, long long tile, int li, int Rp, int lane, const bf16x8 (&h)[3][2]) {
 #pragma unroll
@@ -528,6 +544,10 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
     const float dalpha = alpha * (-0.5f * t * p.bdiff - 0.5f * p.bmin);
     const float dstd = ex * (t * p.bdiff + p.bmin) / (2.0f * std_);
     const float dg = p.bdiff / (2.0f * gg);
+    // the per-sample terms divide by g(t) about 20 times: one correctly rounded reciprocal, then products (each a
+    // full-precision fp32 division expands to ~10 VALU; the products differ by at most an ulp, far inside the
+    // kernel's gates, tests/test_gpu_parity.py)
+    const float igg = 1.0f / gg;
     float xt[D], xd[D];
 #pragma unroll
     for (int k = 0; k < D; ++k) {
@@ -560,6 +580,7 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
     {
       // the record reverse half's input (PH 1 with p.rec; a uniform branch per layer)
       const bool recw = PH == 1 && p.rec != nullptr;
+      RecCoef rcw;
       bf16x8 H[NSTREAM][2], HL[3][2];  // HL: lo residuals of the split streams P, V, C
 #pragma unroll
       for (int R = 0; R < 4; ++R) {
@@ -584,7 +605,7 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
           cd1[r] = d1, cb[r] = d2 * zV[r], cd1c[r] = (1.0f - hc * hc) * (1.0f - pc * pc);
         }
         if (recw) {
-          rec_put_coef<NL>(p.rec, tile, 0, R, lane, cd1, cb, cd1c);
+          rcw.put<NL>(p.rec, tile, 0, R, lane, cd1, cb, cd1c);
           if (R & 1) rec_put_h<NL>(p.rec, tile, 0, R >> 1, lane, *(const bf16x8(*)[3][2])H);
         }
       }
@@ -628,7 +649,7 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
             cd1[r] = d1, cb[r] = d2 * Z[1][r], cd1c[r] = 1.0f - hc * hc;
           }
           if (recw) {
-            rec_put_coef<NL>(p.rec, tile, l, R, lane, cd1, cb, cd1c);
+            rcw.put<NL>(p.rec, tile, l, R, lane, cd1, cb, cd1c);
             if (R & 1) rec_put_h<NL>(p.rec, tile, l, R >> 1, lane, *(const bf16x8(*)[3][2])Hn);
           }
         }
@@ -656,7 +677,7 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
     {
       float s[OUT], dLds[OUT];
 #pragma unroll
-      for (int k = 0; k < OUT; ++k) s[k] = aS[0][k] / gg, dLds[k] = 0.0f, abV[k] = 0.0f, abC[k] = 0.0f;
+      for (int k = 0; k < OUT; ++k) s[k] = aS[0][k] * igg, dLds[k] = 0.0f, abV[k] = 0.0f, abC[k] = 0.0f;
       float dsm = 0.0f;
 #pragma unroll
       for (int k = 0; k < OUT; ++k) {
@@ -668,13 +689,13 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
       if (p.pde != 0) {
         float dsdt[OUT], u[OUT], dds[OUT];
 #pragma unroll
-        for (int k = 0; k < OUT; ++k) dsdt[k] = aS[1][k] / gg - aS[0][k] * dg / (gg * gg);
+        for (int k = 0; k < OUT; ++k) dsdt[k] = aS[1][k] * igg - aS[0][k] * dg * (igg * igg);
         if (p.pde == 1) {  // ScoreFPELoss (losses.py:78-98)
           float J[OUT][D];
 #pragma unroll
           for (int i = 0; i < OUT; ++i)
 #pragma unroll
-            for (int a = 0; a < D; ++a) J[i][a] = aS[3 + a][i] / gg;
+            for (int a = 0; a < D; ++a) J[i][a] = aS[3 + a][i] * igg;
           // second-order streams: 5 = (0,0), 6 = (0,1), 7 = (1,1)
 #pragma unroll
           for (int j = 0; j < D; ++j) {
@@ -683,7 +704,7 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
             for (int i = 0; i < OUT; ++i) {
               const int lo = i < j ? i : j, hi = i < j ? j : i;
               const int sidx = lo == 0 ? (hi == 0 ? 5 : 6) : 7;
-              gx += aS[sidx][i] / gg + (2.0f * s[i] + xt[i]) * J[i][j];
+              gx += aS[sidx][i] * igg + (2.0f * s[i] + xt[i]) * J[i][j];
             }
             u[j] = dsdt[j] - 0.5f * beta * gx;
           }
@@ -708,8 +729,8 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
 #pragma unroll
         for (int k = 0; k < OUT; ++k) {
           const float c = p.lam * dds[k] * p.inv_n;
-          abV[k] = c / gg;
-          dLds[k] += c * (-dg / gg);
+          abV[k] = c * igg;
+          dLds[k] += c * (-dg * igg);
         }
       }
       float ic = 0.0f;
@@ -733,7 +754,7 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
         ic = p.lam2 * rows / D;
       }
 #pragma unroll
-      for (int k = 0; k < OUT; ++k) abP[k] = dLds[k] / gg;
+      for (int k = 0; k < OUT; ++k) abP[k] = dLds[k] * igg;
       if (!valid) {
 #pragma unroll
         for (int k = 0; k < OUT; ++k) abP[k] = abV[k] = abC[k] = 0.0f;
