@@ -56,37 +56,34 @@ typedef __attribute__((address_space(3))) void lds_void;
 
 struct Eng {
   char* lds;
-  const char* pimg;
-  const char* simg;
+  // the per-step chunk stream in stream order (DPS: launch_dps_x3 copies the prior's 17 forward chunks, the
+  // surrogate's 35 and the prior's 18 reverse chunks into one image; MH: the surrogate's image, whose first 17 chunks
+  // are its forward pass): chunk c of a step is image chunk c
+  const char* img;
   int c_issue, s_issue, s_read;
   int w, lane, g;
-  // the per-step chunk stream: chunks [0, na) of image a, then [0, nb) of image b, then image a's chunks [na, ...)
-  // up to nstream (DPS: a = the prior's 17 forward chunks, b = the surrogate's 35, then the prior's 18 reverse
-  // chunks; MH: the surrogate's 17 forward chunks alone, na = nstream = 17, nb = 0)
-  int na = NPF, nb = NS, nstream = NSTREAM;
+  int nstream = NSTREAM;
 
   // the next refill: its source chunk and ring slot (the stream position advances); its PPW pieces per wave go out at
   // once (ring_issue) or beside the consuming chunk's MFMAs (Spread, split_product_h). The pieces are buffer LDS-DMA
   // (dmip_x3k.h's form): the image's buffer resource, the chunk's byte offset as the scalar offset, the wave's and
   // lane's part as the per-lane offset -- no per-piece 64-bit address arithmetic (a VALU and two SALU a piece with
-  // global_load_lds)
-  __amdgpu_buffer_rsrc_t rp, rs, dma_rsrc;
+  // global_load_lds). Round 6: one image in stream order, one buffer resource, the chunk's offset c * 32 KiB (round 5
+  // selected between two images' resources and offsets per chunk: 8 more SGPRs in a kernel at the 106-SGPR limit,
+  // whose spills cost ~850 v_readlane / v_writelane per step)
+  __amdgpu_buffer_rsrc_t dma_rsrc;
   unsigned voff;  // w PPW KiB + 16 lane
   int dma_soff;
   char* dma_dst;
   __device__ __forceinline__ void init_dma() {
-    rp = __builtin_amdgcn_make_buffer_rsrc((void*)pimg, 0, kDpsX3PriorChunks * CHUNK, 0x00020000);
-    rs = __builtin_amdgcn_make_buffer_rsrc((void*)simg, 0, kDpsX3SurChunks * CHUNK, 0x00020000);
+    dma_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)img, 0, nstream * CHUNK, 0x00020000);
     voff = (unsigned)(w * PPW * 1024 + lane * 16);
   }
   __device__ __forceinline__ void ring_target() {
     const int c = __builtin_amdgcn_readfirstlane(c_issue);
-    const int a = __builtin_amdgcn_readfirstlane(na), b = __builtin_amdgcn_readfirstlane(nb);
-    const bool prior = c < a || c >= a + b;
-    dma_rsrc = prior ? rp : rs;
-    dma_soff = __builtin_amdgcn_readfirstlane((c < a ? c : (c < a + b ? c - a : c - b)) * CHUNK);
+    dma_soff = c * CHUNK;
     dma_dst = lds + RING + __builtin_amdgcn_readfirstlane(s_issue) * CHUNK;
-    c_issue = c_issue + 1 == nstream ? 0 : c_issue + 1;
+    c_issue = c + 1 == nstream ? 0 : c + 1;
     s_issue = s_issue + 1 == R ? 0 : s_issue + 1;
   }
   template <int Q>
@@ -245,6 +242,21 @@ __device__ __forceinline__ bool range_bad(int mx) { return !(__int_as_float(mx) 
 // relu on the bits (v_max_i32 with 0; the float select costs a NaN-quieting v_max more): z > 0 passes, every other
 // value (-0 and the negative NaNs included) becomes +0
 __device__ __forceinline__ float relu_bits(float z) { return __int_as_float(max(__float_as_int(z), 0)); }
+// relu and its mask bit. The compare's lane mask lives in an SGPR pair; at the kernel's 106-SGPR limit the 64 masks of a
+// surrogate layer spill to VGPR lanes (v_writelane / v_readlane). Round 6 tried the bit as min(relu bits, 1), VALU only
+// (DMIP_DPS_BITS_MASK, identical results): the lane spills went away but 172 B of VGPRs spilled instead and the kernel
+// ran 1.8 % slower on the same box (profiles/r6_dps/), so the compare stays
+__device__ __forceinline__ void relu_mask(float z, float& h, uint32_t& m, int bit) {
+#ifdef DMIP_DPS_BITS_MASK
+  const int hb = max(__float_as_int(z), 0);
+  h = __int_as_float(hb);
+  m |= min((uint32_t)hb, 1u) << bit;
+#else
+  const bool pos = z > 0.0f;
+  h = pos ? z : 0.0f;
+  m |= (pos ? 1u : 0u) << bit;
+#endif
+}
 
 // The per-tile epilogues of a 256 -> 256 layer (tile o of the layer's output, f32 pre-activations z):
 //   PriorFwd:  r = 1 / (1 + 2^z) (z pre-scaled by 2 log2 e; the next layer is folded for r), D = 4 r (1 - r)
@@ -268,11 +280,7 @@ struct EpiSurFwd {
   __device__ __forceinline__ void operator()(const f32x4& z, int o, u32x4 (&Oh)[KQ], u32x4 (&Ol)[KQ]) const {
     float h[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const bool pos = z[k] > 0.0f;  // (the float select here: relu_bits plus a separate mask compare spills)
-      h[k] = pos ? z[k] : 0.0f;
-      m[o >> 3] |= (pos ? 1u : 0u) << ((o & 7) * 4 + k);
-    }
+    for (int k = 0; k < 4; ++k) relu_mask(z[k], h[k], m[o >> 3], (o & 7) * 4 + k);
     track4_pos(*mx, h);
     store_pair(h, o, Oh, Ol);
   }
@@ -442,7 +450,7 @@ __global__ void __launch_bounds__(NW * 64, 1) dps_x3_kernel(DpsX3Params p) {
   const int yi = blockIdx.y;
   const long long c_local = (long long)blockIdx.x * (NW * 16) + w * 16 + j;
   const bool valid = c_local < p.n_chains;
-  Eng e{lds, p.pimg, p.simg, 0, 0, 0, w, lane, g};
+  Eng e{lds, p.img, 0, 0, 0, w, lane, g};
   e.init_dma();
   {
     // resident parts: the two layer-1 images (lanes 0-31 of each tile), the biases, y
@@ -515,11 +523,7 @@ __global__ void __launch_bounds__(NW * 64, 1) dps_x3_kernel(DpsX3Params p) {
     layer1(e, SL1, SB, l1_b<3>(x0h, g), [&](const f32x4& z, int o) {
       float h[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const bool pos = z[k] > 0.0f;
-        h[k] = pos ? z[k] : 0.0f;
-        m1[o >> 3] |= (pos ? 1u : 0u) << ((o & 7) * 4 + k);
-      }
+      for (int k = 0; k < 4; ++k) relu_mask(z[k], h[k], m1[o >> 3], (o & 7) * 4 + k);
       track4_pos(vmax, h);
       store_pair(h, o, Ah, Al);
     });
@@ -917,9 +921,9 @@ __global__ void __launch_bounds__(NW * 64, 1) mh_x3_kernel(MhX3Params p) {
   const long long c_local = (long long)blockIdx.x * (NW * 16) + w * 16 + j;
   const bool valid = c_local < p.n_chains;
   const long long cc = valid ? c_local : 0;
-  Eng e{lds, p.simg, p.simg, 0, 0, 0, w, lane, g};
+  Eng e{lds, p.simg, 0, 0, 0, w, lane, g};
+  e.nstream = kDpsX3SurFwdChunks;
   e.init_dma();
-  e.na = kDpsX3SurFwdChunks, e.nb = 0, e.nstream = kDpsX3SurFwdChunks;
   {
     const uint4* s2 = (const uint4*)p.sl1;
     uint4* d2 = (uint4*)(lds + SL1);
@@ -1108,17 +1112,29 @@ hipError_t launch_mh_x3(const MhX3Params& p, int n_y, hipStream_t st) {
 hipError_t launch_dps_x3(const DpsX3Params& p, int n_y, hipStream_t st) {
   const long long per_wg = dx3::NW * 16;
   const int S = p.num_steps > 0 ? p.num_steps : 1;
-  float4* coef = nullptr;
-  hipError_t e = hipMallocAsync((void**)&coef, (size_t)2 * S * sizeof(float4), st);
+  // one launch-scoped allocation: the stream-ordered image (the kernel's one buffer resource), then the step table
+  constexpr size_t kImg = (size_t)dx3::NSTREAM * dx3::CHUNK;
+  char* buf = nullptr;
+  hipError_t e = hipMallocAsync((void**)&buf, kImg + (size_t)2 * S * sizeof(float4), st);
   if (e != hipSuccess) return e;
+  float4* coef = (float4*)(buf + kImg);
+  constexpr size_t C = dx3::CHUNK;
+  if ((e = hipMemcpyAsync(buf, p.pimg, dx3::NPF * C, hipMemcpyDeviceToDevice, st)) != hipSuccess ||
+      (e = hipMemcpyAsync(buf + dx3::NPF * C, p.simg, dx3::NS * C, hipMemcpyDeviceToDevice, st)) != hipSuccess ||
+      (e = hipMemcpyAsync(buf + (dx3::NPF + dx3::NS) * C, p.pimg + dx3::NPF * C, dx3::NPB * C, hipMemcpyDeviceToDevice,
+                          st)) != hipSuccess) {
+    (void)hipFreeAsync(buf, st);
+    return e;
+  }
   hipLaunchKernelGGL(dx3::dps_x3_coef_kernel, dim3((unsigned)((S + 255) / 256)), dim3(256), 0, st, coef, S, p.T, p.bmin,
                      p.bdiff);
   DpsX3Params q = p;
+  q.img = buf;
   q.coef = (const float*)coef;
   const dim3 grid((unsigned)((p.n_chains + per_wg - 1) / per_wg), (unsigned)n_y), block(dx3::NW * 64);
   hipLaunchKernelGGL(dx3::dps_x3_kernel, grid, block, 0, st, q);
   e = hipGetLastError();
-  (void)hipFreeAsync(coef, st);
+  (void)hipFreeAsync(buf, st);
   return e;
 }
 

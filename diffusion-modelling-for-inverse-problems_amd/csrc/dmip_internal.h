@@ -216,6 +216,7 @@ struct DpsX3Params {
   float* x_out;         // [n_y][n_chains][3]
   unsigned int* err;    // device status word (kErrRange)
   const float* coef;    // per-step (tau, beta, g, 0), (mean_weight, var, 0, 0): filled by launch_dps_x3
+  const char* img;      // the per-step chunk stream in stream order [70][32 KiB]: filled by launch_dps_x3
 };
 hipError_t launch_dps_x3(const DpsX3Params& p, int n_y, hipStream_t st);
 

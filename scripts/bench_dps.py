@@ -103,7 +103,7 @@ def main():
                         "executed_frac": exe / (launch_ms * 1e-3) / 1e12 / peak,
                         "flops_per_chain_step_alg": 2 * F_PRIOR + 2 * F_SUR,
                         "flops_per_chain_step_executed": exe_cs}}
-    if rank == 0:
+    if rank == 0 and a.gt_chains > 0:  # --gt-chains 0: timing only (A/B runs)
         gt = pkg.mh_sample(fm, prm, y[None], a.gt_chains, 1000, 0.5, seed=99)[0]
         xs = x[:a.gt_chains] if x.ndim == 2 else x[0, :a.gt_chains]
         kl, klr = ev.hist_kl(ev.histograms(gt, 75, (-1.2, 1.2))[0], ev.histograms(xs, 75, (-1.2, 1.2))[0])
@@ -126,6 +126,7 @@ def main():
             klc, _ = ev.hist_kl(ev.histograms(gt, 75, (-1.2, 1.2))[0], ev.histograms(xc, 75, (-1.2, 1.2))[0])
             out["quality_cde"] = {"KL2_vs_mcmc": klc, "W1_vs_mcmc": w1(xc, gt), "mean": xc.mean(0).tolist(),
                                   "std": xc.std(0).tolist()}
+    if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -363,8 +363,9 @@ def test_dps_guided_worst_chain_vs_f64_oracle_50_steps(dmip, golden, fm, precisi
              for l in m.prior_net if isinstance(l, torch.nn.Linear)]
     y = golden("data_scat.npz")["y_test"][0]
     n, S = 200, 50
+    dmip._lib.clear_range_status(torch.device(DEV))  # an earlier test's chaotic case may have left a range report
     x = m.sample_device(torch.from_numpy(y).to(DEV), n, S, seed=11, precision=precision)[0].cpu().numpy()
-    dmip._lib.device_status(torch.device(DEV))
+    dmip._lib.device_status(torch.device(DEV))  # this launch: no range report, no hand-over timeout
     ref = O.dps_sample(prior, sur, y, n, S, 11, zeta=0.005, mode="norm")
     assert np.all(np.isfinite(x))
     e = np.abs(x.astype(np.float64) - ref).max(1) / max(1.0, np.abs(ref).max())
