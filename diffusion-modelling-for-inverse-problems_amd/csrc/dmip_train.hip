@@ -381,6 +381,14 @@ __device__ __forceinline__ float row_sum16(float v) {
   return v;
 }
 
+// timing ablation only (scripts/gpu_r6_c5abl.sh; wrong gradients): the reverse half's weight-gradient contraction
+// MFMAs left out (their scratch reads stay)
+#ifdef DMIP_TRAIN_TIMING_NO_CONTRACT
+#define DMIP_TRAIN_CONTRACT(stmt) asm volatile("" ::"v"(A), "v"(Bm))
+#else
+#define DMIP_TRAIN_CONTRACT(stmt) stmt
+#endif
+
 template <bool GG>
 __device__ __forceinline__ void gadd(float* a, float v) {
   if constexpr (GG) (void)__hip_atomic_fetch_add(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -873,7 +881,7 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
               for (int S = 0; S < 3; ++S) {
                 const bf16x8 A = tread<RS>(SV(v, S), i32, i32 < OUT, hh);
                 const bf16x8 Bm = tread<RS>(SV(v, 3 + S), 32 * U + i32, true, hh);
-                gX = mfma32(A, Bm, gX);
+                DMIP_TRAIN_CONTRACT(gX = mfma32(A, Bm, gX));
               }
           }
         } else {
@@ -973,7 +981,7 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
               for (int S = 0; S < 3; ++S) {
                 const bf16x8 A = tread<RS>(SV(v, S), 32 * w + i32, true, hh);
                 const bf16x8 Bm = tread<RS>(SV(v, 3 + S), i32, i32 <= IN, hh);
-                gX = mfma32(A, Bm, gX);
+                DMIP_TRAIN_CONTRACT(gX = mfma32(A, Bm, gX));
               }
           }
         } else {  // W x W layer li: block (T, U) = (w >> 1, w & 1)
@@ -984,7 +992,7 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
             for (int S = 0; S < 3; ++S) {
               const bf16x8 A = tread<RS>(SV(v, S), 32 * T + i32, true, hh);
               const bf16x8 Bm = tread<RS>(SV(v, 3 + S), 32 * U + i32, true, hh);
-              gW[(li - 1) > 0 ? li - 1 : 0] = mfma32(A, Bm, gW[(li - 1) > 0 ? li - 1 : 0]);
+              DMIP_TRAIN_CONTRACT(gW[(li - 1) > 0 ? li - 1 : 0] = mfma32(A, Bm, gW[(li - 1) > 0 ? li - 1 : 0]));
             }
         }
       } else {
