@@ -86,10 +86,13 @@ struct Eng {
     c_issue = c + 1 == nstream ? 0 : c + 1;
     s_issue = s_issue + 1 == R ? 0 : s_issue + 1;
   }
+  // (round 6: Q's KiB within a group of four pieces in the instruction's offset, which the hardware adds to both the
+  // memory and the LDS address: four pieces share M0 and the scalar offset)
   template <int Q>
   __device__ __forceinline__ void ring_piece() const {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(dma_rsrc, (lds_void*)(dma_dst + (w * PPW + Q) * 1024), 16, voff,
-                                             dma_soff + Q * 1024, 0, 0);
+    constexpr int QH = Q >> 2, QL = Q & 3;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(dma_rsrc, (lds_void*)(dma_dst + (w * PPW + 4 * QH) * 1024), 16, voff,
+                                             dma_soff + QH * 4096, QL * 1024, 0);
   }
   __device__ __forceinline__ void ring_issue() {
     ring_target();

@@ -261,33 +261,35 @@ __device__ __forceinline__ float rec_val(const u32x4 (&d)[2], int R, int r) {
 // the forward half's record writes: row tile R's coefficients (q 3..5) as soon as they exist, and the activations
 // (q 0..2) straight from the packed bf16 B operand of the next layer once its R pair is complete -- the bf16 hi part,
 // the same RNE rounding -- so the writes hold no extra registers across R
-// row tile R's coefficients (q 3..5)
-struct RecCoef {
-  uint32_t st[3][2];
-  template <int NL>
-  __device__ __forceinline__ void put(uint32_t* rec, long long tile, int li, int R, int lane, const float (&d1)[4],
-                                      const float (&b)[4], const float (&d1c)[4]) {
-    const uint32_t v[3][2] = {{pk_f16(d1[0], d1[1]), pk_f16(d1[2], d1[3])},
-                              {pk_bf16(b[0], b[1]), pk_bf16(b[2], b[3])},
-                              {pk_f16(d1c[0], d1c[1]), pk_f16(d1c[2], d1c[3])}};
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-#ifdef DMIP_REC_STASH  // A/B variant (scripts/build_variant.sh): full 16-byte pieces at odd R
-      if ((R & 1) == 0) {
-        st[q][0] = v[q][0], st[q][1] = v[q][1];
-      } else {
-        *rec_at<NL>(rec, tile, li, R >> 1, 3 + q, lane) = u32x4{st[q][0], st[q][1], v[q][0], v[q][1]};
-      }
-#else  // each R's 8-byte half at once (holds nothing across R: fewer spills in the two-waves-per-SIMD forward half)
-      *rec_half<NL>(rec, tile, li, R, 3 + q, lane) = u32x2{v[q][0], v[q][1]};
-#endif
-    }
-  }
-};
+// The forward half's record writes go through a per-tile buffer resource (the tile is wave-uniform): the piece's
+// offset is a compile-time scalar offset and the lane's 16 bytes (+ 8 for an odd row tile) the per-lane offset, so no
+// 64-bit address is formed or kept per store (with global stores the records spilled 128 B of the forward half's
+// 256-register budget)
 template <int NL>
-__device__ __forceinline__ void rec_put_h(uint32_t* rec, long long tile, int li, int Rp, int lane, const bf16x8 (&h)[3][2]) {
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rec_rsrc(uint32_t* rec, long long tile) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)((char*)rec + (size_t)tile * NL * kTrainRecTileBytes), 0,
+                                           NL * kTrainRecTileBytes, 0x00020000);
+}
+constexpr int rec_off(int li, int Rp, int q) { return ((li * 2 + Rp) * kTrainRecQ + q) * 1024; }
+
+// row tile R's coefficients (q 3..5): each R's 8-byte half at once (holds nothing across R; storing each value pair
+// as soon as it exists, or full 16-byte pieces at odd R, measured more spills)
+template <int NL>
+__device__ __forceinline__ void rec_put_coef(__amdgpu_buffer_rsrc_t rr, int li, int R, int lane, const float (&d1)[4],
+                                             const float (&b)[4], const float (&d1c)[4]) {
+  const int vo = lane * 16 + (R & 1) * 8;
+  __builtin_amdgcn_raw_buffer_store_b64(u32x2{pk_f16(d1[0], d1[1]), pk_f16(d1[2], d1[3])}, rr, vo,
+                                        rec_off(li, R >> 1, 3), 0);
+  __builtin_amdgcn_raw_buffer_store_b64(u32x2{pk_bf16(b[0], b[1]), pk_bf16(b[2], b[3])}, rr, vo,
+                                        rec_off(li, R >> 1, 4), 0);
+  __builtin_amdgcn_raw_buffer_store_b64(u32x2{pk_f16(d1c[0], d1c[1]), pk_f16(d1c[2], d1c[3])}, rr, vo,
+                                        rec_off(li, R >> 1, 5), 0);
+}
+template <int NL>
+__device__ __forceinline__ void rec_put_h(__amdgpu_buffer_rsrc_t rr, int li, int Rp, int lane, const bf16x8 (&h)[3][2]) {
 #pragma unroll
-  for (int q = 0; q < 3; ++q) *rec_at<NL>(rec, tile, li, Rp, q, lane) = __builtin_bit_cast(u32x4, h[q][Rp]);
+  for (int q = 0; q < 3; ++q)
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, h[q][Rp]), rr, lane * 16, rec_off(li, Rp, q), 0);
 }
 
 // The shared part of the LDS image (weight fragments, biases, layer-1 columns), packed ONCE per
@@ -588,7 +590,7 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
     {
       // the record reverse half's input (PH 1 with p.rec; a uniform branch per layer)
       const bool recw = PH == 1 && p.rec != nullptr;
-      RecCoef rcw;
+      const __amdgpu_buffer_rsrc_t rr = rec_rsrc<NL>(recw ? p.rec : (uint32_t*)p.adj, tile);
       bf16x8 H[NSTREAM][2], HL[3][2];  // HL: lo residuals of the split streams P, V, C
 #pragma unroll
       for (int R = 0; R < 4; ++R) {
@@ -613,8 +615,8 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
           cd1[r] = d1, cb[r] = d2 * zV[r], cd1c[r] = (1.0f - hc * hc) * (1.0f - pc * pc);
         }
         if (recw) {
-          rcw.put<NL>(p.rec, tile, 0, R, lane, cd1, cb, cd1c);
-          if (R & 1) rec_put_h<NL>(p.rec, tile, 0, R >> 1, lane, *(const bf16x8(*)[3][2])H);
+          rec_put_coef<NL>(rr, 0, R, lane, cd1, cb, cd1c);
+          if (R & 1) rec_put_h<NL>(rr, 0, R >> 1, lane, *(const bf16x8(*)[3][2])H);
         }
       }
 #pragma unroll
@@ -657,8 +659,8 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
             cd1[r] = d1, cb[r] = d2 * Z[1][r], cd1c[r] = 1.0f - hc * hc;
           }
           if (recw) {
-            rcw.put<NL>(p.rec, tile, l, R, lane, cd1, cb, cd1c);
-            if (R & 1) rec_put_h<NL>(p.rec, tile, l, R >> 1, lane, *(const bf16x8(*)[3][2])Hn);
+            rec_put_coef<NL>(rr, l, R, lane, cd1, cb, cd1c);
+            if (R & 1) rec_put_h<NL>(rr, l, R >> 1, lane, *(const bf16x8(*)[3][2])Hn);
           }
         }
 #pragma unroll

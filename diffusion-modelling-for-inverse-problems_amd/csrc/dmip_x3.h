@@ -58,6 +58,11 @@ struct Shape {
 };
 
 constexpr int kLdsBudget = 160 * 1024;
+// A/B knob (scripts/build_variant.sh): the round-5 per-piece scalar offsets and LDS addresses
+#ifndef DMIP_X3_NO_IMM
+#define DMIP_X3_NO_IMM 0
+#endif
+constexpr bool X3_NO_IMM = DMIP_X3_NO_IMM;
 constexpr int kMaxHidden = 3;
 constexpr int k1q_of(int nv) { return (3 * nv + 31) / 32; }
 constexpr int align16(int v) { return (v + 15) / 16 * 16; }
@@ -262,16 +267,24 @@ struct XEngine {
   __device__ __forceinline__ void ring_target() {
     const int c = __builtin_amdgcn_readfirstlane(c_issue);
     const int n = __builtin_amdgcn_readfirstlane(ncn);
+    // (round 6 tried setting a one-network engine's resource once, in init, and only the offset per chunk: with the
+    // immediate-offset pieces below it gave wrong chains at W = 512 with 1 and 3 hidden layers, right ones with 2, and
+    // either change alone was right; not understood, not kept -- scripts/x3_w512_debug.py)
     dma_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(c < n ? img[0] : img[1]), 0, n * CHUNK, 0x00020000);
     dma_soff = __builtin_amdgcn_readfirstlane((c < n ? c : c - n) * CHUNK);
     dma_dst = lds + RING_OFF + __builtin_amdgcn_readfirstlane(s_issue) * CHUNK;
     c_issue = c_issue + 1 == NNET * ncn ? 0 : c_issue + 1;
     s_issue = s_issue + 1 == R ? 0 : s_issue + 1;
   }
+  // (round 6: the instruction's 12-bit offset carries Q's KiB within a group of four pieces -- the hardware adds it to
+  // both the memory and the LDS address -- so four consecutive pieces share M0 and the scalar offset)
+  // (CDiffE at W = 512, L1R, keeps the per-piece form: with the shared offsets its streamed layer 1 spilled 12 B)
+  static constexpr bool IMM = !X3_NO_IMM && !L1R;
   template <int Q>
   __device__ __forceinline__ void ring_piece() const {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(dma_rsrc, (lds_void*)(dma_dst + (w * PPW + Q) * 1024), 16, voff,
-                                             dma_soff + Q * 1024, 0, 0);
+    constexpr int QH = IMM ? Q >> 2 : Q, QL = IMM ? Q & 3 : 0;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(dma_rsrc, (lds_void*)(dma_dst + (w * PPW + (IMM ? 4 : 1) * QH) * 1024), 16,
+                                             voff, dma_soff + QH * (IMM ? 4096 : 1024), QL * 1024, 0);
   }
   template <int Q = 0>
   __device__ __forceinline__ void ring_pieces() const {

@@ -126,10 +126,14 @@ struct KEngine {
   mutable uint64_t ph_vm = 0, ph_bar = 0;  // DIAG & 2: cycles in the ring's vmcnt waits and barriers
 
   // piece Q of chunk C of the step image into slot S (LDS-DMA: 1 KiB per wave-instruction)
+  // (round 6: the instruction's 12-bit offset carries Q's KiB within a group of four pieces -- the hardware adds it to
+  // both the memory and the LDS address -- so four consecutive pieces share M0 and the scalar offset: two scalar moves
+  // per four pieces instead of two per piece)
   template <int C, int S, int Q>
   __device__ __forceinline__ void issue_piece() const {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(lds + KLay::RING + S * CHUNK + (w * PPW + Q) * 1024), 16,
-                                             voff, C * CHUNK + Q * 1024, 0, 0);
+    constexpr int QH = Q >> 2, QL = Q & 3;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(lds + KLay::RING + S * CHUNK + (w * PPW + 4 * QH) * 1024),
+                                             16, voff, C * CHUNK + QH * 4096, QL * 1024, 0);
   }
   template <int C, int S, int Q = 0>
   __device__ __forceinline__ void issue() const {
