@@ -223,7 +223,7 @@ __device__ __forceinline__ float x3_act_r2(float zs) {
 // each evaluation streams (nl - 1) NCH hidden chunks then one output chunk, in the host image's order.
 // DIAG (timing ablations only, never on the product path; DMIP_X3_DIAG): bit 0 = no ring (no DMA, no
 // barrier: stale weights), bit 1 = hidden activations replaced by the split alone, bit 2 = the same for
-// layer 1's double tanh
+// layer 1's double tanh, bit 3 = no ring barrier (DMA and vmcnt waits kept), bit 4 = no LDS-DMA pieces (barrier kept)
 template <int W, int NNET, int K1Q, int R, int RING_OFF, int DIAG = 0, bool L1R = false, bool L1H = false>
 struct XEngine {
   using S = Shape<W>;
@@ -282,6 +282,7 @@ struct XEngine {
   static constexpr bool IMM = !X3_NO_IMM && !L1R;
   template <int Q>
   __device__ __forceinline__ void ring_piece() const {
+    if constexpr ((DIAG & 16) != 0) return;
     constexpr int QH = IMM ? Q >> 2 : Q, QL = IMM ? Q & 3 : 0;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(dma_rsrc, (lds_void*)(dma_dst + (w * PPW + (IMM ? 4 : 1) * QH) * 1024), 16,
                                              voff, dma_soff + QH * (IMM ? 4096 : 1024), QL * 1024, 0);
@@ -334,7 +335,7 @@ struct XEngine {
       return slot;
     }
     wait_vmcnt<(R - 2) * PPW>();
-    lds_barrier();
+    if constexpr ((DIAG & 8) == 0) lds_barrier();
     ring_issue();
     const char* slot = lds + RING_OFF + s_read * CHUNK;
     s_read = s_read + 1 == R ? 0 : s_read + 1;
@@ -345,7 +346,7 @@ struct XEngine {
   // within the chunk that set it, so the vmcnt accounting of chunk_sync holds.
   __device__ __forceinline__ const char* chunk_sync_deferred() {
     wait_vmcnt<(R - 2) * PPW>();
-    lds_barrier();
+    if constexpr ((DIAG & 8) == 0) lds_barrier();
     ring_target();
     const char* slot = lds + RING_OFF + s_read * CHUNK;
     s_read = s_read + 1 == R ? 0 : s_read + 1;
