@@ -223,7 +223,8 @@ __device__ __forceinline__ float x3_act_r2(float zs) {
 // each evaluation streams (nl - 1) NCH hidden chunks then one output chunk, in the host image's order.
 // DIAG (timing ablations only, never on the product path; DMIP_X3_DIAG): bit 0 = no ring (no DMA, no
 // barrier: stale weights), bit 1 = hidden activations replaced by the split alone, bit 2 = the same for
-// layer 1's double tanh, bit 3 = no ring barrier (DMA and vmcnt waits kept), bit 4 = no LDS-DMA pieces (barrier kept)
+// layer 1's double tanh, bit 3 = no ring barrier (DMA and vmcnt waits kept), bit 4 = no LDS-DMA pieces (barrier kept),
+// bit 5 = no vmcnt wait for the ring (pieces and barrier kept: the weights may be read before they land)
 template <int W, int NNET, int K1Q, int R, int RING_OFF, int DIAG = 0, bool L1R = false, bool L1H = false>
 struct XEngine {
   using S = Shape<W>;
@@ -334,7 +335,7 @@ struct XEngine {
       s_read = s_read + 1 == R ? 0 : s_read + 1;
       return slot;
     }
-    wait_vmcnt<(R - 2) * PPW>();
+    if constexpr ((DIAG & 32) == 0) wait_vmcnt<(R - 2) * PPW>();
     if constexpr ((DIAG & 8) == 0) lds_barrier();
     ring_issue();
     const char* slot = lds + RING_OFF + s_read * CHUNK;
@@ -345,7 +346,7 @@ struct XEngine {
   // same waits and barrier, the refill's target set but nothing issued yet. The pieces of a refill are all issued
   // within the chunk that set it, so the vmcnt accounting of chunk_sync holds.
   __device__ __forceinline__ const char* chunk_sync_deferred() {
-    wait_vmcnt<(R - 2) * PPW>();
+    if constexpr ((DIAG & 32) == 0) wait_vmcnt<(R - 2) * PPW>();
     if constexpr ((DIAG & 8) == 0) lds_barrier();
     ring_target();
     const char* slot = lds + RING_OFF + s_read * CHUNK;

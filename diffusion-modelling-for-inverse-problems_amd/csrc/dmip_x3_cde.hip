@@ -6,7 +6,7 @@
 namespace dmip {
 
 #ifdef DMIP_DIAG
-// Diagnostic library only (make diag; never the product build): DMIP_X3_DIAG=d (1..7, 8, 16, 24) runs the timing ablation
+// Diagnostic library only (make diag; never the product build): DMIP_X3_DIAG=d (1..7, 8, 16, 24, 32, 40) runs the timing ablation
 // DIAG = d of the width-256 / width-512, xdim-3 CDE kernels (dmip_x3.h XEngine); see profiles/README.md.
 static int x3_diag() {
   const char* e = getenv("DMIP_X3_DIAG");
@@ -23,7 +23,7 @@ hipError_t launch_x3_sampler_cde(const X3SamplerParams& p, int width, int xdim, 
   case d:                                                                                       \
     return width == 256 ? launch_x3_sampler_t<SAMPLER_CDE, 256, 3, 0, false, d>(p, n_y, st)    \
                         : launch_x3_sampler_t<SAMPLER_CDE, 512, 3, 0, false, d>(p, n_y, st);
-      DG(1) DG(2) DG(3) DG(4) DG(6) DG(7) DG(8) DG(16) DG(24)
+      DG(1) DG(2) DG(3) DG(4) DG(6) DG(7) DG(8) DG(16) DG(24) DG(32) DG(40)
 #undef DG
       default: break;
     }

@@ -7,7 +7,7 @@ TAG=${1:-r6_ring}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
-for d in 0 1 8 16 24; do
+for d in ${DIAGS:-0 1 8 16 24}; do
   echo "=== diag $d ($(date +%T))" | tee -a "$OUT/steps.log"
   DMIP_LIB=abv/diag/libdmip_diag.so DMIP_X3_DIAG=$d timeout -k 10 300 python -u scripts/bench_x3_rows.py \
     --rows cde512 --reps 2 > "$OUT/diag_$d.log" 2>&1
