@@ -245,10 +245,11 @@ __device__ __forceinline__ bool range_bad(int mx) { return !(__int_as_float(mx) 
 // relu on the bits (v_max_i32 with 0; the float select costs a NaN-quieting v_max more): z > 0 passes, every other
 // value (-0 and the negative NaNs included) becomes +0
 __device__ __forceinline__ float relu_bits(float z) { return __int_as_float(max(__float_as_int(z), 0)); }
-// relu and its mask bit. The compare's lane mask lives in an SGPR pair; at the kernel's 106-SGPR limit the 64 masks of a
-// surrogate layer spill to VGPR lanes (v_writelane / v_readlane). Round 6 tried the bit as min(relu bits, 1), VALU only
-// (DMIP_DPS_BITS_MASK, identical results): the lane spills went away but 172 B of VGPRs spilled instead and the kernel
-// ran 1.8 % slower on the same box (profiles/r6_dps/), so the compare stays
+// relu and its mask bit, packed per lane in a VGPR word. Left to itself the compiler keeps each bit of the word as the
+// compare's 64-lane SGPR pair; at the kernel's 106-SGPR limit the 64 masks of a surrogate layer then spill to VGPR lanes
+// (≈830 v_writelane / v_readlane per step). Round 6: the empty asm after each update pins the word in a VGPR, so
+// the bits are built by VALU (no lane spills, no scratch; same box 843 -> 835 ms, profiles/r6_vmask/). (The bit as
+// min(relu bits, 1), DMIP_DPS_BITS_MASK, also removed the lane spills but spilled 172 B of VGPRs and lost 1.8 %.)
 __device__ __forceinline__ void relu_mask(float z, float& h, uint32_t& m, int bit) {
 #ifdef DMIP_DPS_BITS_MASK
   const int hb = max(__float_as_int(z), 0);
@@ -258,6 +259,7 @@ __device__ __forceinline__ void relu_mask(float z, float& h, uint32_t& m, int bi
   const bool pos = z > 0.0f;
   h = pos ? z : 0.0f;
   m |= (pos ? 1u : 0u) << bit;
+  asm volatile("" : "+v"(m));
 #endif
 }
 
@@ -327,7 +329,10 @@ struct EpiBackMask {
   __device__ __forceinline__ void operator()(const f32x4& z, int o, u32x4 (&Oh)[KQ], u32x4 (&Ol)[KQ]) const {
     float v[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) v[k] = ((m[o >> 3] >> ((o & 7) * 4 + k)) & 1u) ? z[k] : 0.0f;
+    for (int k = 0; k < 4; ++k) {  // z AND the bit sign-extended to 32 (v_bfe_i32 + v_and: +0 where relu was off)
+      const int keep = __builtin_amdgcn_sbfe((int)m[o >> 3], (o & 7) * 4 + k, 1);
+      v[k] = __int_as_float(__float_as_int(z[k]) & keep);
+    }
     track4(*mx, v);
     store_pair(v, o, Oh, Ol);
   }

@@ -2,13 +2,14 @@
 # DPS (config 4): the DPS / MH GPU tests, then the in-tree library against A/B variant libraries (DMIP_LIB),
 # alternating processes on one box (scripts/bench_dps.py, 262,144 chains x 1000 steps; KL2 vs a 30k-chain MH
 # ground truth in the first pass only).
-#   usage: bash scripts/gpu_r6_dps.sh <tag> <variant.so>...
+#   usage: [PYTEST_LIB=<variant.so>] bash scripts/gpu_r6_dps.sh <tag> <variant.so>...
+# (PYTEST_LIB: the tests run on that library instead of the in-tree one)
 set -u
 TAG=$1; shift
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
-timeout -k 10 600 python -u -m pytest -q --timeout 240 --timeout-method thread -p no:cacheprovider -rf -s \
+env ${PYTEST_LIB:+DMIP_LIB=$PYTEST_LIB} timeout -k 10 600 python -u -m pytest -q --timeout 240 --timeout-method thread -p no:cacheprovider -rf -s \
   tests/test_gpu_surrogate.py -k "dps or mh" > "$OUT/pytest_dps.log" 2>&1
 rc=$?; echo "pytest rc=$rc: $(tail -1 $OUT/pytest_dps.log)"; case $rc in 0|1) ;; *) exit $rc ;; esac
 for r in 1 2; do
