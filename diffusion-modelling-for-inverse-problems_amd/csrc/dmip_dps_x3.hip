@@ -37,6 +37,13 @@ using x3::mfma16;
 
 constexpr int W = 256, ST = 16, KQ = 8, CT = 2, TILE = KQ * 2048, CHUNK = CT * TILE, NCH = ST / CT;
 constexpr int NW = 4, R = 4, PPW = CHUNK / 1024 / NW;
+// fragment pairs read ahead in a chunk's MFMA chain, in units (3 MFMAs each); DMIP_DPS_FPF = 2 for A/B builds
+#ifdef DMIP_DPS_FPF
+constexpr int FPF = DMIP_DPS_FPF;
+#else
+constexpr int FPF = 1;
+#endif
+static_assert(FPF == 1 || FPF == 2, "read-ahead depth");
 static_assert(CHUNK == 32768 && PPW == 8, "ring geometry");
 // the per-step chunk stream: prior image chunks [0, 17) = P2 (8) | P3 (8) | Pout (1), then the surrogate's 35,
 // then prior chunks [17, 35) = P4^T (1) | P3^T (8) | P2^T (8) | P1^T (1)
@@ -141,7 +148,8 @@ struct Eng {
   // pair read ahead at the last unit (nxt). At one wave per SIMD a wave reaching the barrier early waits while its
   // MFMAs are still in the pipe, and no chunk starts with an LDS-latency bubble. R = 4: a refill issued in chunk c
   // lands by B(c + 2)'s wait, one and a half chunks later.
-  u32x4 nxt0, nxt1;
+  u32x4 nxt0, nxt1;  // the next chunk's unit 0 fragment pair
+  u32x4 nxa0, nxa1;  // and its unit 1 pair (FPF = 2)
   __device__ __forceinline__ void start_mid() {
     for (int q = 0; q < R - 1; ++q) ring_issue();
     wait_vmcnt<(R - 2) * PPW>();
@@ -149,6 +157,14 @@ struct Eng {
     const lds_cptr b0 = (lds_cptr)(lds + RING + lane * 16);
     nxt0 = x3::lds_rd<0>(b0);
     nxt1 = x3::lds_rd<1024>(b0);
+    if constexpr (FPF == 2) {
+      nxa0 = x3::lds_rd<2048>(b0);
+      nxa1 = x3::lds_rd<3072>(b0);
+    }
+    wait_next();
+  }
+  __device__ __forceinline__ void wait_next() {
+    if constexpr (FPF == 2) x3::lds_wait2<0>(nxa0, nxa1);
     x3::lds_wait2<0>(nxt0, nxt1);
   }
   // the current chunk's lane base, the ring advanced: the next chunk's lane base in nb
@@ -164,25 +180,30 @@ template <int NU, int U, int Q = 0>
 __device__ __forceinline__ void mid_pieces(const Eng& e);
 
 // units U0 .. U1 - 1 of a chunk of NU k-step units (unit u: hi / lo fragments at 2u, 2u + 1 KiB), accumulator of unit
-// U = acc[(U - U0) / KQ_], B operand (Hh, Hl)[U % KQ_]; fa[U % 2] holds unit U's pair on entry (unit 0: nxt)
+// U = acc[(U - U0) / KQ_], B operand (Hh, Hl)[U % KQ_]; fragment pairs are read FPF units ahead, fa[U % (FPF + 1)]
+// holds unit U's pair on entry (units 0 .. FPF - 1: nxt, nxa)
 template <int KQ_, int NU, int U0, int U1, int NA, int U = U0>
 __device__ __forceinline__ void mid_units(Eng& e, lds_cptr base, lds_cptr nbase, const u32x4 (&Hh)[KQ_],
-                                          const u32x4 (&Hl)[KQ_], f32x4 (&acc)[NA], u32x4 (&fa)[2][2]) {
+                                          const u32x4 (&Hl)[KQ_], f32x4 (&acc)[NA], u32x4 (&fa)[FPF + 1][2]) {
   if constexpr (U < U1) {
     constexpr int MIDU = NU / 2;
-    static_assert(MIDU < NU - 1, "the barrier precedes the read-ahead");
-    if constexpr (U + 1 < NU) {
-      fa[(U + 1) % 2][0] = x3::lds_rd<(2 * (U + 1)) * 1024>(base);
-      fa[(U + 1) % 2][1] = x3::lds_rd<(2 * (U + 1) + 1) * 1024>(base);
-    } else {  // after B(c + 1): the next chunk has landed for every wave
+    static_assert(MIDU < NU - FPF, "the barrier precedes the read-ahead");
+    constexpr int A = U + FPF, S = U % (FPF + 1);
+    if constexpr (A < NU) {
+      fa[A % (FPF + 1)][0] = x3::lds_rd<(2 * A) * 1024>(base);
+      fa[A % (FPF + 1)][1] = x3::lds_rd<(2 * A + 1) * 1024>(base);
+    } else if constexpr (A == NU) {  // after B(c + 1): the next chunk has landed for every wave
       e.nxt0 = x3::lds_rd<0>(nbase);
       e.nxt1 = x3::lds_rd<1024>(nbase);
+    } else {
+      e.nxa0 = x3::lds_rd<2048>(nbase);
+      e.nxa1 = x3::lds_rd<3072>(nbase);
     }
-    x3::lds_wait2<2>(fa[U % 2][0], fa[U % 2][1]);
+    x3::lds_wait2<2 * FPF>(fa[S][0], fa[S][1]);
     constexpr int t = (U - U0) / KQ_, q = U % KQ_;
-    acc[t] = mfma16(fa[U % 2][0], Hl[q], acc[t]);
-    acc[t] = mfma16(fa[U % 2][1], Hh[q], acc[t]);
-    acc[t] = mfma16(fa[U % 2][0], Hh[q], acc[t]);
+    acc[t] = mfma16(fa[S][0], Hl[q], acc[t]);
+    acc[t] = mfma16(fa[S][1], Hh[q], acc[t]);
+    acc[t] = mfma16(fa[S][0], Hh[q], acc[t]);
     if constexpr (U == MIDU) {  // own pieces of chunk c + 1 landed (chunk c + 2's younger), then everyone's
       wait_vmcnt<PPW>();
       lds_barrier();
@@ -205,10 +226,11 @@ template <int KQ_, int NU, int NA>
 __device__ __forceinline__ void mid_chunk(Eng& e, const u32x4 (&Hh)[KQ_], const u32x4 (&Hl)[KQ_], f32x4 (&acc)[NA]) {
   lds_cptr nb;
   const lds_cptr b = e.take(nb);
-  u32x4 fa[2][2];
+  u32x4 fa[FPF + 1][2];
   fa[0][0] = e.nxt0, fa[0][1] = e.nxt1;
+  if constexpr (FPF == 2) fa[1][0] = e.nxa0, fa[1][1] = e.nxa1;
   mid_units<KQ_, NU, 0, NU, NA>(e, b, nb, Hh, Hl, acc, fa);
-  x3::lds_wait2<0>(e.nxt0, e.nxt1);  // an asm load's registers must not leave the chunk before its data lands
+  e.wait_next();  // an asm load's registers must not leave the chunk before its data lands
 }
 
 // (hi, lo) B operand of k-step q from two accumulator-form tiles' f32 values v[2 q], v[2 q + 1] (dmip_x3.h
@@ -383,11 +405,12 @@ __device__ __forceinline__ void wide1(Eng& e, const u32x4& Bh, const u32x4& Bl, 
   {  // one chunk of ST units (one k-step per tile), in two halves of accumulators
     lds_cptr nb;
     const lds_cptr b = e.take(nb);
-    u32x4 fa[2][2];
+    u32x4 fa[FPF + 1][2];
     fa[0][0] = e.nxt0, fa[0][1] = e.nxt1;
+    if constexpr (FPF == 2) fa[1][0] = e.nxa0, fa[1][1] = e.nxa1;
     mid_units<1, ST, 0, ST / 2, ST / 2>(e, b, nb, bh, bl, a0, fa);
     mid_units<1, ST, ST / 2, ST, ST / 2>(e, b, nb, bh, bl, a1, fa);
-    x3::lds_wait2<0>(e.nxt0, e.nxt1);
+    e.wait_next();
   }
 #pragma unroll
   for (int t = 0; t < ST / 2; ++t) epi(a0[t], t, Oh, Ol);
@@ -756,7 +779,8 @@ struct EngK {
   __device__ __forceinline__ f32x4 bias4(int off_bytes, int tile) const {
     return *(const f32x4*)(lds + off_bytes + (16 * tile + 4 * g) * 4);
   }
-  u32x4 nxt0, nxt1;
+  u32x4 nxt0, nxt1;  // the next chunk's unit 0 fragment pair
+  u32x4 nxa0, nxa1;  // and its unit 1 pair (FPF = 2)
   __device__ __forceinline__ void start_mid() {
     for (int q = 0; q < R - 1; ++q) ring_issue();
     wait_vmcnt<(R - 2) * PPW>();
@@ -764,6 +788,14 @@ struct EngK {
     const lds_cptr b0 = (lds_cptr)(lds + RING + lane * 16);
     nxt0 = x3::lds_rd<0>(b0);
     nxt1 = x3::lds_rd<1024>(b0);
+    if constexpr (FPF == 2) {
+      nxa0 = x3::lds_rd<2048>(b0);
+      nxa1 = x3::lds_rd<3072>(b0);
+    }
+    wait_next();
+  }
+  __device__ __forceinline__ void wait_next() {
+    if constexpr (FPF == 2) x3::lds_wait2<0>(nxa0, nxa1);
     x3::lds_wait2<0>(nxt0, nxt1);
   }
   __device__ __forceinline__ lds_cptr take(lds_cptr& nb) {
