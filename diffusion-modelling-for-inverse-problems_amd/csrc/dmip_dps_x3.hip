@@ -44,6 +44,20 @@ constexpr int FPF = DMIP_DPS_FPF;
 constexpr int FPF = 1;
 #endif
 static_assert(FPF == 1 || FPF == 2, "read-ahead depth");
+// timing ablations of A/B builds only (never the product library; the range report is off in them):
+// DMIP_DPS_DIAG bit 0 = no LDS-DMA pieces (stale weights), bit 1 = no ring barriers, bit 2 = no ring vmcnt waits
+#ifdef DMIP_DPS_DIAG
+constexpr int DDIAG = DMIP_DPS_DIAG;
+#else
+constexpr int DDIAG = 0;
+#endif
+__device__ __forceinline__ void ring_barrier() {
+  if constexpr ((DDIAG & 2) == 0) lds_barrier();
+}
+template <int N>
+__device__ __forceinline__ void ring_vmcnt() {
+  if constexpr ((DDIAG & 4) == 0) wait_vmcnt<N>();
+}
 static_assert(CHUNK == 32768 && PPW == 8, "ring geometry");
 // the per-step chunk stream: prior image chunks [0, 17) = P2 (8) | P3 (8) | Pout (1), then the surrogate's 35,
 // then prior chunks [17, 35) = P4^T (1) | P3^T (8) | P2^T (8) | P1^T (1)
@@ -97,6 +111,7 @@ struct Eng {
   // memory and the LDS address: four pieces share M0 and the scalar offset)
   template <int Q>
   __device__ __forceinline__ void ring_piece() const {
+    if constexpr ((DDIAG & 1) != 0) return;
     constexpr int QH = Q >> 2, QL = Q & 3;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(dma_rsrc, (lds_void*)(dma_dst + (w * PPW + 4 * QH) * 1024), 16, voff,
                                              dma_soff + QH * 4096, QL * 1024, 0);
@@ -123,16 +138,16 @@ struct Eng {
   // chunk ago is refilled R - 1 chunks ahead -- its pieces issued here (chunk_sync) or by the chunk's MFMAs
   // (chunk_sync_deferred + Spread: every piece of a refill within the chunk that set it, so the vmcnt count holds)
   __device__ __forceinline__ lds_cptr chunk_sync() {
-    wait_vmcnt<(R - 2) * PPW>();
-    lds_barrier();
+    ring_vmcnt<(R - 2) * PPW>();
+    ring_barrier();
     ring_issue();
     const char* slot = lds + RING + s_read * CHUNK;
     s_read = s_read + 1 == R ? 0 : s_read + 1;
     return (lds_cptr)(slot + lane * 16);
   }
   __device__ __forceinline__ lds_cptr chunk_sync_deferred() {
-    wait_vmcnt<(R - 2) * PPW>();
-    lds_barrier();
+    ring_vmcnt<(R - 2) * PPW>();
+    ring_barrier();
     ring_target();
     const char* slot = lds + RING + s_read * CHUNK;
     s_read = s_read + 1 == R ? 0 : s_read + 1;
@@ -152,8 +167,8 @@ struct Eng {
   u32x4 nxa0, nxa1;  // and its unit 1 pair (FPF = 2)
   __device__ __forceinline__ void start_mid() {
     for (int q = 0; q < R - 1; ++q) ring_issue();
-    wait_vmcnt<(R - 2) * PPW>();
-    lds_barrier();
+    ring_vmcnt<(R - 2) * PPW>();
+    ring_barrier();
     const lds_cptr b0 = (lds_cptr)(lds + RING + lane * 16);
     nxt0 = x3::lds_rd<0>(b0);
     nxt1 = x3::lds_rd<1024>(b0);
@@ -205,8 +220,8 @@ __device__ __forceinline__ void mid_units(Eng& e, lds_cptr base, lds_cptr nbase,
     acc[t] = mfma16(fa[S][1], Hh[q], acc[t]);
     acc[t] = mfma16(fa[S][0], Hh[q], acc[t]);
     if constexpr (U == MIDU) {  // own pieces of chunk c + 1 landed (chunk c + 2's younger), then everyone's
-      wait_vmcnt<PPW>();
-      lds_barrier();
+      ring_vmcnt<PPW>();
+      ring_barrier();
       e.ring_target();  // chunk c - 1's slot: every wave has passed its last read
     }
     if constexpr (U > MIDU) mid_pieces<NU, U>(e);
@@ -660,7 +675,7 @@ __global__ void __launch_bounds__(NW * 64, 1) dps_x3_kernel(DpsX3Params p) {
     }
   }
   wait_vmcnt<0>();  // the prefetched chunks of a step that never ran land before the workgroup exits
-  x3::report_range((oor || range_bad(vmax)) && valid, p.err, lane);
+  if constexpr (DDIAG == 0) x3::report_range((oor || range_bad(vmax)) && valid, p.err, lane);
   if (valid && g == 0) {
     float* dst = p.x_out + ((size_t)yi * p.n_chains + c_local) * 3;
 #pragma unroll
