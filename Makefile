@@ -47,7 +47,7 @@ $(CSRC)/dmip_f32_%.o: $(CSRC)/dmip_f32_%.hip $(CSRC)/dmip_f32.h $(HDRS)
 $(CSRC)/dmip_x3.o: $(CSRC)/dmip_x3.hip $(CSRC)/dmip_x3.h $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -fno-slp-vectorize -c $< -o $@
 
-$(CSRC)/dmip_x3_%.o: $(CSRC)/dmip_x3_%.hip $(CSRC)/dmip_x3.h $(HDRS)
+$(CSRC)/dmip_x3_%.o: $(CSRC)/dmip_x3_%.hip $(CSRC)/dmip_x3.h $(CSRC)/dmip_x3s.h $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -fno-slp-vectorize -c $< -o $@
 
 # the k-major multi-tile fp32x3 CDE engine (width 256): its own header
@@ -73,7 +73,7 @@ $(PKG)/libdmip.so: $(OBJS)
 DIAG_DIR := abv/diag
 DIAG_SRCS := dmip_x3_cde dmip_x3k dmip_capi
 diag: $(DIAG_DIR)/libdmip_diag.so
-$(DIAG_DIR)/%_diag.o: $(CSRC)/%.hip $(CSRC)/dmip_x3k.h $(CSRC)/dmip_x3.h $(HDRS)
+$(DIAG_DIR)/%_diag.o: $(CSRC)/%.hip $(CSRC)/dmip_x3k.h $(CSRC)/dmip_x3.h $(CSRC)/dmip_x3s.h $(HDRS)
 	@mkdir -p $(DIAG_DIR)
 	$(HIPCC) $(HIPFLAGS) -fno-slp-vectorize -DDMIP_DIAG -c $< -o $@
 X3P_DIAG ?=

@@ -1,5 +1,6 @@
 // fp32-accurate split-fp16 sampler instantiations: SAMPLER_CDE (dmip_x3.h).
 #include "dmip_x3.h"
+#include "dmip_x3s.h"
 
 #include <cstdlib>
 
@@ -29,6 +30,10 @@ hipError_t launch_x3_sampler_cde(const X3SamplerParams& p, int width, int xdim, 
     }
   }
 #endif
+  if (width == 64 && x3s_eligible(p, n_y)) {  // the latency engine (dmip_x3s.h)
+    if (xdim == 2) return launch_x3s_sampler<2>(p, n_y, st);
+    if (xdim == 3) return launch_x3s_sampler<3>(p, n_y, st);
+  }
 #define X(Wv, Dv) \
   if (width == Wv && xdim == Dv) return launch_x3_sampler_n<SAMPLER_CDE, Wv, Dv, 0>(p, n_y, st);
   X(64, 2) X(128, 2) X(256, 2) X(512, 2) X(64, 3) X(128, 3) X(256, 3) X(512, 3)

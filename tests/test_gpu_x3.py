@@ -164,6 +164,45 @@ def test_x3_cdiffe_scat_width512_runs_fp32x3(dmip):
     assert est._fused_precision(PREC, dmip._lib.DMIP_SAMPLER_CDIFFE, 512, 3, 3, 23) == PREC
 
 
+# ------------------------------------------------------- the width-64 latency engine (dmip_x3s.h, round 6)
+@pytest.mark.parametrize("NL", [1, 2, 3])
+@pytest.mark.parametrize("xd,yd", [(2, 2), (3, 23)])
+def test_x3_latency_engine_bit_identical_to_one_tile_engine(dmip, monkeypatch, NL, xd, yd):
+    """Small CDE launches at width 64 run one tile per four-wave workgroup (dmip_x3s.h); every value is formed as in
+    the one-tile engine, so the samples, a sharded run and the snapshots are bit-identical to it (DMIP_X3_SPLIT=0)."""
+    torch.manual_seed(64 + NL + xd)
+    m = dmip.CDE(xd, yd, [64] * NL)
+    ys = torch.from_numpy(np.random.default_rng(NL).uniform(0, 1, (2, yd)).astype(np.float32)).to(DEV)
+    n, S, seed = 1000, 40, 21
+    a = m.sample_device(ys, n, S, seed=seed, precision=PREC)
+    xa, sa = m.sample_trajectory(ys, 333, S, 8, seed=seed, chain_offset=101, precision=PREC)
+    monkeypatch.setenv("DMIP_X3_SPLIT", "0")
+    b = m.sample_device(ys, n, S, seed=seed, precision=PREC)
+    xb, sb = m.sample_trajectory(ys, 333, S, 8, seed=seed, chain_offset=101, precision=PREC)
+    monkeypatch.delenv("DMIP_X3_SPLIT")
+    assert torch.isfinite(a).all()
+    assert torch.equal(a, b)
+    assert torch.equal(xa, xb) and torch.equal(sa, sb)
+    assert torch.equal(xa, a[:, 101:434])
+
+
+def test_x3_latency_engine_injected_noise_bit_identical(dmip, golden, monkeypatch):
+    """The reference's own x0 and per-step noise (G3, linear fixture) through both width-64 engines."""
+    tr = golden("traj_lin.npz")
+    m = _cde(dmip, "lin", golden("ckpt_lin.npz"))
+    S = int(tr["num_steps"])
+    noise = torch.from_numpy(np.concatenate([tr["x0"][None], tr["xi"]], 0)[:, None]).to(DEV)
+    n = tr["x0"].shape[0]
+    y = torch.from_numpy(tr["y"]).to(DEV)
+    a = m.sample_device(y, n, S, noise=noise, precision=PREC)
+    monkeypatch.setenv("DMIP_X3_SPLIT", "0")
+    b = m.sample_device(y, n, S, noise=noise, precision=PREC)
+    monkeypatch.delenv("DMIP_X3_SPLIT")
+    assert torch.equal(a, b)
+    print(f"\n[x3s] G3 lin through the latency engine: {n} chains, max err / max|x| = "
+          f"{_rel(a[0].cpu().numpy(), tr['x_final']):.3e}")
+
+
 # ------------------------------------------------------- the two fp32 engines over a long trajectory
 @pytest.mark.parametrize("tag", ["lin", "scat"])
 def test_x3_matches_exact_f32_engine_over_1000_steps(dmip, golden, tag):
