@@ -111,6 +111,19 @@ unsigned* status_word(int dev) {
   return g_status[dev];
 }
 
+// a pinned host mirror of the status word: dmip_device_status copies the word into it on the stream and synchronises
+// once (round 6; before, a stream synchronise and then a blocking 4-byte hipMemcpy: two round trips per read)
+unsigned* g_status_host[dmip::kMaxDevices] = {};
+unsigned* status_host(int dev) {
+  if (dev < 0 || dev >= dmip::kMaxDevices) return nullptr;
+  std::lock_guard<std::mutex> lk(g_status_mu);
+  if (!g_status_host[dev]) {
+    unsigned* h = nullptr;
+    if (hipHostMalloc((void**)&h, sizeof(unsigned), hipHostMallocDefault) == hipSuccess) g_status_host[dev] = h;
+  }
+  return g_status_host[dev];
+}
+
 // test hook (not ABI): DMIP_DEBUG_NO_HANDOVER=1 makes the balanced sampler's producers never publish
 // their hand-over, with a short spin bound, so the consumer's timeout path runs
 int debug_no_handover() {
@@ -598,12 +611,21 @@ const char* dmip_last_error(void) { return g_err.c_str(); }
 
 int dmip_device_status(void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  hipError_t e = hipStreamSynchronize(st);
-  if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
-  unsigned* w = status_word(dmip::stream_device(st));
+  const int dev = dmip::stream_device(st);
+  unsigned* w = status_word(dev);
   if (!w) return fail(DMIP_ERR_ALLOC, "device status word");
+  unsigned* h = status_host(dev);
+  hipError_t e = hipSuccess;
   unsigned v = 0;
-  if ((e = hipMemcpy(&v, w, sizeof(unsigned), hipMemcpyDeviceToHost)) != hipSuccess) return hip_fail(e, "hipMemcpy");
+  if (h) {  // the word's copy ordered after the stream's work, then one synchronise
+    if ((e = hipMemcpyAsync(h, w, sizeof(unsigned), hipMemcpyDeviceToHost, st)) != hipSuccess)
+      return hip_fail(e, "hipMemcpyAsync");
+    if ((e = hipStreamSynchronize(st)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+    v = *(volatile unsigned*)h;
+  } else {
+    if ((e = hipStreamSynchronize(st)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+    if ((e = hipMemcpy(&v, w, sizeof(unsigned), hipMemcpyDeviceToHost)) != hipSuccess) return hip_fail(e, "hipMemcpy");
+  }
   if (v == 0) return DMIP_OK;
   (void)hipMemset(w, 0, sizeof(unsigned));
   if (v == dmip::kErrHandover)
