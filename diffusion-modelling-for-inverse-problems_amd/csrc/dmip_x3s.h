@@ -13,7 +13,8 @@
 //
 // Every value is formed exactly as in the one-tile engine (the same fragments, MFMA order, activations, splits,
 // EM update and RNG), so the two engines' samples are bit-identical (tests/test_gpu_x3.py); no hand-over or balanced
-// schedule is needed, since a launch has at most kMaxTiles tiles, one per workgroup.
+// schedule is needed, since a launch has at most kMaxTiles tiles, one per workgroup. (Computing all four layer-1
+// tiles in every wave instead of exchanging them was measured slower: 0.375 vs 0.340 ms per config-1 call.)
 #pragma once
 #include <cstdlib>
 
