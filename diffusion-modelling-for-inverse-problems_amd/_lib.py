@@ -292,6 +292,7 @@ def mlp_forward(handle, x, y, t, out, y_stride, t_stride, precision="fp32"):
 def em_sample(handle, sde, y, n_chains, chain_offset, num_steps, mean, std, seed, out, noise=None,
               precision="fp16"):
     calls["em_sample"] += 1
+    _status_pending.add(_dev_index(y.device))
     n_y, ydim = y.shape
     check(lib().dmip_em_sample(handle.h, ctypes.byref(sde), ptr(y), n_y, ydim, handle.xdim,
                                int(n_chains), int(chain_offset), int(num_steps), float(mean),
@@ -302,6 +303,7 @@ def em_sample(handle, sde, y, n_chains, chain_offset, num_steps, mean, std, seed
 def em_sample_posterior(prior, likelihood, sde, y, n_chains, chain_offset, num_steps, mean, std, seed, out,
                         precision="fp16"):
     calls["em_sample_posterior"] += 1
+    _status_pending.add(_dev_index(y.device))
     n_y, ydim = y.shape
     check(lib().dmip_em_sample_posterior(prior.h, likelihood.h, ctypes.byref(sde), ptr(y), n_y, ydim,
                                          likelihood.xdim, int(n_chains), int(chain_offset), int(num_steps),
@@ -312,6 +314,7 @@ def em_sample_posterior(prior, likelihood, sde, y, n_chains, chain_offset, num_s
 def em_sample_cdiffe(handle, sde, y, n_chains, chain_offset, num_steps, mean, std, seed, out, corrector_steps=0,
                      snr=0.16, precision="fp16"):
     calls["em_sample_cdiffe"] += 1
+    _status_pending.add(_dev_index(y.device))
     n_y, ydim = y.shape
     check(lib().dmip_em_sample_cdiffe(handle.h, ctypes.byref(sde), ptr(y), n_y, ydim, handle.xdim,
                                       int(n_chains), int(chain_offset), int(num_steps), float(mean), float(std),
@@ -324,6 +327,7 @@ def em_sample_snapshots(mode, net, prior, sde, y, n_chains, chain_offset, num_st
     """dmip_em_sample_snapshots: the fused sampler of `mode` that also writes x after every
     snapshot_every-th step into snaps [num_steps // snapshot_every][n_y][n_chains][xdim]."""
     calls["em_sample_snapshots"] = calls.get("em_sample_snapshots", 0) + 1
+    _status_pending.add(_dev_index(y.device))
     n_y, ydim = y.shape
     check(lib().dmip_em_sample_snapshots(int(mode), net.h, prior.h if prior is not None else None, ctypes.byref(sde),
                                          ptr(y), n_y, ydim, net.xdim, int(n_chains), int(chain_offset),
@@ -337,11 +341,24 @@ def sampler_supported(width, n_hidden, xdim, ydim=0, mode=DMIP_SAMPLER_CDE, prec
     return bool(lib().dmip_sampler_supported_precision(precision_code(precision), mode, width, n_hidden, xdim, ydim))
 
 
+# devices with a launch of a status-writing kernel (the samplers, MH, DPS) whose status word has not been read since;
+# clear_range_status skips the read (a stream synchronise and a copy) when there is none
+_status_pending = set()
+
+
+def _dev_index(device):
+    d = torch.device(device)
+    return d.index if d.index is not None else torch.cuda.current_device()
+
+
 def device_status(device):
     """Synchronise the device's current stream and raise if a kernel reported an asynchronous failure
     (dmip_device_status: the balanced sampler's hand-over timeout, or an fp32x3 chain outside the fp16 range).
     Reading clears the status word."""
-    check(lib().dmip_device_status(stream_of(device)))
+    try:
+        check(lib().dmip_device_status(stream_of(device)))
+    finally:
+        _status_pending.discard(_dev_index(device))
 
 
 def is_range_error(e):
@@ -351,7 +368,10 @@ def is_range_error(e):
 
 def clear_range_status(device):
     """Read and clear the device status word before a launch whose range report will be read: a stale fp16-range
-    report of an earlier launch (whose caller did not read it) is dropped; any other stale failure raises."""
+    report of an earlier launch (whose caller did not read it) is dropped; any other stale failure raises. Nothing to
+    read (no status-writing launch of this process since the last read): returns at once."""
+    if _dev_index(device) not in _status_pending:
+        return
     try:
         device_status(device)
     except RuntimeError as e:
@@ -450,6 +470,7 @@ def mh_sample(handle, noise, y, n_chains, chain_offset, num_steps, noise_std, se
               inj_noise=None, inj_unif=None, e_out=None, precision="fp32"):
     """dmip_mh_sample_ex: "fp32" the exact-f32 kernel, "fp32x3" the split-fp16 one (dmip_dps_x3.hip mh_x3_kernel)."""
     calls["mh_sample"] = calls.get("mh_sample", 0) + 1
+    _status_pending.add(_dev_index(y.device))
     check(lib().dmip_mh_sample_ex(handle.h, ctypes.byref(noise), ptr(y), int(y.shape[0]), int(n_chains),
                                   int(chain_offset), int(num_steps), float(noise_std),
                                   ctypes.c_uint64(int(seed) & 0xFFFFFFFFFFFFFFFF), ptr(x_init), ptr(inj_noise),
@@ -461,6 +482,7 @@ def dps_sample(prior, surrogate, noise, sde, y, n_chains, chain_offset, num_step
                precision="fp32"):
     """dmip_dps_sample_ex: "fp32" the exact-f32 kernel, "fp32x3" the split-fp16 one (dmip_dps_x3.hip)."""
     calls["dps_sample"] = calls.get("dps_sample", 0) + 1
+    _status_pending.add(_dev_index(y.device))
     check(lib().dmip_dps_sample_ex(prior.h, surrogate.h, ctypes.byref(noise), ctypes.byref(sde), ptr(y),
                                    int(y.shape[0]), int(n_chains), int(chain_offset), int(num_steps), float(mean),
                                    float(std), ctypes.c_uint64(int(seed) & 0xFFFFFFFFFFFFFFFF), int(mode), float(zeta),
