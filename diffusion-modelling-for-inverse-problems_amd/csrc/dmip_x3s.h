@@ -14,7 +14,9 @@
 // Every value is formed exactly as in the one-tile engine (the same fragments, MFMA order, activations, splits,
 // EM update and RNG), so the two engines' samples are bit-identical (tests/test_gpu_x3.py); no hand-over or balanced
 // schedule is needed, since a launch has at most kMaxTiles tiles, one per workgroup. (Computing all four layer-1
-// tiles in every wave instead of exchanging them was measured slower: 0.375 vs 0.340 ms per config-1 call.)
+// tiles in every wave instead of exchanging them was measured slower: 0.375 vs 0.340 ms per config-1 call; so was
+// drawing the step's noise before the network instead of after it: 0.260-0.269 vs 0.252-0.254 ms per launch,
+// scripts/bench_x3s_kernel.py.)
 #pragma once
 #include <cstdlib>
 
