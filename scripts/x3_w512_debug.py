@@ -1,5 +1,5 @@
 # Width-512 one-tile fp32x3 CDE against the oracle (NL 1..3, xdim 2 / 3, 1 / 2 / 6 steps): which chains are wrong.
-# Debug aid of round 6 (scripts/gpu_r6_x3dbg.sh); prints one line per case.
+# Debug aid of round 6 (scripts/archive/gpu_r6_x3dbg.sh); prints one line per case.
 import importlib, os, sys
 
 import numpy as np
