@@ -31,8 +31,13 @@ using x3::mfma16;
 constexpr int W = 64, KQ = x3::Shape<W>::KQ, NWS = x3::Shape<W>::ST;  // 2 k-steps; 4 waves = 4 output tiles
 constexpr int CHUNK = x3::Shape<W>::CHUNK;                             // one 64-wide layer's 4 tiles (16 KiB)
 static_assert(KQ == 2 && NWS == 4 && x3::Shape<W>::NCH == 1, "one stream chunk per 64-wide layer");
-// launches up to this many tiles (all ys) take this engine: one workgroup per tile, <= 4 waves per SIMD
-constexpr long long kMaxTiles = 1024;
+// launches up to this many tiles (all ys) take this engine: one workgroup per tile, <= 4 waves per SIMD (at 4,096
+// tiles, 65,536 chains x 200 steps, it took 1.82-1.86 ms against the one-tile engine's 1.49-1.53: DMIP_X3S_MAX_TILES
+// A/B build, scripts/archive/gpu_r6_x3s_tiles.sh)
+#ifndef DMIP_X3S_MAX_TILES
+#define DMIP_X3S_MAX_TILES 1024
+#endif
+constexpr long long kMaxTiles = DMIP_X3S_MAX_TILES;
 
 __device__ __forceinline__ u32x4 ld16(const char* p) { return *(const u32x4*)p; }
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *(const f32x4*)p; }
