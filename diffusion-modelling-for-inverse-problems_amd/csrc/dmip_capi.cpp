@@ -1046,7 +1046,13 @@ static int em_sample_x3(int mode, const dmip_mlp* net0, const dmip_mlp* net1, co
   if (net1) p.net[1] = dmip::X3Net{net1->x3_l1, net1->x3_stream, net1->x3_bias};
   p.n_hidden = net0->n_hidden;
   float* bias_y = nullptr;
-  if (mode != DMIP_SAMPLER_CDIFFE) {
+  if (dmip::x3s_sampler_eligible(mode, net0->width, net0->n_hidden, xdim, a.n_chains, a.n_y)) {
+    // the width-64 latency engine forms the per-y bias itself (round 6: one launch and one allocation fewer)
+    p.l1w = net0->w1;
+    p.l1b = net0->b1;
+    p.l1_in = net0->in_dim;
+    p.ydim = ydim;
+  } else if (mode != DMIP_SAMPLER_CDIFFE) {
     // y is constant per y index: c (b1 + W1_y y) becomes layer 1's per-y bias (f64 prep)
     hipError_t e = hipMallocAsync((void**)&bias_y, (size_t)a.n_y * net0->width * sizeof(float), st);
     if (e != hipSuccess) return fail(DMIP_ERR_ALLOC, std::string("hipMallocAsync: ") + hipGetErrorString(e));

@@ -339,7 +339,15 @@ struct X3SamplerParams {
   unsigned int spin_limit;
   int debug_flags;
   const float* coef;          // x3k: per-step (tau, beta, g, 0) [num_steps][4] of step_coef (its launch fills it)
+  // the width-64 latency engine (dmip_x3s.h) with bias_y null: layer 1's per-y bias from W1 [W][l1_in], b1 and y_obs
+  // [n_y][ydim] in the kernel, as x3_bias_prep_kernel forms it (no prep launch, no allocation)
+  const float* l1w;
+  const float* l1b;
+  int l1_in, ydim;
 };
+// the latency engine takes this launch (CDE, width 64, xdim 2 or 3, 1-3 hidden layers, <= 1,024 tiles over all ys;
+// DMIP_X3_SPLIT=0 opts out): launch_x3_sampler_cde's own test, exposed so the caller can skip the bias prep
+bool x3s_sampler_eligible(int mode, int width, int n_hidden, int xdim, long long n_chains, int n_y);
 
 struct X3BiasPrepParams {
   const float* w1;  // [width][in_dim] (nn.Linear layout)

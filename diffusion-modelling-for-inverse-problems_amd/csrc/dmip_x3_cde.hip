@@ -15,6 +15,13 @@ static int x3_diag() {
 }
 #endif
 
+bool x3s_sampler_eligible(int mode, int width, int n_hidden, int xdim, long long n_chains, int n_y) {
+  X3SamplerParams q{};
+  q.n_chains = n_chains;
+  q.n_hidden = n_hidden;
+  return mode == SAMPLER_CDE && width == 64 && (xdim == 2 || xdim == 3) && x3s_eligible(q, n_y);
+}
+
 hipError_t launch_x3_sampler_cde(const X3SamplerParams& p, int width, int xdim, int n_y, hipStream_t st, bool* ok) {
   *ok = true;
 #ifdef DMIP_DIAG
@@ -34,6 +41,7 @@ hipError_t launch_x3_sampler_cde(const X3SamplerParams& p, int width, int xdim, 
     if (xdim == 2) return launch_x3s_sampler<2>(p, n_y, st);
     if (xdim == 3) return launch_x3s_sampler<3>(p, n_y, st);
   }
+  if (!p.bias_y) return hipErrorInvalidValue;  // (a caller that skipped the bias prep for the latency engine)
 #define X(Wv, Dv) \
   if (width == Wv && xdim == Dv) return launch_x3_sampler_n<SAMPLER_CDE, Wv, Dv, 0>(p, n_y, st);
   X(64, 2) X(128, 2) X(256, 2) X(512, 2) X(64, 3) X(128, 3) X(256, 3) X(512, 3)

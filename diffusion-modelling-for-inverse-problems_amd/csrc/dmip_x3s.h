@@ -113,7 +113,19 @@ __global__ void __launch_bounds__(NWS * 64) x3s_sampler_kernel(X3SamplerParams p
   for (int q = 0; q < KQ; ++q)
 #pragma unroll
     for (int s = 0; s < 2; ++s) fo[q][s] = ld16(p.net[0].stream + (size_t)(nl - 1) * CHUNK + (2 * q + s) * 1024 + lane * 16);
-  const f32x4 b1 = ld4(p.bias_y + (size_t)yi * W + 16 * w + 4 * g);
+  f32x4 b1;
+  if (p.bias_y) {
+    b1 = ld4(p.bias_y + (size_t)yi * W + 16 * w + 4 * g);
+  } else {  // c (b1 + W1_y y) of this lane's 4 units, in f64 as x3_bias_prep_kernel (dmip_x3.hip) forms it
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int u = 16 * w + 4 * g + r;
+      const float* wrow = p.l1w + (size_t)u * p.l1_in;
+      double c = p.l1b[u];
+      for (int m = 0; m < p.ydim; ++m) c += (double)wrow[D + m] * (double)p.y_obs[(size_t)yi * p.ydim + m];
+      b1[r] = (float)((double)kTanhScale * c);
+    }
+  }
   const f32x4 bo = ld4(p.net[0].bias + nl * W + 4 * g);
 
   const int S = p.num_steps;
@@ -197,6 +209,7 @@ inline bool x3s_eligible(const X3SamplerParams& p, int n_y) {
   const long long tiles = (p.n_chains + 15) / 16;
   return p.n_hidden >= 1 && p.n_hidden <= 3 && tiles >= 1 && tiles * (n_y > 0 ? n_y : 1) <= x3s::kMaxTiles;
 }
+// (launch_x3_sampler_cde takes the latency engine exactly when this holds, x3s_sampler_eligible below)
 
 template <int D>
 inline hipError_t launch_x3s_sampler(const X3SamplerParams& p, int n_y, hipStream_t st) {
