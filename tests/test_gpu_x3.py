@@ -186,6 +186,20 @@ def test_x3_latency_engine_bit_identical_to_one_tile_engine(dmip, monkeypatch, N
     assert torch.equal(xa, a[:, 101:434])
 
 
+@pytest.mark.parametrize("n", [1, 17, 16 * 1024, 16 * 1024 + 1])
+def test_x3_latency_engine_ragged_and_threshold_counts(dmip, monkeypatch, n):
+    """Ragged tiles (1 and 17 chains) and the engine threshold (1,024 tiles run on the latency engine, one chain more
+    on the one-tile engine): every count gives the one-tile engine's samples bit for bit."""
+    torch.manual_seed(5)
+    m = dmip.CDE(2, 2, [64] * 3)
+    y = torch.tensor([0.3, 0.7], device=DEV)
+    a = m.sample_device(y, n, 12, seed=3, precision=PREC)
+    monkeypatch.setenv("DMIP_X3_SPLIT", "0")
+    b = m.sample_device(y, n, 12, seed=3, precision=PREC)
+    monkeypatch.delenv("DMIP_X3_SPLIT")
+    assert torch.isfinite(a).all() and torch.equal(a, b)
+
+
 def test_x3_latency_engine_injected_noise_bit_identical(dmip, golden, monkeypatch):
     """The reference's own x0 and per-step noise (G3, linear fixture) through both width-64 engines."""
     tr = golden("traj_lin.npz")
