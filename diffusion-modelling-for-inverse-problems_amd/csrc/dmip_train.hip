@@ -271,6 +271,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rec_rsrc(uint32_t* rec, long l
                                            NL * kTrainRecTileBytes, 0x00020000);
 }
 constexpr int rec_off(int li, int Rp, int q) { return ((li * 2 + Rp) * kTrainRecQ + q) * 1024; }
+// cache policy of the record stores (A/B knob DMIP_TRAIN_REC_AUX; 0 = default)
+#ifndef DMIP_TRAIN_REC_AUX
+#define DMIP_TRAIN_REC_AUX 0
+#endif
+constexpr int kRecAux = DMIP_TRAIN_REC_AUX;
 
 // row tile R's coefficients (q 3..5): each R's 8-byte half at once (holds nothing across R; storing each value pair
 // as soon as it exists, or full 16-byte pieces at odd R, measured more spills)
@@ -279,17 +284,17 @@ __device__ __forceinline__ void rec_put_coef(__amdgpu_buffer_rsrc_t rr, int li, 
                                              const float (&b)[4], const float (&d1c)[4]) {
   const int vo = lane * 16 + (R & 1) * 8;
   __builtin_amdgcn_raw_buffer_store_b64(u32x2{pk_f16(d1[0], d1[1]), pk_f16(d1[2], d1[3])}, rr, vo,
-                                        rec_off(li, R >> 1, 3), 0);
+                                        rec_off(li, R >> 1, 3), kRecAux);
   __builtin_amdgcn_raw_buffer_store_b64(u32x2{pk_bf16(b[0], b[1]), pk_bf16(b[2], b[3])}, rr, vo,
-                                        rec_off(li, R >> 1, 4), 0);
+                                        rec_off(li, R >> 1, 4), kRecAux);
   __builtin_amdgcn_raw_buffer_store_b64(u32x2{pk_f16(d1c[0], d1c[1]), pk_f16(d1c[2], d1c[3])}, rr, vo,
-                                        rec_off(li, R >> 1, 5), 0);
+                                        rec_off(li, R >> 1, 5), kRecAux);
 }
 template <int NL>
 __device__ __forceinline__ void rec_put_h(__amdgpu_buffer_rsrc_t rr, int li, int Rp, int lane, const bf16x8 (&h)[3][2]) {
 #pragma unroll
   for (int q = 0; q < 3; ++q)
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, h[q][Rp]), rr, lane * 16, rec_off(li, Rp, q), 0);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, h[q][Rp]), rr, lane * 16, rec_off(li, Rp, q), kRecAux);
 }
 
 // The shared part of the LDS image (weight fragments, biases, layer-1 columns), packed ONCE per
@@ -589,7 +594,11 @@ __global__ void __launch_bounds__((TL<NL, PH>::NW * 64), (PH == 1 ? 2 : 1)) loss
     float aS[NSTREAM][OUT];
     {
       // the record reverse half's input (PH 1 with p.rec; a uniform branch per layer)
+#ifdef DMIP_TRAIN_TIMING_NO_REC_STORE
+      const bool recw = false;  // timing ablation only (A/B builds): the forward half writes no records
+#else
       const bool recw = PH == 1 && p.rec != nullptr;
+#endif
       const __amdgpu_buffer_rsrc_t rr = rec_rsrc<NL>(recw ? p.rec : (uint32_t*)p.adj, tile);
       bf16x8 H[NSTREAM][2], HL[3][2];  // HL: lo residuals of the split streams P, V, C
 #pragma unroll
